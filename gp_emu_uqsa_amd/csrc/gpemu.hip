@@ -1,0 +1,1275 @@
+// gpemu.hip -- host side of libgpemu.so: context, HBM buffers, launch schedule
+// and the C-ABI declared in include/gpemu.h.
+//
+// One objective evaluation (gp4ml / MUCM, value + gradient) runs as:
+//   scale points -> K-build (lower tiles) -> right-looking blocked Cholesky
+//   (per 128-column step: diagonal-block factor+inverse, panel GEMM, trailing
+//   SYRK GEMM) -> recursive triangular inverse (grouped GEMM per level) ->
+//   [f H] skinny solve + Gram -> host q x q algebra -> A^-1 = L^-T L^-1 (one
+//   grouped GEMM) -> [alpha, W] skinny product -> fused gradient contraction.
+// See DESIGN.md for the flop / byte accounting of each step.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gpemu.h"
+#include "gpemu_kernels.hpp"
+
+using namespace gpe;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+constexpr int MAX_PROBS = 1 << 16;
+constexpr int AUX_DESC_BASE = 1 << 15;
+constexpr int ADHOC_DESC_BASE = MAX_PROBS - 64;
+
+struct Launch {       // one grouped GEMM launch of the cached schedule
+  int kind;           // 0: <0,0>, 1: <1,0>, 2: <1,1>, 3: <0,1>
+  int first, count;   // descriptor range
+  int tiles;
+  double flops;       // algorithmic flops
+};
+
+struct Plan {
+  long long n_pad = 0;
+  const double* a_ptr = nullptr;   // buffers the descriptors point into
+  const double* b_ptr = nullptr;
+  // potrf: per step kt the panel launch and the syrk launch (index into launches or -1)
+  std::vector<int> panel, syrk;
+  std::vector<int> trtri;   // launches in order
+  int lauum = -1;
+  std::vector<Launch> launches;
+  std::vector<GemmProb> probs;
+};
+
+// A factorisation workspace: two n_pad x n_pad buffers and their GEMM schedule.
+struct Fact {
+  long long n_pad = 0;
+  int NB = 0;
+  double* A = nullptr;   // K-build -> L -> A^-1
+  double* B = nullptr;   // Dinv tiles -> L^-1 (strictly-upper tiles: scratch)
+  size_t cap = 0;
+  double* logdet = nullptr;  // NB per-block log-determinant parts
+  int desc_base = 0;         // first slot of its descriptors in the device array
+  Plan plan;
+};
+
+}  // namespace
+
+struct gpe_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+
+  long long n = 0, n_pad = 0;
+  int d = 0, q = 0, NB = 0;
+  bool has_r = false;
+
+  double* dX = nullptr;      // n_pad x d row-major (raw)
+  double* dXw = nullptr;     // scaled by 1/delta
+  double* dF = nullptr;      // n_pad x (q+1) col-major: [f H]
+  double* dr = nullptr;      // n_pad
+  Fact tr;                   // training matrix workspace
+  Fact aux;                  // gpe_cholesky workspace
+
+  int* dinfo = nullptr;
+  double* dinvdelta = nullptr;
+  double* dZ = nullptr;      // n_pad x SK_PMAX
+  double* dR2 = nullptr;     // n_pad x SK_PMAX
+  double* dWa = nullptr;     // n_pad x SK_PMAX
+  double* dskp = nullptr;    // skinny partials
+  size_t skp_cap = 0;
+  double* dgpart = nullptr;  // gram partials
+  double* dgram = nullptr;   // SK_PMAX^2
+  double* dT2 = nullptr;     // SK_PMAX^2
+  double* dcpart = nullptr;  // contraction partials
+  size_t cpart_cap = 0;
+  double* dcsum = nullptr;   // d+2
+  GemmProb* dprobs = nullptr;
+
+  // posterior workspace
+  double* dW1 = nullptr;
+  double* dW2 = nullptr;
+  size_t w_cap = 0;
+  double* dW3 = nullptr;     // full posterior covariance
+  size_t w3_cap = 0;
+  double* dXs = nullptr;
+  double* dXsw = nullptr;
+  size_t xs_cap = 0;
+  double* dsmall = nullptr;  // generic small device scratch
+  size_t small_cap = 0;
+
+  // pinned host staging
+  double* hpin = nullptr;
+  size_t hpin_cap = 0;
+
+  // resident factor (gpe_factor)
+  bool factor_valid = false;
+  int f_kernel = 0;
+  std::vector<double> f_delta;
+  double f_nu = 0.0;
+
+  // profiling
+  bool prof = false;
+  hipEvent_t ev[16] = {};
+  std::vector<hipEvent_t> gev;  // pairs around GEMM launches
+  double phase_ms[8] = {0};
+  double gemm_ms = 0.0, gemm_launches = 0.0, gemm_flops = 0.0;
+};
+
+namespace {
+
+#define HIPCHK(ctx, expr)                                                          \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) {                                                        \
+      (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);              \
+      return GPE_ERR_HIP;                                                          \
+    }                                                                              \
+  } while (0)
+
+#define CHK(expr)                    \
+  do {                               \
+    int rc_ = (expr);                \
+    if (rc_ != GPE_OK) return rc_;   \
+  } while (0)
+
+int fail(gpe_ctx* c, int code, const std::string& msg) {
+  c->err = msg;
+  return code;
+}
+
+template <typename T>
+int dalloc(gpe_ctx* c, T** p, size_t count) {
+  if (*p) {
+    (void)hipFree(*p);
+    *p = nullptr;
+  }
+  if (count == 0) return GPE_OK;
+  hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return fail(c, GPE_ERR_ALLOC, std::string("hipMalloc failed: ") + hipGetErrorString(e) +
+                                      " (" + std::to_string(count * sizeof(T)) + " bytes)");
+  }
+  return GPE_OK;
+}
+
+int ensure_pinned(gpe_ctx* c, size_t doubles) {
+  if (doubles <= c->hpin_cap) return GPE_OK;
+  if (c->hpin) hipHostFree(c->hpin);
+  c->hpin = nullptr;
+  size_t cap = std::max<size_t>(doubles, 1 << 16);
+  HIPCHK(c, hipHostMalloc((void**)&c->hpin, cap * sizeof(double), hipHostMallocDefault));
+  c->hpin_cap = cap;
+  return GPE_OK;
+}
+
+int ensure_small(gpe_ctx* c, size_t doubles) {
+  if (doubles <= c->small_cap) return GPE_OK;
+  CHK(dalloc(c, &c->dsmall, doubles));
+  c->small_cap = doubles;
+  return GPE_OK;
+}
+
+inline int pmax_bucket(int P) { return P <= 8 ? 8 : (P <= 16 ? 16 : 32); }
+
+// ------------------------------------------------------------------ launches
+int launch_pairs(gpe_ctx* c, const PairArgs& a, int nblocks) {
+  const int dm = a.d <= 4 ? 4 : a.d <= 8 ? 8 : a.d <= 16 ? 16 : 32;
+  switch (dm) {
+    case 4: hipLaunchKernelGGL(k_pairs<4>, dim3(nblocks), dim3(256), 0, c->stream, a); break;
+    case 8: hipLaunchKernelGGL(k_pairs<8>, dim3(nblocks), dim3(256), 0, c->stream, a); break;
+    case 16: hipLaunchKernelGGL(k_pairs<16>, dim3(nblocks), dim3(256), 0, c->stream, a); break;
+    default: hipLaunchKernelGGL(k_pairs<32>, dim3(nblocks), dim3(256), 0, c->stream, a); break;
+  }
+  HIPCHK(c, hipGetLastError());
+  return GPE_OK;
+}
+
+int launch_gemm_range(gpe_ctx* c, const Launch& L) {
+  const size_t lds = G_LDS_DOUBLES * sizeof(double);
+  const GemmProb* pr = c->dprobs + L.first;
+  if (c->prof) {
+    hipEvent_t e0, e1;
+    HIPCHK(c, hipEventCreate(&e0));
+    HIPCHK(c, hipEventCreate(&e1));
+    c->gev.push_back(e0);
+    c->gev.push_back(e1);
+    HIPCHK(c, hipEventRecord(e0, c->stream));
+  }
+  switch (L.kind) {
+    case 0: hipLaunchKernelGGL((k_gemm<false, false>), dim3(L.tiles), dim3(256), lds, c->stream, pr, L.count, c->dinfo); break;
+    case 1: hipLaunchKernelGGL((k_gemm<true, false>), dim3(L.tiles), dim3(256), lds, c->stream, pr, L.count, c->dinfo); break;
+    case 2: hipLaunchKernelGGL((k_gemm<true, true>), dim3(L.tiles), dim3(256), lds, c->stream, pr, L.count, c->dinfo); break;
+    default: hipLaunchKernelGGL((k_gemm<false, true>), dim3(L.tiles), dim3(256), lds, c->stream, pr, L.count, c->dinfo); break;
+  }
+  HIPCHK(c, hipGetLastError());
+  if (c->prof) {
+    HIPCHK(c, hipEventRecord(c->gev.back(), c->stream));
+    c->gemm_launches += 1.0;
+    c->gemm_flops += L.flops;
+  }
+  return GPE_OK;
+}
+
+// tiles of a problem
+int prob_tiles(const GemmProb& p) {
+  return (p.flags & G_CLOWER) ? p.mt * (p.mt + 1) / 2 : p.mt * p.nt;
+}
+
+void add_launch(Plan& pl, int kind, std::vector<GemmProb> probs, double flops) {
+  Launch L;
+  L.kind = kind;
+  L.first = (int)pl.probs.size();
+  L.count = (int)probs.size();
+  int t = 0;
+  for (auto& p : probs) {
+    p.tile_begin = t;
+    p.ntiles = prob_tiles(p);
+    t += p.ntiles;
+    pl.probs.push_back(p);
+  }
+  L.tiles = t;
+  L.flops = flops;
+  pl.launches.push_back(L);
+}
+
+GemmProb mkprob(const double* A, long long lda, const double* B, long long ldb, double* C,
+                long long ldc, int mt, int nt, int K, int flags, double alpha, double beta) {
+  GemmProb p;
+  p.A = A; p.B = B; p.C = C;
+  p.lda = lda; p.ldb = ldb; p.ldc = ldc;
+  p.mt = mt; p.nt = nt; p.K = K; p.flags = flags;
+  p.alpha = alpha; p.beta = beta;
+  p.tile_begin = 0; p.ntiles = 0;
+  return p;
+}
+
+// Build the (n_pad-dependent, data-independent) GEMM schedule and upload it.
+int build_plan(gpe_ctx* c, Fact& F) {
+  Plan& pl = F.plan;
+  if (pl.n_pad == F.n_pad && pl.a_ptr == F.A && pl.b_ptr == F.B && !pl.launches.empty()) return GPE_OK;
+  pl = Plan();
+  pl.n_pad = F.n_pad;
+  pl.a_ptr = F.A;
+  pl.b_ptr = F.B;
+  const long long ld = F.n_pad;
+  const int NB = F.NB;
+  const double T = TILE;
+  double* A = F.A;
+  double* B = F.B;
+  auto tile = [&](double* M, int i, int j) { return M + (long long)i * TILE + (long long)j * TILE * ld; };
+  // --- Cholesky (right-looking, 128-column steps)
+  pl.panel.assign(NB, -1);
+  pl.syrk.assign(NB, -1);
+  for (int kt = 0; kt + 1 < NB; ++kt) {
+    const int m = NB - kt - 1;
+    // L(kt+1:, kt) = A(kt+1:, kt) * Dinv_kt^T     (opB(k,n) = Dinv(n,k): N-contiguous)
+    pl.panel[kt] = (int)pl.launches.size();
+    add_launch(pl, 0,
+               {mkprob(tile(A, kt + 1, kt), ld, tile(B, kt, kt), ld, tile(A, kt + 1, kt), ld, m, 1,
+                       TILE, 0, 1.0, 0.0)},
+               (double)m * T * T * T);
+    // A(kt+1:, kt+1:) -= L(kt+1:, kt) L(kt+1:, kt)^T   (lower tiles)
+    pl.syrk[kt] = (int)pl.launches.size();
+    add_launch(pl, 0,
+               {mkprob(tile(A, kt + 1, kt), ld, tile(A, kt + 1, kt), ld, tile(A, kt + 1, kt + 1), ld,
+                       m, m, TILE, G_CLOWER, -1.0, 1.0)},
+               (double)m * T * ((double)m * T + 1.0) * T);
+  }
+  // --- triangular inverse X = L^-1 in B (diagonal tiles already hold Dinv)
+  for (int s = 2; s / 2 < NB; s *= 2) {
+    std::vector<GemmProb> pa, pb;
+    double fa = 0.0, fb = 0.0;
+    for (int t0 = 0; t0 < NB; t0 += s) {
+      const int h = t0 + s / 2;
+      if (h >= NB) continue;
+      const int t1 = std::min(t0 + s, NB);
+      const int a = h - t0, b = t1 - h;
+      // T^T (a x b tiles, stored in the upper block rows t0:h, cols h:t1 of B)
+      //   = X11^T L21^T ;  opA(m,k) = X11(k,m): K-contiguous, upper -> kbeg = ti*128
+      pa.push_back(mkprob(tile(B, t0, t0), ld, tile(A, h, t0), ld, tile(B, t0, h), ld, a, b,
+                          a * TILE, G_KBEG_TI, 1.0, 0.0));
+      fa += (double)a * T * a * T * b * T;   // triangular a x a times a x b
+      // X21 = -X22 T ;  opA = X22 lower -> kend = (ti+1)*128 ; opB(k,n) = T^T(n,k)
+      pb.push_back(mkprob(tile(B, h, h), ld, tile(B, t0, h), ld, tile(B, h, t0), ld, b, a,
+                          b * TILE, G_KEND_TI, -1.0, 0.0));
+      fb += (double)b * T * b * T * a * T;
+    }
+    if (pa.empty()) continue;
+    pl.trtri.push_back((int)pl.launches.size());
+    add_launch(pl, 1, pa, fa);
+    pl.trtri.push_back((int)pl.launches.size());
+    add_launch(pl, 0, pb, fb);
+  }
+  // --- A^-1 = X^T X (lower tiles), written over L in A
+  pl.lauum = (int)pl.launches.size();
+  {
+    const double N = (double)F.n_pad;
+    add_launch(pl, 2, {mkprob(B, ld, B, ld, A, ld, NB, NB, (int)F.n_pad, G_CLOWER | G_KBEG_TI, 1.0, 0.0)},
+               N * N * N / 3.0);
+  }
+  const int limit = (F.desc_base == 0) ? AUX_DESC_BASE : ADHOC_DESC_BASE - AUX_DESC_BASE;
+  if ((int)pl.probs.size() > limit) return fail(c, GPE_ERR_UNSUPPORTED, "GEMM schedule too large");
+  for (auto& L : pl.launches) L.first += F.desc_base;
+  HIPCHK(c, hipMemcpy(c->dprobs + F.desc_base, pl.probs.data(), pl.probs.size() * sizeof(GemmProb),
+                      hipMemcpyHostToDevice));
+  return GPE_OK;
+}
+
+// (re)allocate a workspace for an n_pad x n_pad problem
+int ensure_fact(gpe_ctx* c, Fact& F, long long n_pad) {
+  const size_t big = (size_t)n_pad * n_pad;
+  if (big > F.cap) {
+    CHK(dalloc(c, &F.A, 0));
+    CHK(dalloc(c, &F.B, 0));
+    CHK(dalloc(c, &F.A, big));
+    CHK(dalloc(c, &F.B, big));
+    F.cap = big;
+    F.plan = Plan();
+  }
+  if (F.n_pad != n_pad) {
+    F.n_pad = n_pad;
+    F.NB = (int)(n_pad / TILE);
+    CHK(dalloc(c, &F.logdet, (size_t)F.NB));
+    F.plan = Plan();
+  }
+  return GPE_OK;
+}
+
+// scaled points for the training set
+int scale_training(gpe_ctx* c, const double* delta) {
+  CHK(ensure_pinned(c, 64));
+  for (int k = 0; k < c->d; ++k) {
+    if (!(delta[k] > 0.0) && !(delta[k] < 0.0))
+      return fail(c, GPE_ERR_ARG, "delta must be non-zero");
+    c->hpin[k] = 1.0 / delta[k];
+  }
+  HIPCHK(c, hipMemcpyAsync(c->dinvdelta, c->hpin, c->d * sizeof(double), hipMemcpyHostToDevice,
+                           c->stream));
+  const long long tot = c->n_pad * c->d;
+  hipLaunchKernelGGL(k_scale_points, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
+                     c->dX, c->dinvdelta, c->d, (int)c->n, (int)c->n_pad, c->dXw);
+  HIPCHK(c, hipGetLastError());
+  return GPE_OK;
+}
+
+void kernel_consts(int kernel, double nu, bool predict, double* coff, double* cdiag) {
+  if (kernel == GPE_KERNEL_ALT_NUG) {
+    *coff = 1.0;
+    *cdiag = predict ? 1.0 + nu * nu : 1.0;
+  } else {
+    *coff = 1.0 - nu;
+    *cdiag = predict ? 1.0 : 1.0 - nu;
+  }
+}
+
+// K-build of the training matrix into dA (lower tiles)
+int kbuild(gpe_ctx* c, int kernel, double nu, double s2, double rscale) {
+  PairArgs a;
+  a.xr = c->dXw; a.xc = c->dXw; a.out = c->tr.A; a.ld = c->n_pad;
+  a.d = c->d; a.nr_valid = (int)c->n; a.nc_valid = (int)c->n;
+  a.mt = c->NB; a.nt = c->NB; a.mode = 1 | 2;
+  double coff, cdiag;
+  kernel_consts(kernel, nu, true, &coff, &cdiag);
+  a.s2 = s2; a.coff = coff; a.cdiag = cdiag;
+  a.rscale = rscale; a.r = (c->has_r && rscale != 0.0) ? c->dr : nullptr;
+  return launch_pairs(c, a, c->NB * (c->NB + 1) / 2);
+}
+
+int potrf(gpe_ctx* c, Fact& F) {
+  const Plan& pl = F.plan;
+  for (int kt = 0; kt < F.NB; ++kt) {
+    hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(DIAG_THREADS), 0, c->stream, F.A, (long long)F.n_pad,
+                       kt, F.B, (long long)F.n_pad, F.logdet, c->dinfo);
+    HIPCHK(c, hipGetLastError());
+    if (kt + 1 < F.NB) {
+      CHK(launch_gemm_range(c, pl.launches[pl.panel[kt]]));
+      CHK(launch_gemm_range(c, pl.launches[pl.syrk[kt]]));
+    }
+  }
+  return GPE_OK;
+}
+
+int trtri(gpe_ctx* c, Fact& F) {
+  for (int li : F.plan.trtri) CHK(launch_gemm_range(c, F.plan.launches[li]));
+  return GPE_OK;
+}
+
+// Y(0:n_rows, 0:P) = op(M) x R  with M lower-tiled (ld = n_pad) or full
+int skinny(gpe_ctx* c, bool transposed, const double* M, long long ldm, int ntr, int nit,
+           bool lower, const double* R, long long ldr, int P, double* Y, long long ldy) {
+  if (P > SK_PMAX) return fail(c, GPE_ERR_UNSUPPORTED, "too many right-hand sides");
+  const int nch = lower ? (std::max(ntr, nit) + SK_CH - 1) / SK_CH : (ntr + SK_CH - 1) / SK_CH;
+  const long long rows = (long long)nit * TILE;
+  const size_t need = (size_t)nch * rows * P;
+  if (need > c->skp_cap) {
+    CHK(dalloc(c, &c->dskp, need));
+    c->skp_cap = need;
+  }
+  SkinnyArgs a;
+  a.M = M; a.ldm = ldm; a.R = R; a.ldr = ldr; a.part = c->dskp; a.ldp = rows;
+  a.pstride = rows * P; a.P = P; a.ntr = ntr; a.lower = lower ? 1 : 0; a.nit = nit;
+  a.abort_flag = c->dinfo;
+  const int pm = pmax_bucket(P);
+  dim3 grid(nit * nch);
+  if (!transposed) {
+    if (pm == 8) hipLaunchKernelGGL(k_trmm_skinny_n<8>, grid, dim3(256), 0, c->stream, a);
+    else if (pm == 16) hipLaunchKernelGGL(k_trmm_skinny_n<16>, grid, dim3(256), 0, c->stream, a);
+    else hipLaunchKernelGGL(k_trmm_skinny_n<32>, grid, dim3(256), 0, c->stream, a);
+  } else {
+    if (pm == 8) hipLaunchKernelGGL(k_trmm_skinny_t<8>, grid, dim3(256), 0, c->stream, a);
+    else if (pm == 16) hipLaunchKernelGGL(k_trmm_skinny_t<16>, grid, dim3(256), 0, c->stream, a);
+    else hipLaunchKernelGGL(k_trmm_skinny_t<32>, grid, dim3(256), 0, c->stream, a);
+  }
+  HIPCHK(c, hipGetLastError());
+  const int mode = lower ? (transposed ? 1 : 0) : 2;
+  const long long tot = rows * P;
+  // partial layout is [ch][p][rows]; reduce into Y (ld = ldy >= rows)
+  if (ldy != rows) return fail(c, GPE_ERR_STATE, "skinny: output ld mismatch");
+  hipLaunchKernelGGL(k_reduce_chunks, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
+                     c->dskp, (long long)(rows * P), Y, rows, P, (int)rows, ntr, mode, c->dinfo);
+  HIPCHK(c, hipGetLastError());
+  return GPE_OK;
+}
+
+// G = Z^T Z (P x P) on the host (doubles, row-major == col-major: symmetric)
+int gram(gpe_ctx* c, const double* Z, long long ldz, int P, int nrows, double* host_out) {
+  const int nblk = (nrows + 255) / 256;
+  const size_t need = (size_t)nblk * P * P;
+  CHK(ensure_small(c, need + P * P));
+  hipLaunchKernelGGL(k_gram, dim3(nblk), dim3(256), 0, c->stream, Z, ldz, P, nrows, c->dsmall, c->dinfo);
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(k_reduce_rows, dim3(P * P), dim3(256), 0, c->stream, c->dsmall, nblk, P * P,
+                     c->dgram);
+  HIPCHK(c, hipGetLastError());
+  CHK(ensure_pinned(c, (size_t)P * P + 8));
+  HIPCHK(c, hipMemcpyAsync(c->hpin, c->dgram, (size_t)P * P * sizeof(double), hipMemcpyDeviceToHost,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::memcpy(host_out, c->hpin, (size_t)P * P * sizeof(double));
+  return GPE_OK;
+}
+
+// dense Cholesky of a small SPD matrix (row-major), false if not PD
+bool small_chol(std::vector<double>& a, int q) {
+  for (int j = 0; j < q; ++j) {
+    double s = a[j * q + j];
+    for (int k = 0; k < j; ++k) s -= a[j * q + k] * a[j * q + k];
+    if (!(s > 0.0)) return false;
+    const double dj = std::sqrt(s);
+    a[j * q + j] = dj;
+    for (int i = j + 1; i < q; ++i) {
+      double t = a[i * q + j];
+      for (int k = 0; k < j; ++k) t -= a[i * q + k] * a[j * q + k];
+      a[i * q + j] = t / dj;
+    }
+    for (int k = j + 1; k < q; ++k) a[j * q + k] = 0.0;
+  }
+  return true;
+}
+
+// solve K y = b (K lower, row-major)
+void small_fwd(const std::vector<double>& K, int q, double* b) {
+  for (int i = 0; i < q; ++i) {
+    double s = b[i];
+    for (int k = 0; k < i; ++k) s -= K[i * q + k] * b[k];
+    b[i] = s / K[i * q + i];
+  }
+}
+void small_bwd(const std::vector<double>& K, int q, double* b) {
+  for (int i = q - 1; i >= 0; --i) {
+    double s = b[i];
+    for (int k = i + 1; k < q; ++k) s -= K[k * q + i] * b[k];
+    b[i] = s / K[i * q + i];
+  }
+}
+// inverse of lower-triangular K (row-major)
+std::vector<double> small_trinv(const std::vector<double>& K, int q) {
+  std::vector<double> X((size_t)q * q, 0.0);
+  for (int c0 = 0; c0 < q; ++c0) {
+    std::vector<double> e(q, 0.0);
+    e[c0] = 1.0;
+    small_fwd(K, q, e.data());
+    for (int i = 0; i < q; ++i) X[i * q + c0] = e[i];
+  }
+  return X;
+}
+
+struct SmallAlgebra {
+  double zz = 0, quad = 0, logdetQ = 0;
+  std::vector<double> Kq, beta;  // Kq row-major lower (q x q)
+  bool ok = false;
+};
+
+SmallAlgebra small_from_gram(const std::vector<double>& G, int P) {
+  // G over [z w]: zz = G00, wz = G[1:,0], Q = G[1:,1:]
+  SmallAlgebra s;
+  const int q = P - 1;
+  s.zz = G[0];
+  std::vector<double> Q((size_t)q * q), wz(q);
+  for (int i = 0; i < q; ++i) {
+    wz[i] = G[(i + 1) * P + 0];
+    for (int j = 0; j < q; ++j) Q[i * q + j] = G[(i + 1) * P + (j + 1)];
+  }
+  if (!small_chol(Q, q)) return s;
+  s.Kq = Q;
+  s.beta = wz;
+  small_fwd(Q, q, s.beta.data());
+  small_bwd(Q, q, s.beta.data());
+  double wzB = 0.0;
+  for (int i = 0; i < q; ++i) wzB += wz[i] * s.beta[i];
+  s.quad = s.zz - wzB;
+  s.logdetQ = 0.0;
+  for (int i = 0; i < q; ++i) s.logdetQ += 2.0 * std::log(Q[i * q + i]);
+  s.ok = true;
+  return s;
+}
+
+int read_info_logdet(gpe_ctx* c, const Fact& F, int* info, double* logdetA) {
+  CHK(ensure_pinned(c, (size_t)F.NB + 8));
+  HIPCHK(c, hipMemcpyAsync(c->hpin, F.logdet, F.NB * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->hpin + F.NB, c->dinfo, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::memcpy(info, c->hpin + F.NB, sizeof(int));
+  double s = 0.0;
+  for (int k = 0; k < F.NB; ++k) s += c->hpin[k];
+  *logdetA = 2.0 * s;
+  return GPE_OK;
+}
+
+int check_ready(gpe_ctx* c) {
+  if (!c) return GPE_ERR_ARG;
+  if (c->n <= 0) return fail(c, GPE_ERR_STATE, "gpe_set_data has not been called");
+  HIPCHK(c, hipSetDevice(c->device));
+  return GPE_OK;
+}
+
+void ev_rec(gpe_ctx* c, int i) {
+  if (c->prof) hipEventRecord(c->ev[i], c->stream);
+}
+
+int factor_and_invert(gpe_ctx* c, int kernel, const double* delta, double nu, double s2,
+                      double rscale) {
+  HIPCHK(c, hipMemsetAsync(c->dinfo, 0, sizeof(int), c->stream));
+  CHK(build_plan(c, c->tr));
+  ev_rec(c, 0);
+  CHK(scale_training(c, delta));
+  CHK(kbuild(c, kernel, nu, s2, rscale));
+  ev_rec(c, 1);
+  CHK(potrf(c, c->tr));
+  ev_rec(c, 2);
+  CHK(trtri(c, c->tr));
+  ev_rec(c, 3);
+  return GPE_OK;
+}
+
+}  // namespace
+
+// =====================================================================  C-ABI
+extern "C" {
+
+int gpe_abi_version(void) { return GPE_ABI_VERSION; }
+
+int gpe_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+gpe_ctx* gpe_create(int32_t device) {
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev <= 0) {
+    g_create_error = std::string("no HIP device available: ") + hipGetErrorString(e);
+    return nullptr;
+  }
+  if (device < 0 || device >= ndev) {
+    g_create_error = "device index out of range";
+    return nullptr;
+  }
+  gpe_ctx* c = new gpe_ctx();
+  c->device = device;
+  c->aux.desc_base = AUX_DESC_BASE;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    g_create_error = "failed to initialise device/stream";
+    delete c;
+    return nullptr;
+  }
+  bool ok = dalloc(c, &c->dinfo, 4) == GPE_OK && dalloc(c, &c->dprobs, MAX_PROBS) == GPE_OK &&
+            dalloc(c, &c->dgram, SK_PMAX * SK_PMAX) == GPE_OK &&
+            dalloc(c, &c->dT2, SK_PMAX * SK_PMAX) == GPE_OK && dalloc(c, &c->dinvdelta, 64) == GPE_OK &&
+            dalloc(c, &c->dcsum, 64) == GPE_OK;
+  for (int i = 0; i < 16 && ok; ++i) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
+  if (ok) {
+    const int gl = G_LDS_DOUBLES * (int)sizeof(double);
+    ok = hipFuncSetAttribute((const void*)k_gemm<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_gemm<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_gemm<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_gemm<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess;
+    if (!ok) c->err = "hipFuncSetAttribute(max dynamic LDS) failed";
+  }
+  if (!ok) {
+    g_create_error = c->err;
+    gpe_destroy(c);
+    return nullptr;
+  }
+  return c;
+}
+
+void gpe_destroy(gpe_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  double* bufs[] = {c->dX, c->dXw, c->dF, c->dr, c->tr.A, c->tr.B, c->tr.logdet, c->aux.A, c->aux.B,
+                    c->aux.logdet, c->dinvdelta, c->dZ,
+                    c->dR2, c->dWa, c->dskp, c->dgpart, c->dgram, c->dT2, c->dcpart, c->dcsum,
+                    c->dW1, c->dW2, c->dW3, c->dXs, c->dXsw, c->dsmall};
+  for (double* b : bufs)
+    if (b) hipFree(b);
+  if (c->dinfo) hipFree(c->dinfo);
+  if (c->dprobs) hipFree(c->dprobs);
+  if (c->hpin) hipHostFree(c->hpin);
+  for (auto& e : c->ev)
+    if (e) hipEventDestroy(e);
+  for (auto& e : c->gev) hipEventDestroy(e);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* gpe_last_error(const gpe_ctx* c) {
+  if (!c) return g_create_error.c_str();
+  return c->err.c_str();
+}
+
+int gpe_set_data(gpe_ctx* c, int64_t n, int32_t d, int32_t q, const double* X, const double* f,
+                 const double* H, const double* r) {
+  if (!c) return GPE_ERR_ARG;
+  if (n <= 0 || d <= 0 || q <= 0 || !X || !f || !H) return fail(c, GPE_ERR_ARG, "bad data arguments");
+  if (d > 32) return fail(c, GPE_ERR_UNSUPPORTED, "d > 32 input dimensions is not supported");
+  if (q + 1 > SK_PMAX) return fail(c, GPE_ERR_UNSUPPORTED, "q > 31 basis functions is not supported");
+  if (n > (1LL << 20)) return fail(c, GPE_ERR_UNSUPPORTED, "n too large");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const long long n_pad = ((n + TILE - 1) / TILE) * TILE;
+  const bool resize = (n_pad != c->n_pad) || (d != c->d) || (q != c->q);
+  c->n = n; c->d = d; c->q = q; c->n_pad = n_pad; c->NB = (int)(n_pad / TILE);
+  c->factor_valid = false;
+  if (resize) {
+    CHK(ensure_fact(c, c->tr, n_pad));
+    CHK(dalloc(c, &c->dX, (size_t)n_pad * d));
+    CHK(dalloc(c, &c->dXw, (size_t)n_pad * d));
+    CHK(dalloc(c, &c->dF, (size_t)n_pad * (q + 1)));
+    CHK(dalloc(c, &c->dr, (size_t)n_pad));
+    CHK(dalloc(c, &c->dZ, (size_t)n_pad * SK_PMAX));
+    CHK(dalloc(c, &c->dR2, (size_t)n_pad * SK_PMAX));
+    CHK(dalloc(c, &c->dWa, (size_t)n_pad * SK_PMAX));
+    const size_t cp = (size_t)c->NB * (c->NB + 1) / 2 * (d + 2);
+    CHK(dalloc(c, &c->dcpart, cp));
+    c->cpart_cap = cp;
+  }
+  // stage: X (row-major, padded rows 0), F = [f H] column-major, r
+  const size_t nx = (size_t)n_pad * d, nf = (size_t)n_pad * (q + 1);
+  CHK(ensure_pinned(c, std::max(nx, nf) + n_pad));
+  std::memset(c->hpin, 0, nx * sizeof(double));
+  std::memcpy(c->hpin, X, (size_t)n * d * sizeof(double));
+  HIPCHK(c, hipMemcpy(c->dX, c->hpin, nx * sizeof(double), hipMemcpyHostToDevice));
+  std::memset(c->hpin, 0, nf * sizeof(double));
+  for (long long i = 0; i < n; ++i) {
+    c->hpin[i] = f[i];
+    for (int p = 0; p < q; ++p) c->hpin[i + (long long)(p + 1) * n_pad] = H[i * q + p];
+  }
+  HIPCHK(c, hipMemcpy(c->dF, c->hpin, nf * sizeof(double), hipMemcpyHostToDevice));
+  c->has_r = (r != nullptr);
+  std::memset(c->hpin, 0, n_pad * sizeof(double));
+  if (r) std::memcpy(c->hpin, r, (size_t)n * sizeof(double));
+  HIPCHK(c, hipMemcpy(c->dr, c->hpin, n_pad * sizeof(double), hipMemcpyHostToDevice));
+  return GPE_OK;
+}
+
+int gpe_set_profiling(gpe_ctx* c, int32_t on) {
+  if (!c) return GPE_ERR_ARG;
+  c->prof = on != 0;
+  return GPE_OK;
+}
+
+int gpe_phase_times(gpe_ctx* c, double* ms_out, int32_t n) {
+  if (!c || !ms_out) return GPE_ERR_ARG;
+  for (int i = 0; i < n && i < 8; ++i) ms_out[i] = c->phase_ms[i];
+  return GPE_OK;
+}
+
+int gpe_gemm_stats(gpe_ctx* c, double* ms_out, double* launches_out, double* flops_out) {
+  if (!c) return GPE_ERR_ARG;
+  if (ms_out) *ms_out = c->gemm_ms;
+  if (launches_out) *launches_out = c->gemm_launches;
+  if (flops_out) *flops_out = c->gemm_flops;
+  return GPE_OK;
+}
+
+int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp, int32_t n_hp,
+                  double nu_fixed, int32_t want_grad, double* llh_out, double* grad_out,
+                  double* sigma2_out) {
+  CHK(check_ready(c));
+  if (!hp || !llh_out) return fail(c, GPE_ERR_ARG, "null output");
+  if (variant != GPE_GP4ML && variant != GPE_MUCM) return fail(c, GPE_ERR_ARG, "bad variant");
+  if (kernel != GPE_KERNEL_STD && kernel != GPE_KERNEL_ALT_NUG) return fail(c, GPE_ERR_ARG, "bad kernel");
+  const int d = c->d, q = c->q;
+  const bool gp4ml = variant == GPE_GP4ML;
+  const int base = gp4ml ? d + 1 : d;
+  if (n_hp != base && n_hp != base + 1) return fail(c, GPE_ERR_ARG, "n_hp inconsistent with d");
+  if (want_grad && !grad_out) return fail(c, GPE_ERR_ARG, "grad_out is NULL");
+  const bool fitnug = (n_hp == base + 1);
+  const double nu = fitnug ? hp[d] : nu_fixed;
+  const double sigma = gp4ml ? hp[n_hp - 1] : 1.0;
+  const double s2 = gp4ml ? sigma * sigma : 1.0;
+  const double rscale = (gp4ml && kernel == GPE_KERNEL_ALT_NUG) ? 1.0 : 0.0;
+  c->factor_valid = false;
+  if (c->prof) {
+    for (auto& e : c->gev) hipEventDestroy(e);
+    c->gev.clear();
+    c->gemm_launches = c->gemm_flops = c->gemm_ms = 0.0;
+  }
+
+  CHK(factor_and_invert(c, kernel, hp, nu, s2, rscale));
+  // z, w = L^-1 [f H]
+  const int P = q + 1;
+  const long long np = c->n_pad;
+  CHK(skinny(c, false, c->tr.B, np, c->NB, c->NB, true, c->dF, np, P, c->dZ, np));
+  std::vector<double> G((size_t)P * P);
+  CHK(gram(c, c->dZ, np, P, (int)np, G.data()));
+  int info = 0;
+  double logdetA = 0.0;
+  CHK(read_info_logdet(c, c->tr, &info, &logdetA));
+  if (info != 0) {
+    c->err = "matrix not positive definite (pivot " + std::to_string(info) + ")";
+    return GPE_NOT_PD;
+  }
+  SmallAlgebra sa = small_from_gram(G, P);
+  if (!sa.ok) {
+    c->err = "H^T A^-1 H not positive definite";
+    return GPE_NOT_PD;
+  }
+  const double n = (double)c->n;
+  double llh, sig2, cfac, gscale;
+  if (gp4ml) {
+    llh = 0.5 * (sa.quad + logdetA + sa.logdetQ + (n - q) * std::log(2.0 * M_PI));
+    sig2 = s2;
+    cfac = 1.0;
+    gscale = s2;
+  } else {
+    sig2 = sa.quad / (n - q - 2.0);
+    llh = 0.5 * ((n - q) * std::log(sig2) + logdetA + sa.logdetQ);
+    cfac = (n - q) / (sig2 * (n - q - 2.0));
+    gscale = sig2;
+  }
+  *llh_out = llh;
+  if (sigma2_out) *sigma2_out = sig2;
+  if (!want_grad) {
+    ev_rec(c, 4);
+    ev_rec(c, 5);
+    ev_rec(c, 6);
+    goto done;
+  }
+  {
+    ev_rec(c, 4);
+    // A^-1 = L^-T L^-1 over L in dA
+    CHK(launch_gemm_range(c, c->tr.plan.launches[c->tr.plan.lauum]));
+    ev_rec(c, 5);
+    // R2 = [sqrt(c)(z - w B), w Kq^-T] ; [sqrt(c) alpha, W] = L^-T R2
+    std::vector<double> Kinv = small_trinv(sa.Kq, q);  // row-major
+    CHK(ensure_pinned(c, (size_t)P * P + 8));
+    std::vector<double> T2((size_t)P * P, 0.0);    // column-major P x P
+    const double sc = std::sqrt(cfac);
+    T2[0] = sc;
+    for (int i = 0; i < q; ++i) T2[(i + 1) + 0 * P] = -sc * sa.beta[i];
+    for (int o = 0; o < q; ++o)
+      for (int i = 0; i < q; ++i) T2[(i + 1) + (o + 1) * P] = Kinv[o * q + i];  // (Kq^-T)(i,o) = Kinv(o,i)
+    std::memcpy(c->hpin, T2.data(), T2.size() * sizeof(double));
+    HIPCHK(c, hipMemcpyAsync(c->dT2, c->hpin, T2.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_apply_small, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, c->stream,
+                       c->dZ, np, P, c->dT2, P, c->dR2, np, (int)np, c->dinfo);
+    HIPCHK(c, hipGetLastError());
+    CHK(skinny(c, true, c->tr.B, np, c->NB, c->NB, true, c->dR2, np, P, c->dWa, np));
+    ev_rec(c, 6);
+    // contraction
+    const int nblk = c->NB * (c->NB + 1) / 2;
+    const int bucket = std::max(d, P);
+    if (bucket <= 8) {
+      hipLaunchKernelGGL((k_contract<8, 9>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo);
+    } else if (bucket <= 16) {
+      hipLaunchKernelGGL((k_contract<16, 17>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo);
+    } else {
+      hipLaunchKernelGGL((k_contract<32, 33>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo);
+    }
+    HIPCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(k_reduce_rows, dim3(d + 2), dim3(256), 0, c->stream, c->dcpart, nblk, d + 2, c->dcsum);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(c->hpin, c->dcsum, (d + 2) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const double* red = c->hpin;
+    double coff, cdiag;
+    kernel_consts(kernel, nu, true, &coff, &cdiag);
+    const double pref = (kernel == GPE_KERNEL_ALT_NUG) ? 1.0 : (1.0 - nu);
+    const double SE = 2.0 * red[d], Tr = red[d + 1];
+    for (int k = 0; k < d; ++k) grad_out[k] = 0.5 * gscale * pref * 2.0 * red[k];
+    if (fitnug) {
+      grad_out[d] = (kernel == GPE_KERNEL_ALT_NUG) ? 0.5 * gscale * nu * nu * Tr
+                                                   : 0.5 * gscale * (-0.5 * nu) * SE;
+    }
+    if (gp4ml) grad_out[n_hp - 1] = 0.5 * s2 * (coff * SE + cdiag * Tr);
+  }
+done:
+  if (c->prof) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float ms;
+    const int pairs[7][2] = {{0, 1}, {1, 2}, {2, 3}, {4, 5}, {3, 4}, {5, 6}, {0, 6}};
+    for (int i = 0; i < 7; ++i) {
+      ms = 0.f;
+      (void)hipEventElapsedTime(&ms, c->ev[pairs[i][0]], c->ev[pairs[i][1]]);
+      c->phase_ms[i] = ms;
+    }
+    double g = 0.0;
+    for (size_t i = 0; i + 1 < c->gev.size(); i += 2) {
+      ms = 0.f;
+      (void)hipEventElapsedTime(&ms, c->gev[i], c->gev[i + 1]);
+      g += ms;
+    }
+    c->gemm_ms = g;
+  }
+  return GPE_OK;
+}
+
+int gpe_factor(gpe_ctx* c, int32_t kernel, const double* delta, double nu, double s2, double r_scale) {
+  CHK(check_ready(c));
+  if (!delta) return fail(c, GPE_ERR_ARG, "null delta");
+  if (kernel != GPE_KERNEL_STD && kernel != GPE_KERNEL_ALT_NUG) return fail(c, GPE_ERR_ARG, "bad kernel");
+  c->factor_valid = false;
+  CHK(factor_and_invert(c, kernel, delta, nu, s2, r_scale));
+  int info = 0;
+  double logdet = 0.0;
+  CHK(read_info_logdet(c, c->tr, &info, &logdet));
+  if (info != 0) {
+    c->err = "matrix not positive definite (pivot " + std::to_string(info) + ")";
+    return GPE_NOT_PD;
+  }
+  c->factor_valid = true;
+  c->f_kernel = kernel;
+  c->f_delta.assign(delta, delta + c->d);
+  c->f_nu = nu;
+  return GPE_OK;
+}
+
+int gpe_beta(gpe_ctx* c, double* beta_out) {
+  CHK(check_ready(c));
+  if (!c->factor_valid) return fail(c, GPE_ERR_STATE, "no resident factor (call gpe_factor)");
+  const int P = c->q + 1;
+  const long long np = c->n_pad;
+  CHK(skinny(c, false, c->tr.B, np, c->NB, c->NB, true, c->dF, np, P, c->dZ, np));
+  std::vector<double> G((size_t)P * P);
+  CHK(gram(c, c->dZ, np, P, (int)np, G.data()));
+  SmallAlgebra sa = small_from_gram(G, P);
+  if (!sa.ok) return fail(c, GPE_NOT_PD, "H^T A^-1 H not positive definite");
+  for (int i = 0; i < c->q; ++i) beta_out[i] = sa.beta[i];
+  return GPE_OK;
+}
+
+int gpe_posterior(gpe_ctx* c, int64_t m, const double* Xs, const double* Hs, const double* beta,
+                  double sigma, int32_t full_var, double* mean_out, double* var_out) {
+  CHK(check_ready(c));
+  if (!c->factor_valid) return fail(c, GPE_ERR_STATE, "no resident factor (call gpe_factor)");
+  if (m <= 0 || !Xs || !Hs || !beta || !mean_out || !var_out) return fail(c, GPE_ERR_ARG, "bad posterior args");
+  const int d = c->d, q = c->q, P = q + 1;
+  const long long np = c->n_pad;
+  const long long CHUNK = full_var ? 16384 : 4096;
+  if (full_var && m > CHUNK) return fail(c, GPE_ERR_UNSUPPORTED, "full posterior variance limited to m <= 16384");
+  // [gamma, G] = A^-1 [f - H beta, H]
+  CHK(ensure_pinned(c, (size_t)P * P + 64));
+  {
+    std::vector<double> T((size_t)P * P, 0.0);  // col-major
+    T[0] = 1.0;
+    for (int i = 0; i < q; ++i) {
+      T[(i + 1) + 0 * P] = -beta[i];
+      T[(i + 1) + (i + 1) * P] = 1.0;
+    }
+    std::memcpy(c->hpin, T.data(), T.size() * sizeof(double));
+    HIPCHK(c, hipMemcpyAsync(c->dT2, c->hpin, T.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  }
+  hipLaunchKernelGGL(k_apply_small, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, c->stream,
+                     c->dF, np, P, c->dT2, P, c->dR2, np, (int)np, nullptr);
+  HIPCHK(c, hipGetLastError());
+  CHK(skinny(c, false, c->tr.B, np, c->NB, c->NB, true, c->dR2, np, P, c->dZ, np));   // L^-1 [f-Hb, H]
+  CHK(skinny(c, true, c->tr.B, np, c->NB, c->NB, true, c->dZ, np, P, c->dWa, np));   // A^-1 [f-Hb, H]
+  std::vector<double> G((size_t)P * P);
+  CHK(gram(c, c->dZ, np, P, (int)np, G.data()));
+  // Q = H^T A^-1 H = G[1:,1:]
+  std::vector<double> Kq((size_t)q * q);
+  for (int i = 0; i < q; ++i)
+    for (int j = 0; j < q; ++j) Kq[i * q + j] = G[(i + 1) * P + (j + 1)];
+  if (!small_chol(Kq, q)) return fail(c, GPE_NOT_PD, "H^T A^-1 H not positive definite");
+  std::vector<double> Kinv = small_trinv(Kq, q);
+  double coff, cdiag;
+  kernel_consts(c->f_kernel, c->f_nu, true, &coff, &cdiag);
+  const double s2 = sigma * sigma;
+
+  for (long long s0 = 0; s0 < m; s0 += CHUNK) {
+    const long long mc = std::min(CHUNK, m - s0);
+    const long long mp = ((mc + TILE - 1) / TILE) * TILE;
+    const int mt = (int)(mp / TILE);
+    // workspace: K* (np x mp) and V (np x mp) [+ full var mp x mp]
+    const size_t need = (size_t)np * mp;
+    if (need > c->w_cap) {
+      CHK(dalloc(c, &c->dW1, need));
+      CHK(dalloc(c, &c->dW2, need));
+      c->w_cap = need;
+    }
+    if ((size_t)mp * d > c->xs_cap) {
+      CHK(dalloc(c, &c->dXs, (size_t)mp * d));
+      CHK(dalloc(c, &c->dXsw, (size_t)mp * d));
+      c->xs_cap = (size_t)mp * d;
+    }
+    CHK(ensure_pinned(c, std::max<size_t>((size_t)mp * d, (size_t)mp * P) + 64));
+    std::memset(c->hpin, 0, (size_t)mp * d * sizeof(double));
+    std::memcpy(c->hpin, Xs + s0 * d, (size_t)mc * d * sizeof(double));
+    HIPCHK(c, hipMemcpyAsync(c->dXs, c->hpin, (size_t)mp * d * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    for (int k = 0; k < d; ++k) c->hpin[(size_t)mp * d + k] = 1.0 / c->f_delta[k];
+    HIPCHK(c, hipMemcpyAsync(c->dinvdelta, c->hpin + (size_t)mp * d, d * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    {
+      const long long tot = mp * d;
+      hipLaunchKernelGGL(k_scale_points, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
+                         c->dXs, c->dinvdelta, d, (int)mc, (int)mp, c->dXsw);
+      HIPCHK(c, hipGetLastError());
+    }
+    // K*(i, s) = coff * exp(-|x_i - xs_s|^2), padded rows/cols 0
+    {
+      PairArgs a;
+      a.xr = c->dXw; a.xc = c->dXsw; a.out = c->dW1; a.ld = np; a.d = d;
+      a.nr_valid = (int)c->n; a.nc_valid = (int)mc; a.mt = c->NB; a.nt = mt; a.mode = 0;
+      a.s2 = 1.0; a.coff = coff; a.cdiag = cdiag; a.rscale = 0.0; a.r = nullptr;
+      CHK(launch_pairs(c, a, c->NB * mt));
+    }
+    // Y = K*^T [gamma, G]  (mp x P)
+    double* dY = c->dR2;   // reuse (np >= ... not guaranteed) -> use dsmall
+    CHK(ensure_small(c, (size_t)mp * P + 64));
+    dY = c->dsmall;
+    {
+      // skinny transposed over a full matrix: M = K* (np x mp), k tiles = NB, out tiles = mt
+      const int nch = (c->NB + SK_CH - 1) / SK_CH;
+      const size_t needp = (size_t)nch * mp * P;
+      if (needp > c->skp_cap) {
+        CHK(dalloc(c, &c->dskp, needp));
+        c->skp_cap = needp;
+      }
+      SkinnyArgs a;
+      a.M = c->dW1; a.ldm = np; a.R = c->dWa; a.ldr = np; a.part = c->dskp; a.ldp = mp;
+      a.pstride = mp * P; a.P = P; a.ntr = c->NB; a.lower = 0; a.nit = mt; a.abort_flag = nullptr;
+      const int pm = pmax_bucket(P);
+      dim3 grid(mt * nch);
+      if (pm == 8) hipLaunchKernelGGL(k_trmm_skinny_t<8>, grid, dim3(256), 0, c->stream, a);
+      else if (pm == 16) hipLaunchKernelGGL(k_trmm_skinny_t<16>, grid, dim3(256), 0, c->stream, a);
+      else hipLaunchKernelGGL(k_trmm_skinny_t<32>, grid, dim3(256), 0, c->stream, a);
+      HIPCHK(c, hipGetLastError());
+      const long long tot = mp * P;
+      hipLaunchKernelGGL(k_reduce_chunks, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
+                         c->dskp, (long long)(mp * P), dY, mp, P, (int)mp, c->NB, 2, nullptr);
+      HIPCHK(c, hipGetLastError());
+    }
+    // V = L^-1 K*   (np x mp), X lower-triangular -> kend = (ti+1)*128
+    {
+      std::vector<GemmProb> pv = {mkprob(c->tr.B, np, c->dW1, np, c->dW2, np, c->NB, mt, (int)np,
+                                         G_KEND_TI, 1.0, 0.0)};
+      pv[0].tile_begin = 0;
+      pv[0].ntiles = c->NB * mt;
+      HIPCHK(c, hipMemcpyAsync(c->dprobs + ADHOC_DESC_BASE, pv.data(), sizeof(GemmProb), hipMemcpyHostToDevice, c->stream));
+      Launch L{3, ADHOC_DESC_BASE, 1, c->NB * mt, 0.0};
+      CHK(launch_gemm_range(c, L));
+    }
+    // host pieces: mean, T = Hs - K*^T G
+    std::vector<double> Yh((size_t)mp * P);
+    HIPCHK(c, hipMemcpyAsync(c->hpin, dY, (size_t)mp * P * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::memcpy(Yh.data(), c->hpin, Yh.size() * sizeof(double));
+    std::vector<double> Tt((size_t)mc * q);   // T Kq^-T, row-major mc x q
+    for (long long s = 0; s < mc; ++s) {
+      const double* hs = Hs + (s0 + s) * q;
+      double mu = Yh[s];
+      for (int i = 0; i < q; ++i) mu += hs[i] * beta[i];
+      mean_out[s0 + s] = mu;
+      for (int o = 0; o < q; ++o) {
+        double acc = 0.0;
+        for (int i = 0; i < q; ++i) acc += (hs[i] - Yh[s + (long long)(i + 1) * mp]) * Kinv[o * q + i];
+        Tt[s * q + o] = acc;
+      }
+    }
+    if (!full_var) {
+      CHK(ensure_small(c, (size_t)mp * P + mp + 64));
+      double* dn = c->dsmall + (size_t)mp * P;
+      hipLaunchKernelGGL(k_colnorm2, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, c->stream, c->dW2, np,
+                         (int)np, (int)mp, dn);
+      HIPCHK(c, hipGetLastError());
+      HIPCHK(c, hipMemcpyAsync(c->hpin, dn, (size_t)mp * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      for (long long s = 0; s < mc; ++s) {
+        double tq = 0.0;
+        for (int o = 0; o < q; ++o) tq += Tt[s * q + o] * Tt[s * q + o];
+        var_out[s0 + s] = s2 * (cdiag - c->hpin[s] + tq);
+      }
+    } else {
+      // C = s2 * (A** - V^T V + Tt Tt^T), all tiles (full symmetric)
+      const size_t needc = (size_t)mp * mp;
+      const int kq = ((q + 15) / 16) * 16;
+      if (needc + (size_t)mp * kq > c->w3_cap) {
+        CHK(dalloc(c, &c->dW3, needc + (size_t)mp * kq));
+        c->w3_cap = needc + (size_t)mp * kq;
+      }
+      double* dC = c->dW3;
+      double* dTt = c->dW3 + needc;
+      {
+        PairArgs a;
+        a.xr = c->dXsw; a.xc = c->dXsw; a.out = dC; a.ld = mp; a.d = d;
+        a.nr_valid = (int)mc; a.nc_valid = (int)mc; a.mt = mt; a.nt = mt; a.mode = 1 | 2 | 4;
+        a.s2 = s2; a.coff = coff; a.cdiag = cdiag; a.rscale = 0.0; a.r = nullptr;
+        CHK(launch_pairs(c, a, mt * (mt + 1) / 2));
+      }
+      std::vector<double> tth((size_t)mp * kq, 0.0);   // column-major mp x kq
+      for (long long s = 0; s < mc; ++s)
+        for (int o = 0; o < q; ++o) tth[s + (size_t)o * mp] = Tt[s * q + o];
+      CHK(ensure_pinned(c, tth.size() + 64));
+      std::memcpy(c->hpin, tth.data(), tth.size() * sizeof(double));
+      HIPCHK(c, hipMemcpyAsync(dTt, c->hpin, tth.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
+      std::vector<GemmProb> p2 = {
+          mkprob(c->dW2, np, c->dW2, np, dC, mp, mt, mt, (int)np, 0, -s2, 1.0),
+          mkprob(dTt, mp, dTt, mp, dC, mp, mt, mt, kq, 0, s2, 1.0)};
+      p2[0].tile_begin = 0; p2[0].ntiles = mt * mt;
+      p2[1].tile_begin = 0; p2[1].ntiles = mt * mt;
+      HIPCHK(c, hipMemcpyAsync(c->dprobs + ADHOC_DESC_BASE + 1, p2.data(), 2 * sizeof(GemmProb), hipMemcpyHostToDevice, c->stream));
+      Launch L1{2, ADHOC_DESC_BASE + 1, 1, mt * mt, 0.0};
+      CHK(launch_gemm_range(c, L1));
+      Launch L2{0, ADHOC_DESC_BASE + 2, 1, mt * mt, 0.0};
+      CHK(launch_gemm_range(c, L2));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      // copy out m x m (col-major == row-major for the symmetric result)
+      std::vector<double> hc((size_t)mp * mc);
+      HIPCHK(c, hipMemcpy(hc.data(), dC, hc.size() * sizeof(double), hipMemcpyDeviceToHost));
+      for (long long j = 0; j < mc; ++j)
+        std::memcpy(var_out + j * m, hc.data() + (size_t)j * mp, (size_t)mc * sizeof(double));
+    }
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GPE_OK;
+}
+
+int gpe_kernel_var(gpe_ctx* c, int32_t kernel, const double* delta, int32_t d, double nu,
+                   int32_t predict, int64_t m, const double* X, const double* r, double r_scale,
+                   double* A_out) {
+  if (!c) return GPE_ERR_ARG;
+  if (!delta || !X || !A_out || m <= 0 || d <= 0 || d > 32) return fail(c, GPE_ERR_ARG, "bad kernel_var args");
+  HIPCHK(c, hipSetDevice(c->device));
+  const long long mp = ((m + TILE - 1) / TILE) * TILE;
+  const int mt = (int)(mp / TILE);
+  double *dx = nullptr, *dxw = nullptr, *dout = nullptr, *dr = nullptr;
+  CHK(dalloc(c, &dx, (size_t)mp * d));
+  CHK(dalloc(c, &dxw, (size_t)mp * d));
+  int rc = dalloc(c, &dout, (size_t)mp * mp);
+  if (rc == GPE_OK && r) rc = dalloc(c, &dr, (size_t)mp);
+  if (rc == GPE_OK) {
+    rc = ensure_pinned(c, (size_t)mp * d + 64 + (size_t)mp);
+  }
+  if (rc == GPE_OK) {
+    std::memset(c->hpin, 0, (size_t)mp * d * sizeof(double));
+    std::memcpy(c->hpin, X, (size_t)m * d * sizeof(double));
+    for (int k = 0; k < d; ++k) c->hpin[(size_t)mp * d + k] = 1.0 / delta[k];
+    (void)hipMemcpy(dx, c->hpin, (size_t)mp * d * sizeof(double), hipMemcpyHostToDevice);
+    (void)hipMemcpy(c->dinvdelta, c->hpin + (size_t)mp * d, d * sizeof(double), hipMemcpyHostToDevice);
+    if (r) {
+      std::memset(c->hpin, 0, (size_t)mp * sizeof(double));
+      std::memcpy(c->hpin, r, (size_t)m * sizeof(double));
+      (void)hipMemcpy(dr, c->hpin, (size_t)mp * sizeof(double), hipMemcpyHostToDevice);
+    }
+    const long long tot = mp * d;
+    hipLaunchKernelGGL(k_scale_points, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
+                       dx, c->dinvdelta, d, (int)m, (int)mp, dxw);
+    PairArgs a;
+    a.xr = dxw; a.xc = dxw; a.out = dout; a.ld = mp; a.d = d; a.nr_valid = (int)m; a.nc_valid = (int)m;
+    a.mt = mt; a.nt = mt; a.mode = 1 | 2 | 4;
+    double coff, cdiag;
+    kernel_consts(kernel, nu, predict != 0, &coff, &cdiag);
+    a.s2 = 1.0; a.coff = coff; a.cdiag = cdiag; a.rscale = r_scale; a.r = dr;
+    rc = launch_pairs(c, a, mt * (mt + 1) / 2);
+    if (rc == GPE_OK) {
+      hipError_t e = hipStreamSynchronize(c->stream);
+      if (e != hipSuccess) rc = fail(c, GPE_ERR_HIP, hipGetErrorString(e));
+    }
+    if (rc == GPE_OK) {
+      for (long long j = 0; j < m; ++j)
+        (void)hipMemcpy(A_out + j * m, dout + j * mp, (size_t)m * sizeof(double), hipMemcpyDeviceToHost);
+    }
+  }
+  (void)hipFree(dx);
+  (void)hipFree(dxw);
+  if (dout) hipFree(dout);
+  if (dr) hipFree(dr);
+  return rc;
+}
+
+int gpe_kernel_covar(gpe_ctx* c, int32_t kernel, const double* delta, int32_t d, double nu,
+                     int64_t n, const double* XT, int64_t m, const double* XV, double* C_out) {
+  if (!c) return GPE_ERR_ARG;
+  if (!delta || !XT || !XV || !C_out || n <= 0 || m <= 0 || d <= 0 || d > 32)
+    return fail(c, GPE_ERR_ARG, "bad kernel_covar args");
+  HIPCHK(c, hipSetDevice(c->device));
+  // compute C^T (m x n, column-major == n x m row-major)
+  const long long mp = ((m + TILE - 1) / TILE) * TILE, np = ((n + TILE - 1) / TILE) * TILE;
+  double *dxt = nullptr, *dxv = nullptr, *dxtw = nullptr, *dxvw = nullptr, *dout = nullptr;
+  int rc = GPE_OK;
+  rc = dalloc(c, &dxt, (size_t)np * d);
+  if (rc == GPE_OK) rc = dalloc(c, &dxtw, (size_t)np * d);
+  if (rc == GPE_OK) rc = dalloc(c, &dxv, (size_t)mp * d);
+  if (rc == GPE_OK) rc = dalloc(c, &dxvw, (size_t)mp * d);
+  if (rc == GPE_OK) rc = dalloc(c, &dout, (size_t)mp * np);
+  if (rc == GPE_OK) rc = ensure_pinned(c, (size_t)std::max(np, mp) * d + 64);
+  if (rc == GPE_OK) {
+    for (int k = 0; k < d; ++k) c->hpin[k] = 1.0 / delta[k];
+    (void)hipMemcpy(c->dinvdelta, c->hpin, d * sizeof(double), hipMemcpyHostToDevice);
+    std::memset(c->hpin, 0, (size_t)np * d * sizeof(double));
+    std::memcpy(c->hpin, XT, (size_t)n * d * sizeof(double));
+    (void)hipMemcpy(dxt, c->hpin, (size_t)np * d * sizeof(double), hipMemcpyHostToDevice);
+    std::memset(c->hpin, 0, (size_t)mp * d * sizeof(double));
+    std::memcpy(c->hpin, XV, (size_t)m * d * sizeof(double));
+    (void)hipMemcpy(dxv, c->hpin, (size_t)mp * d * sizeof(double), hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(k_scale_points, dim3((unsigned)((np * d + 255) / 256)), dim3(256), 0, c->stream,
+                       dxt, c->dinvdelta, d, (int)n, (int)np, dxtw);
+    hipLaunchKernelGGL(k_scale_points, dim3((unsigned)((mp * d + 255) / 256)), dim3(256), 0, c->stream,
+                       dxv, c->dinvdelta, d, (int)m, (int)mp, dxvw);
+    PairArgs a;
+    a.xr = dxvw; a.xc = dxtw; a.out = dout; a.ld = mp; a.d = d; a.nr_valid = (int)m; a.nc_valid = (int)n;
+    a.mt = (int)(mp / TILE); a.nt = (int)(np / TILE); a.mode = 0;
+    double coff, cdiag;
+    kernel_consts(kernel, nu, true, &coff, &cdiag);
+    a.s2 = 1.0; a.coff = coff; a.cdiag = cdiag; a.rscale = 0.0; a.r = nullptr;
+    rc = launch_pairs(c, a, a.mt * a.nt);
+    if (rc == GPE_OK) {
+      hipError_t e = hipStreamSynchronize(c->stream);
+      if (e != hipSuccess) rc = fail(c, GPE_ERR_HIP, hipGetErrorString(e));
+    }
+    if (rc == GPE_OK) {
+      // dout column j (= training point j) holds C[j, 0:m]
+      for (long long j = 0; j < n; ++j)
+        (void)hipMemcpy(C_out + j * m, dout + j * mp, (size_t)m * sizeof(double), hipMemcpyDeviceToHost);
+    }
+  }
+  (void)hipFree(dxt); hipFree(dxtw); hipFree(dxv); hipFree(dxvw);
+  if (dout) hipFree(dout);
+  return rc;
+}
+
+int gpe_cholesky(gpe_ctx* c, int64_t m, const double* A, double* L_out, double* Linv_out,
+                 double* Ainv_out, double* logdet_out) {
+  if (!c) return GPE_ERR_ARG;
+  if (!A || m <= 0) return fail(c, GPE_ERR_ARG, "bad cholesky args");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const long long mp = ((m + TILE - 1) / TILE) * TILE;
+  Fact& F = c->aux;
+  CHK(ensure_fact(c, F, mp));
+  CHK(build_plan(c, F));
+  // stage the lower triangle column-major, identity padding
+  const size_t tot = (size_t)mp * mp;
+  CHK(ensure_pinned(c, tot));
+  std::memset(c->hpin, 0, tot * sizeof(double));
+  for (long long j = 0; j < m; ++j)
+    for (long long i = j; i < m; ++i) c->hpin[i + j * mp] = A[i * m + j];
+  for (long long i = m; i < mp; ++i) c->hpin[i + i * mp] = 1.0;
+  HIPCHK(c, hipMemcpy(F.A, c->hpin, tot * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemsetAsync(c->dinfo, 0, sizeof(int), c->stream));
+  CHK(potrf(c, F));
+  int info = 0;
+  double logdet = 0.0;
+  CHK(read_info_logdet(c, F, &info, &logdet));
+  if (info != 0) {
+    c->err = "matrix not positive definite (pivot " + std::to_string(info) + ")";
+    return GPE_NOT_PD;
+  }
+  if (logdet_out) *logdet_out = logdet;
+  auto fetch_lower = [&](const double* dsrc, double* out, bool full_sym) -> int {
+    HIPCHK(c, hipMemcpy(c->hpin, dsrc, tot * sizeof(double), hipMemcpyDeviceToHost));
+    for (long long i = 0; i < m; ++i)
+      for (long long j = 0; j < m; ++j) {
+        double v;
+        if (j <= i) v = c->hpin[i + j * mp];
+        else v = full_sym ? c->hpin[j + i * mp] : 0.0;
+        out[i * m + j] = v;
+      }
+    return GPE_OK;
+  };
+  if (L_out) CHK(fetch_lower(F.A, L_out, false));
+  if (Linv_out || Ainv_out) {
+    CHK(trtri(c, F));
+    if (Linv_out) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      CHK(fetch_lower(F.B, Linv_out, false));
+    }
+    if (Ainv_out) {
+      CHK(launch_gemm_range(c, F.plan.launches[F.plan.lauum]));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      CHK(fetch_lower(F.A, Ainv_out, true));
+    }
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GPE_OK;
+}
+
+int gpe_test_gemm(gpe_ctx* c, int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
+                  const double* A, const double* B, double* C, double alpha, double beta) {
+  if (!c) return GPE_ERR_ARG;
+  if (M <= 0 || N <= 0 || K <= 0 || M % TILE || N % TILE || K % GK || !A || !B || !C)
+    return fail(c, GPE_ERR_ARG, "gpe_test_gemm: M, N must be multiples of 128 and K of 16");
+  HIPCHK(c, hipSetDevice(c->device));
+  double *da = nullptr, *db = nullptr, *dc = nullptr;
+  int rc = dalloc(c, &da, (size_t)M * K);
+  if (rc == GPE_OK) rc = dalloc(c, &db, (size_t)K * N);
+  if (rc == GPE_OK) rc = dalloc(c, &dc, (size_t)M * N);
+  if (rc == GPE_OK) {
+    std::vector<double> ha((size_t)M * K), hb((size_t)K * N), hc((size_t)M * N);
+    long long lda, ldb;
+    if (trans_a) { for (long long m = 0; m < M; ++m) for (long long k = 0; k < K; ++k) ha[k + m * K] = A[m * K + k]; lda = K; }
+    else { for (long long m = 0; m < M; ++m) for (long long k = 0; k < K; ++k) ha[m + k * M] = A[m * K + k]; lda = M; }
+    if (trans_b) { for (long long k = 0; k < K; ++k) for (long long n = 0; n < N; ++n) hb[k + n * K] = B[k * N + n]; ldb = K; }
+    else { for (long long k = 0; k < K; ++k) for (long long n = 0; n < N; ++n) hb[n + k * N] = B[k * N + n]; ldb = N; }
+    for (long long m = 0; m < M; ++m) for (long long n = 0; n < N; ++n) hc[m + n * M] = C[m * N + n];
+    (void)hipMemcpy(da, ha.data(), ha.size() * sizeof(double), hipMemcpyHostToDevice);
+    (void)hipMemcpy(db, hb.data(), hb.size() * sizeof(double), hipMemcpyHostToDevice);
+    (void)hipMemcpy(dc, hc.data(), hc.size() * sizeof(double), hipMemcpyHostToDevice);
+    GemmProb p = mkprob(da, lda, db, ldb, dc, M, (int)(M / TILE), (int)(N / TILE), (int)K, 0, alpha, beta);
+    p.tile_begin = 0;
+    p.ntiles = p.mt * p.nt;
+    (void)hipMemcpy(c->dprobs + ADHOC_DESC_BASE + 8, &p, sizeof(GemmProb), hipMemcpyHostToDevice);
+    HIPCHK(c, hipMemsetAsync(c->dinfo, 0, sizeof(int), c->stream));
+    const int kind = trans_a ? (trans_b ? 2 : 1) : (trans_b ? 3 : 0);
+    Launch L{kind, ADHOC_DESC_BASE + 8, 1, p.ntiles, 0.0};
+    rc = launch_gemm_range(c, L);
+    if (rc == GPE_OK) {
+      hipError_t e = hipStreamSynchronize(c->stream);
+      if (e != hipSuccess) rc = fail(c, GPE_ERR_HIP, hipGetErrorString(e));
+    }
+    if (rc == GPE_OK) {
+      (void)hipMemcpy(hc.data(), dc, hc.size() * sizeof(double), hipMemcpyDeviceToHost);
+      for (long long m = 0; m < M; ++m) for (long long n = 0; n < N; ++n) C[m * N + n] = hc[m + n * M];
+    }
+  }
+  if (da) (void)hipFree(da);
+  if (db) (void)hipFree(db);
+  if (dc) (void)hipFree(dc);
+  return rc;
+}
+
+}  // extern "C"
+

@@ -1,0 +1,741 @@
+// gpemu_kernels.hpp -- gfx950 (CDNA4) device kernels of the GP-emulator hot path.
+//
+// Storage conventions (see DESIGN.md "Data layout in HBM"):
+//  * every n x n matrix is column-major fp64 with ld = n_pad (n rounded up to a
+//    multiple of TILE = 128); the padded block is the identity, so Cholesky,
+//    inverse and logdet of the padded matrix equal those of the real one;
+//  * only lower tiles (ti >= tj) carry data; strictly-upper tiles are scratch;
+//  * point sets (X scaled by 1/delta) are row-major n_pad x d, padded rows 0;
+//  * skinny right-hand sides ([f H], [u w], ...) are column-major n_pad x P.
+//
+// Kernels (reference call they replace):
+//  k_pairs          K.var / K.covar pair kernel (pdist+exp+squareform, a1,a2,a11)
+//  k_potrf_diag     128x128 diagonal-block Cholesky + its inverse (dpotrf leaf)
+//  k_gemm<AK,BK>    grouped fp64 MFMA GEMM (v_mfma_f64_16x16x4_f64), used for the
+//                   trailing SYRK, panel TRSM, recursive TRTRI and LAUUM
+//  k_trmm_skinny*   L^-1 x [f H] and L^-T x [u w] (the n x q solves of a7)
+//  k_contract       fused <M, dA/dtheta> for all d+2 hyperparameters (a4,a5,a7)
+//  small kernels    Gram, reductions, apply q x q transform, column norms
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gpe {
+
+constexpr int TILE = 128;
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------
+// pair kernel: out(i,j) = s2*coff*exp(-|xr_i - xc_j|^2)   (x already / delta)
+// mode bit0: lower tiles only (grid enumerates ti >= tj)
+// mode bit1: "training" diagonal/padding rules: gi==gj -> s2*cdiag + rscale*r[gi];
+//            gi or gj >= n_valid -> identity.  Without bit1 padded -> 0.
+// mode bit2: mirror: also write out(j,i) (full symmetric materialisation)
+// ---------------------------------------------------------------------------
+struct PairArgs {
+  const double* xr;   // rows point set, row-major [*, d]
+  const double* xc;   // cols point set, row-major [*, d]
+  double* out;        // column-major
+  long long ld;
+  int d, nr_valid, nc_valid, mt, nt, mode;
+  double s2, coff, cdiag, rscale;
+  const double* r;
+};
+
+__device__ inline void tri_decode(int e, int& ti, int& tj) {
+  int r = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+  while ((r + 1) * (r + 2) / 2 <= e) ++r;
+  while (r * (r + 1) / 2 > e) --r;
+  ti = r;
+  tj = e - r * (r + 1) / 2;
+}
+
+template <int DMAX>
+__global__ void __launch_bounds__(256) k_pairs(PairArgs a) {
+  __shared__ double xs_col[TILE * DMAX];
+  int ti, tj;
+  if (a.mode & 1) tri_decode(blockIdx.x, ti, tj);
+  else { ti = blockIdx.x % a.mt; tj = blockIdx.x / a.mt; }
+  const int tid = threadIdx.x;
+  const int d = a.d;
+  for (int e = tid; e < TILE * d; e += 256) {
+    int c = e / d, k = e - c * d;
+    xs_col[e] = a.xc[(long long)(tj * TILE + c) * d + k];
+  }
+  const int r = tid & (TILE - 1);
+  const int gi = ti * TILE + r;
+  double xi[DMAX];
+#pragma unroll
+  for (int k = 0; k < DMAX; ++k) xi[k] = (k < d) ? a.xr[(long long)gi * d + k] : 0.0;
+  __syncthreads();
+  const double pre = a.s2 * a.coff;
+  const bool train = (a.mode & 2) != 0;
+  for (int c = (tid >> 7); c < TILE; c += 2) {
+    const int gj = tj * TILE + c;
+    double v;
+    if (train && (gi >= a.nr_valid || gj >= a.nc_valid)) {
+      v = (gi == gj) ? 1.0 : 0.0;
+    } else if (!train && (gi >= a.nr_valid || gj >= a.nc_valid)) {
+      v = 0.0;
+    } else if (train && gi == gj) {
+      v = a.s2 * a.cdiag + (a.r ? a.rscale * a.r[gi] : 0.0);
+    } else {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < DMAX; ++k) {
+        if (k < d) {
+          double df = xi[k] - xs_col[c * d + k];
+          s = fma(df, df, s);
+        }
+      }
+      v = pre * exp(-s);
+    }
+    a.out[(long long)gi + (long long)gj * a.ld] = v;
+    if ((a.mode & 4) && ti != tj) a.out[(long long)gj + (long long)gi * a.ld] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// diagonal-block Cholesky + inverse of one 128x128 tile.
+// In : A tile (kt,kt) lower part.  Out: L_kk (lower, in place), Dinv_kk = L_kk^-1
+// into tile (kt,kt) of the inverse buffer (upper part zeroed), sum log(L_jj) into
+// logdet[kt], info = 1-based global column of the first bad pivot (LAPACK dpotrf
+// convention) on failure.  Pivot test `!(p > 0)` rejects 0, negatives and NaN.
+// 1024 threads; thread t owns the 4x4 block (rows 4*(t%32).., cols 4*(t/32)..)
+// of L and of X = L^-1 in registers; only lower blocks are active.  Column j of L
+// and row j of X are broadcast through LDS: two barriers per column for the
+// right-looking factorisation, two per column for the forward-substitution
+// inverse [L | I] -> [I | L^-1].
+// ---------------------------------------------------------------------------
+constexpr int DIAG_THREADS = 1024;
+
+__global__ void __launch_bounds__(DIAG_THREADS) k_potrf_diag(double* A, long long lda, int kt,
+                                                             double* Dinv, long long ldd,
+                                                             double* logdet, int* info) {
+  __shared__ double colbuf[TILE];
+  __shared__ double rowbuf[TILE];
+  __shared__ double diagbuf[TILE];
+  __shared__ double red[16];
+  __shared__ double pivot_s;
+  __shared__ int fail_s;
+  if (*info) return;
+  const int t = threadIdx.x;
+  const int bi = t & 31, bk = t >> 5;
+  const bool active = bi >= bk;
+  double* Akk = A + (long long)kt * TILE * (lda + 1);
+  double a[4][4], x[4][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      a[r][c] = active ? Akk[(4 * bi + r) + (long long)(4 * bk + c) * lda] : 0.0;
+      x[r][c] = (bi == bk && r == c) ? 1.0 : 0.0;
+    }
+  if (t == 0) {
+    pivot_s = a[0][0];
+    fail_s = 0;
+  }
+  __syncthreads();
+  for (int j = 0; j < TILE; ++j) {
+    const int jb = j >> 2, jr = j & 3;
+    const double piv = pivot_s;
+    if (!(piv > 0.0)) {
+      if (t == 0) fail_s = j + 1;
+      break;  // uniform: every thread read the same pivot
+    }
+    const double dj = sqrt(piv), rdj = 1.0 / dj;
+    if (active && bk == jb) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 4 * bi + r;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (c == jr) {
+            if (i > j) {
+              a[r][c] *= rdj;
+              colbuf[i] = a[r][c];
+            } else if (i == j) {
+              a[r][c] = dj;
+              diagbuf[j] = dj;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (active && bk >= jb) {
+      double ci[4], ck[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ci[r] = colbuf[4 * bi + r];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) ck[c] = colbuf[4 * bk + c];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int i = 4 * bi + r, k = 4 * bk + c;
+          if (k > j && i >= k) a[r][c] = fma(-ci[r], ck[c], a[r][c]);
+        }
+      const int jn = j + 1;
+      if (jn < TILE && bi == (jn >> 2) && bk == (jn >> 2)) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (r == (jn & 3)) pivot_s = a[r][r];
+      }
+    }
+    __syncthreads();
+  }
+  if (fail_s) {
+    if (t == 0) atomicCAS(info, 0, kt * TILE + fail_s);
+    return;
+  }
+  // log-determinant contribution (fixed reduction tree)
+  double lg = (t < TILE) ? log(diagbuf[t]) : 0.0;
+  for (int off = 32; off > 0; off >>= 1) lg += __shfl_down(lg, off, 64);
+  if ((t & 63) == 0) red[t >> 6] = lg;
+  // X = L^-1: row j of X is final once scaled; rows below get X(i,c) -= L(i,j) X(j,c)
+  for (int j = 0; j < TILE; ++j) {
+    const int jb = j >> 2, jr = j & 3;
+    const double rl = 1.0 / diagbuf[j];
+    if (active && bi == jb) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (r == jr) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int col = 4 * bk + c;
+            if (col <= j) {
+              x[r][c] *= rl;
+              rowbuf[col] = x[r][c];
+            }
+          }
+        }
+    }
+    if (active && bk == jb) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 4 * bi + r;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (c == jr && i > j) colbuf[i] = a[r][c];
+      }
+    }
+    __syncthreads();
+    if (active && bi >= jb && bk <= jb) {
+      double li[4], xc[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) li[r] = colbuf[4 * bi + r];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) xc[c] = rowbuf[4 * bk + c];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int i = 4 * bi + r, col = 4 * bk + c;
+          if (i > j && col <= j) x[r][c] = fma(-li[r], xc[c], x[r][c]);
+        }
+    }
+    __syncthreads();
+  }
+  if (t == 0) logdet[kt] = (red[0] + red[1]) + (red[2] + red[3]);
+  double* Dkk = Dinv + (long long)kt * TILE * (ldd + 1);
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * bi + r, k = 4 * bk + c;
+      if (active && i >= k) Akk[i + (long long)k * lda] = a[r][c];
+      Dkk[i + (long long)k * ldd] = (active && i >= k) ? x[r][c] : 0.0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// grouped fp64 MFMA GEMM:  C(m,n) = alpha * sum_k opA(m,k) opB(k,n) + beta * C(m,n)
+// over 128x128 output tiles; each problem of a group may skip upper tiles
+// (G_CLOWER) and restrict its K range to a triangular operand's support.
+// AK: opA(m,k) at A[k + m*lda] (K-contiguous) else A[m + k*lda]
+// BK: opB(k,n) at B[k + n*ldb] (K-contiguous) else B[n + k*ldb]
+// C (m,n) at C[m + n*ldc].  256 threads = 4 waves in 2x2, 64x64 per wave =
+// 4x4 v_mfma_f64_16x16x4_f64 accumulators.  K staged 16 deep, double-buffered
+// LDS ([k][m], pitch 144 doubles: conflict-free fragment reads).
+// ---------------------------------------------------------------------------
+enum : int { G_CLOWER = 1, G_KBEG_TI = 2, G_KEND_TI = 4 };
+
+struct GemmProb {
+  const double* A;
+  const double* B;
+  double* C;
+  long long lda, ldb, ldc;
+  int mt, nt, K, flags;
+  double alpha, beta;
+  int tile_begin, ntiles;
+};
+
+constexpr int GK = 16;
+constexpr int GP = 144;
+constexpr int G_LDS_DOUBLES = 2 * 2 * GK * GP;   // 9216 doubles = 73,728 B
+
+// MFMA f64 16x16x4 accumulator layout: lane l, register r -> (row, col) of D
+__device__ inline int mfma64_row(int lane, int r) { return (lane >> 4) + 4 * r; }
+
+template <bool AK, bool BK>
+__global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restrict__ probs, int nprob,
+                                                  const int* __restrict__ abort_flag) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  if (abort_flag && *abort_flag) return;
+  int p = 0;
+  for (int i = 1; i < nprob; ++i)
+    if ((int)blockIdx.x >= probs[i].tile_begin) p = i;
+  const GemmProb P = probs[p];
+  const int local = blockIdx.x - P.tile_begin;
+  int ti, tj;
+  if (P.flags & G_CLOWER) tri_decode(local, ti, tj);
+  else { ti = local % P.mt; tj = local / P.mt; }
+  int kbeg = 0, kend = P.K;
+  if (P.flags & G_KBEG_TI) kbeg = ti * TILE;
+  if (P.flags & G_KEND_TI) kend = min(kend, (ti + 1) * TILE);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+
+  const double* Ab = AK ? P.A + (long long)ti * TILE * P.lda : P.A + (long long)ti * TILE;
+  const double* Bb = BK ? P.B + (long long)tj * TILE * P.ldb : P.B + (long long)tj * TILE;
+
+  // operands are swapped in the MFMA, so D = (A B)^T: lane&15 -> m, row map -> n.
+  // beta != 0: the accumulators start at (beta/alpha) C, loaded in one burst so
+  // the C read latency overlaps the first K stage (no per-element RMW chain).
+  double* Cb = P.C + (long long)ti * TILE + (long long)tj * TILE * P.ldc;
+  d4 acc[4][4];
+  if (P.beta != 0.0) {
+    const double sc = P.beta / P.alpha;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = wm + i * 16 + (lane & 15);
+          const int n = wn + j * 16 + mfma64_row(lane, r);
+          acc[i][j][r] = sc * Cb[m + (long long)n * P.ldc];
+        }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+  }
+
+  double2 ra[4], rb[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int c = tid + 256 * s;
+      if (!AK) {
+        const int kk = c >> 6, mm = (c & 63) * 2;
+        ra[s] = *reinterpret_cast<const double2*>(Ab + mm + (long long)(k0 + kk) * P.lda);
+      } else {
+        const int mm = c >> 3, kk = (c & 7) * 2;
+        ra[s] = *reinterpret_cast<const double2*>(Ab + (long long)mm * P.lda + k0 + kk);
+      }
+      if (!BK) {
+        const int kk = c >> 6, nn = (c & 63) * 2;
+        rb[s] = *reinterpret_cast<const double2*>(Bb + nn + (long long)(k0 + kk) * P.ldb);
+      } else {
+        const int nn = c >> 3, kk = (c & 7) * 2;
+        rb[s] = *reinterpret_cast<const double2*>(Bb + (long long)nn * P.ldb + k0 + kk);
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+    double* As = lds + buf * (2 * GK * GP);
+    double* Bs = As + GK * GP;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int c = tid + 256 * s;
+      if (!AK) {
+        const int kk = c >> 6, mm = (c & 63) * 2;
+        *reinterpret_cast<double2*>(As + kk * GP + mm) = ra[s];
+      } else {
+        const int mm = c >> 3, kk = (c & 7) * 2;
+        As[kk * GP + mm] = ra[s].x;
+        As[(kk + 1) * GP + mm] = ra[s].y;
+      }
+      if (!BK) {
+        const int kk = c >> 6, nn = (c & 63) * 2;
+        *reinterpret_cast<double2*>(Bs + kk * GP + nn) = rb[s];
+      } else {
+        const int nn = c >> 3, kk = (c & 7) * 2;
+        Bs[kk * GP + nn] = rb[s].x;
+        Bs[(kk + 1) * GP + nn] = rb[s].y;
+      }
+    }
+  };
+
+  const int nk = (kend - kbeg) / GK;
+  if (nk > 0) {
+    gload(kbeg);
+    sstore(0);
+    __syncthreads();
+    for (int s = 0; s < nk; ++s) {
+      if (s + 1 < nk) gload(kbeg + (s + 1) * GK);
+      const double* As = lds + (s & 1) * (2 * GK * GP);
+      const double* Bs = As + GK * GP;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int krow = ks * 4 + (lane >> 4);
+        double af[4], bf[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = As[krow * GP + wm + i * 16 + (lane & 15)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[j] = Bs[krow * GP + wn + j * 16 + (lane & 15)];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(bf[j], af[i], acc[i][j], 0, 0, 0);
+      }
+      if (s + 1 < nk) sstore((s + 1) & 1);
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = wm + i * 16 + (lane & 15);
+        const int n = wn + j * 16 + mfma64_row(lane, r);
+        Cb[m + (long long)n * P.ldc] = P.alpha * acc[i][j][r];
+      }
+}
+
+// ---------------------------------------------------------------------------
+// skinny products with a lower-triangular (or full) tiled matrix M (ld = ldm):
+//   k_trmm_skinny_n : part[ch] = M[rows it, cols k in chunk] x R[k, 0:P]
+//   k_trmm_skinny_t : part[ch] = M[rows k in chunk, cols it]^T x R[k, 0:P]
+// R column-major (ld = ldr), partials column-major [ch][P][ldp].
+// Chunks of CH k-tiles bound the partial buffer; k_reduce_chunks sums them
+// in a fixed order (bitwise reproducible).
+// ---------------------------------------------------------------------------
+constexpr int SK_CH = 16;
+constexpr int SK_PMAX = 32;
+
+struct SkinnyArgs {
+  const double* M;
+  long long ldm;
+  const double* R;
+  long long ldr;
+  double* part;
+  long long ldp;       // rows of one partial column
+  long long pstride;   // doubles between chunk partials
+  int P, ntr;          // columns of R; number of row tiles of M (k extent, t-kernel)
+  int lower;           // 1: M lower-triangular by tiles
+  int nit;             // output tiles
+  const int* abort_flag;
+};
+
+// grid: blockIdx.x = it + nit * ch
+template <int PM>
+__global__ void __launch_bounds__(256) k_trmm_skinny_n(SkinnyArgs a) {
+  __shared__ double Rs[TILE * PM];
+  __shared__ double red[TILE * PM];
+  if (a.abort_flag && *a.abort_flag) return;
+  const int it = blockIdx.x % a.nit, ch = blockIdx.x / a.nit;
+  const int kt_end_all = a.lower ? it + 1 : a.ntr;
+  const int kt0 = ch * SK_CH;
+  if (kt0 >= kt_end_all) return;
+  const int kt1 = min(kt0 + SK_CH, kt_end_all);
+  const int tid = threadIdx.x, r = tid & (TILE - 1), h = tid >> 7;
+  const int P = a.P;
+  double acc[PM];
+#pragma unroll
+  for (int p = 0; p < PM; ++p) acc[p] = 0.0;
+  for (int kt = kt0; kt < kt1; ++kt) {
+    __syncthreads();
+    for (int e = tid; e < TILE * P; e += 256) {
+      int kk = e & (TILE - 1), p = e >> 7;
+      Rs[kk * PM + p] = a.R[(long long)(kt * TILE + kk) + (long long)p * a.ldr];
+    }
+    __syncthreads();
+    const double* mcol = a.M + (long long)(it * TILE + r) + (long long)(kt * TILE) * a.ldm;
+    for (int kk = h * 64; kk < h * 64 + 64; ++kk) {
+      const double x = mcol[(long long)kk * a.ldm];
+#pragma unroll
+      for (int p = 0; p < PM; ++p)
+        if (p < P) acc[p] = fma(x, Rs[kk * PM + p], acc[p]);
+    }
+  }
+  __syncthreads();
+  if (h == 1) {
+#pragma unroll
+    for (int p = 0; p < PM; ++p) red[r * PM + p] = acc[p];
+  }
+  __syncthreads();
+  if (h == 0) {
+    double* out = a.part + (long long)ch * a.pstride + it * TILE + r;
+#pragma unroll
+    for (int p = 0; p < PM; ++p)
+      if (p < P) out[(long long)p * a.ldp] = acc[p] + red[r * PM + p];
+  }
+}
+
+// grid: blockIdx.x = it + nit * ch ; k tiles: lower ? [it + ch*CH, ...) : [ch*CH, ...)
+template <int PM>
+__global__ void __launch_bounds__(256) k_trmm_skinny_t(SkinnyArgs a) {
+  constexpr int KS = 64;            // k rows staged per pass
+  __shared__ double Ms[TILE * (KS + 1)];   // [col i][k]
+  __shared__ double Rs[KS * PM];
+  __shared__ double red[TILE * PM];
+  if (a.abort_flag && *a.abort_flag) return;
+  const int it = blockIdx.x % a.nit, ch = blockIdx.x / a.nit;
+  const int kbase = a.lower ? it : 0;
+  const int kt0 = kbase + ch * SK_CH;
+  if (kt0 >= a.ntr) return;
+  const int kt1 = min(kt0 + SK_CH, a.ntr);
+  const int tid = threadIdx.x, c = tid & (TILE - 1), h = tid >> 7;
+  const int P = a.P;
+  double acc[PM];
+#pragma unroll
+  for (int p = 0; p < PM; ++p) acc[p] = 0.0;
+  for (int k0 = kt0 * TILE; k0 < kt1 * TILE; k0 += KS) {
+    __syncthreads();
+    // stage M[k0:k0+KS, it*128 : +128] (column i contiguous in k)
+    for (int e = tid; e < TILE * KS; e += 256) {
+      int kk = e & (KS - 1), i = e >> 6;
+      Ms[i * (KS + 1) + kk] = a.M[(long long)(k0 + kk) + (long long)(it * TILE + i) * a.ldm];
+    }
+    for (int e = tid; e < KS * P; e += 256) {
+      int kk = e & (KS - 1), p = e >> 6;
+      Rs[kk * PM + p] = a.R[(long long)(k0 + kk) + (long long)p * a.ldr];
+    }
+    __syncthreads();
+    for (int kk = h * 32; kk < h * 32 + 32; ++kk) {
+      const double x = Ms[c * (KS + 1) + kk];
+#pragma unroll
+      for (int p = 0; p < PM; ++p)
+        if (p < P) acc[p] = fma(x, Rs[kk * PM + p], acc[p]);
+    }
+  }
+  __syncthreads();
+  if (h == 1) {
+#pragma unroll
+    for (int p = 0; p < PM; ++p) red[c * PM + p] = acc[p];
+  }
+  __syncthreads();
+  if (h == 0) {
+    double* out = a.part + (long long)ch * a.pstride + it * TILE + c;
+#pragma unroll
+    for (int p = 0; p < PM; ++p)
+      if (p < P) out[(long long)p * a.ldp] = acc[p] + red[c * PM + p];
+  }
+}
+
+// out[i + p*ldp] = sum_{ch < nch(i)} part[ch][i + p*ldp], fixed order
+// nch(i) for the n-kernel (lower): ceil((it+1)/CH); t-kernel lower: ceil((ntr-it)/CH)
+__global__ void k_reduce_chunks(const double* part, long long pstride, double* out,
+                                long long ldp, int P, int nrows, int ntr, int mode,
+                                const int* abort_flag) {
+  if (abort_flag && *abort_flag) return;
+  long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)nrows * P) return;
+  int i = (int)(e % nrows), p = (int)(e / nrows);
+  int it = i / TILE;
+  int nch;
+  if (mode == 0) nch = (it + SK_CH) / SK_CH;                 // lower, n-kernel
+  else if (mode == 1) nch = (ntr - it + SK_CH - 1) / SK_CH;  // lower, t-kernel
+  else nch = (ntr + SK_CH - 1) / SK_CH;                      // full
+  double s = 0.0;
+  for (int ch = 0; ch < nch; ++ch) s += part[ch * pstride + i + (long long)p * ldp];
+  out[i + (long long)p * ldp] = s;
+}
+
+// ---------------------------------------------------------------------------
+// Gram: part[blk][a*P+b] = sum_{rows in blk} Z(row,a) Z(row,b); rows 256 per block
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_gram(const double* Z, long long ldz, int P, int nrows,
+                                              double* part, const int* abort_flag) {
+  __shared__ double zs[256 * (SK_PMAX + 1)];
+  if (abort_flag && *abort_flag) return;
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * 256;
+  for (int e = tid; e < 256 * P; e += 256) {
+    int rr = e & 255, p = e >> 8;
+    int row = r0 + rr;
+    zs[rr * (SK_PMAX + 1) + p] = (row < nrows) ? Z[row + (long long)p * ldz] : 0.0;
+  }
+  __syncthreads();
+  for (int e = tid; e < P * P; e += 256) {
+    int x = e % P, y = e / P;
+    double s = 0.0;
+    for (int rr = 0; rr < 256; ++rr) s = fma(zs[rr * (SK_PMAX + 1) + x], zs[rr * (SK_PMAX + 1) + y], s);
+    part[(long long)blockIdx.x * P * P + e] = s;
+  }
+}
+
+// out[j] = sum_w part[w*len + j]; one block per j, fixed tree -> reproducible
+__global__ void __launch_bounds__(256) k_reduce_rows(const double* part, int nw, int len,
+                                                     double* out) {
+  __shared__ double red[256];
+  const int j = blockIdx.x, tid = threadIdx.x;
+  double s = 0.0;
+  for (int w = tid; w < nw; w += 256) s += part[(long long)w * len + j];
+  red[tid] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (tid < off) red[tid] += red[tid + off];
+    __syncthreads();
+  }
+  if (tid == 0) out[j] = red[0];
+}
+
+// Y(i, :) = Z(i, :) x T   (T P x Pout column-major, Z/Y column-major)
+__global__ void k_apply_small(const double* Z, long long ldz, int P, const double* T,
+                              int Pout, double* Y, long long ldy, int nrows,
+                              const int* abort_flag) {
+  if (abort_flag && *abort_flag) return;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nrows) return;
+  double z[SK_PMAX];
+#pragma unroll
+  for (int p = 0; p < SK_PMAX; ++p) z[p] = (p < P) ? Z[i + (long long)p * ldz] : 0.0;
+  for (int o = 0; o < Pout; ++o) {
+    double s = 0.0;
+#pragma unroll
+    for (int p = 0; p < SK_PMAX; ++p)
+      if (p < P) s = fma(z[p], T[p + o * P], s);
+    Y[i + (long long)o * ldy] = s;
+  }
+}
+
+// colsum2[j] = sum_i V(i, j)^2  (one wave per column)
+__global__ void __launch_bounds__(256) k_colnorm2(const double* V, long long ldv, int nrows,
+                                                  int ncols, double* out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int j = blockIdx.x * 4 + wave;
+  if (j >= ncols) return;
+  const double* col = V + (long long)j * ldv;
+  double s = 0.0;
+  for (int i = lane; i < nrows; i += 64) s = fma(col[i], col[i], s);
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+  if (lane == 0) out[j] = s;
+}
+
+// ---------------------------------------------------------------------------
+// gradient contraction over the lower tiles of A^-1:
+//   M(i,j) = Ainv(i,j) - sum_p Wa(i,p) Wa(j,p)     (Wa = [sqrt(c) alpha, W], q+1 cols,
+//            column-major, ld = ldw)
+//   off-diagonal (i>j):  accE += M E,  acc_k += M E (x_ik - x_jk)^2 / delta_k^2
+//   diagonal:            accT += M(i,i)
+// E recomputed from the scaled points (no n x n exp cache, no n x n dA).
+// part[blk][0:d] = acc_k, [d] = accE, [d+1] = accT
+// ---------------------------------------------------------------------------
+template <int DMAX, int QMAX>
+__global__ void __launch_bounds__(256) k_contract(const double* Ainv, long long lda,
+                                                  const double* xw, int d,
+                                                  const double* Wa, long long ldw, int q1,
+                                                  int n_valid, double* part,
+                                                  const int* abort_flag) {
+  __shared__ double xs[TILE * DMAX];
+  __shared__ double ws[TILE * QMAX];
+  __shared__ double red[4 * (DMAX + 2)];
+  if (abort_flag && *abort_flag) return;
+  int ti, tj;
+  tri_decode(blockIdx.x, ti, tj);
+  const int tid = threadIdx.x;
+  for (int e = tid; e < TILE * d; e += 256) {
+    int c = e / d, k = e - c * d;
+    xs[c * DMAX + k] = xw[(long long)(tj * TILE + c) * d + k];
+  }
+  for (int e = tid; e < TILE * q1; e += 256) {
+    int c = e / q1, k = e - c * q1;
+    ws[c * QMAX + k] = Wa[(long long)(tj * TILE + c) + (long long)k * ldw];
+  }
+  const int r = tid & (TILE - 1);
+  const int gi = ti * TILE + r;
+  double xi[DMAX], wi[QMAX], acc[DMAX];
+#pragma unroll
+  for (int k = 0; k < DMAX; ++k) {
+    xi[k] = (k < d) ? xw[(long long)gi * d + k] : 0.0;
+    acc[k] = 0.0;
+  }
+#pragma unroll
+  for (int k = 0; k < QMAX; ++k) wi[k] = (k < q1) ? Wa[gi + (long long)k * ldw] : 0.0;
+  double accE = 0.0, accT = 0.0;
+  __syncthreads();
+  if (gi < n_valid) {
+    const double* acol = Ainv + gi + (long long)tj * TILE * lda;
+    const int cend = (ti == tj) ? r + 1 : TILE;
+    for (int c = (tid >> 7); c < cend; c += 2) {
+      const int gj = tj * TILE + c;
+      if (gj >= n_valid) break;
+      double mij = acol[(long long)c * lda];
+#pragma unroll
+      for (int k = 0; k < QMAX; ++k)
+        if (k < q1) mij = fma(-wi[k], ws[c * QMAX + k], mij);
+      if (gj == gi) {
+        accT += mij;
+      } else {
+        double df2[DMAX];
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) {
+          if (k < d) {
+            double df = xi[k] - xs[c * DMAX + k];
+            df2[k] = df * df;
+            s += df2[k];
+          } else {
+            df2[k] = 0.0;
+          }
+        }
+        const double me = mij * exp(-s);
+        accE += me;
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k)
+          if (k < d) acc[k] = fma(me, df2[k], acc[k]);
+      }
+    }
+  }
+  // block reduction, fixed order
+  const int nv = d + 2;
+  const int lane = tid & 63, wave = tid >> 6;
+  for (int k = 0; k < nv; ++k) {
+    double v = 0.0;
+#pragma unroll
+    for (int kk = 0; kk < DMAX; ++kk)
+      if (kk == k) v = acc[kk];
+    if (k == d) v = accE;
+    if (k == d + 1) v = accT;
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if (lane == 0) red[wave * (DMAX + 2) + k] = v;
+  }
+  __syncthreads();
+  if (tid < nv) {
+    const double s = (red[tid] + red[(DMAX + 2) + tid]) +
+                     (red[2 * (DMAX + 2) + tid] + red[3 * (DMAX + 2) + tid]);
+    part[(long long)blockIdx.x * nv + tid] = s;
+  }
+}
+
+// xw(i,k) = X(i,k) / delta_k  for i < n, 0 for padded rows
+__global__ void k_scale_points(const double* X, const double* inv_delta, int d, int n,
+                               int n_pad, double* xw) {
+  long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)n_pad * d) return;
+  int i = (int)(e / d), k = (int)(e % d);
+  xw[e] = (i < n) ? X[e] * inv_delta[k] : 0.0;
+}
+
+// set tile (t,t) of M to the identity for t >= t0 (padding blocks of the inverse)
+__global__ void k_identity_tiles(double* M, long long ld, int t0) {
+  const int t = t0 + blockIdx.x;
+  double* base = M + (long long)t * TILE * (ld + 1);
+  for (int e = threadIdx.x; e < TILE * TILE; e += blockDim.x) {
+    int i = e & (TILE - 1), j = e >> 7;
+    base[i + (long long)j * ld] = (i == j) ? 1.0 : 0.0;
+  }
+}
+
+}  // namespace gpe

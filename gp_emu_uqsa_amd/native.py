@@ -1,0 +1,266 @@
+"""ctypes binding of libgpemu.so (the HIP/gfx950 hot path, include/gpemu.h).
+
+There is no CPU fallback: if the library cannot be loaded, or no GPU is
+visible, every entry point raises ``NativeUnavailable``.  The reference's
+arithmetic (NumPy/SciPy, _emulatorkernels.py / _emulatoroptimise.py /
+_emulatorclasses.py) is replaced here, not mirrored.
+"""
+from __future__ import annotations
+
+import ctypes as _ct
+import os as _os
+import threading as _threading
+
+import numpy as _np
+
+_HERE = _os.path.dirname(_os.path.abspath(__file__))
+LIB_PATH = _os.environ.get("GPEMU_LIB", _os.path.join(_HERE, "libgpemu.so"))
+
+GPE_OK = 0
+GPE_NOT_PD = 1
+KERNEL_STD = 0
+KERNEL_ALT_NUG = 1
+GP4ML = 0
+MUCM = 1
+
+_D = _ct.POINTER(_ct.c_double)
+_VP = _ct.c_void_p
+
+# name -> (restype, argtypes); the full exported surface of include/gpemu.h
+SIGNATURES = {
+    "gpe_abi_version": (_ct.c_int, []),
+    "gpe_device_count": (_ct.c_int, []),
+    "gpe_create": (_VP, [_ct.c_int32]),
+    "gpe_destroy": (None, [_VP]),
+    "gpe_last_error": (_ct.c_char_p, [_VP]),
+    "gpe_set_data": (_ct.c_int, [_VP, _ct.c_int64, _ct.c_int32, _ct.c_int32, _D, _D, _D, _D]),
+    "gpe_objective": (_ct.c_int, [_VP, _ct.c_int32, _ct.c_int32, _D, _ct.c_int32, _ct.c_double,
+                                  _ct.c_int32, _D, _D, _D]),
+    "gpe_factor": (_ct.c_int, [_VP, _ct.c_int32, _D, _ct.c_double, _ct.c_double, _ct.c_double]),
+    "gpe_beta": (_ct.c_int, [_VP, _D]),
+    "gpe_posterior": (_ct.c_int, [_VP, _ct.c_int64, _D, _D, _D, _ct.c_double, _ct.c_int32, _D, _D]),
+    "gpe_kernel_var": (_ct.c_int, [_VP, _ct.c_int32, _D, _ct.c_int32, _ct.c_double, _ct.c_int32,
+                                   _ct.c_int64, _D, _D, _ct.c_double, _D]),
+    "gpe_kernel_covar": (_ct.c_int, [_VP, _ct.c_int32, _D, _ct.c_int32, _ct.c_double, _ct.c_int64,
+                                     _D, _ct.c_int64, _D, _D]),
+    "gpe_cholesky": (_ct.c_int, [_VP, _ct.c_int64, _D, _D, _D, _D, _D]),
+    "gpe_test_gemm": (_ct.c_int, [_VP, _ct.c_int32, _ct.c_int32, _ct.c_int64, _ct.c_int64,
+                                  _ct.c_int64, _D, _D, _D, _ct.c_double, _ct.c_double]),
+    "gpe_set_profiling": (_ct.c_int, [_VP, _ct.c_int32]),
+    "gpe_phase_times": (_ct.c_int, [_VP, _D, _ct.c_int32]),
+    "gpe_gemm_stats": (_ct.c_int, [_VP, _D, _D, _D]),
+}
+
+
+class NativeUnavailable(RuntimeError):
+    """libgpemu.so is missing or no HIP device is visible (no CPU fallback)."""
+
+
+class NotPositiveDefinite(ArithmeticError):
+    """Cholesky met a non-positive / NaN pivot (the reference's LinAlgError)."""
+
+
+_lib = None
+_lib_lock = _threading.Lock()
+
+
+def load_library(path: str | None = None):
+    """Load and type the shared library (idempotent)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not _os.path.exists(p):
+            raise NativeUnavailable(
+                f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        lib = _ct.CDLL(p)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    return a.ctypes.data_as(_D)
+
+
+def _f64(a, shape=None):
+    arr = _np.ascontiguousarray(a, dtype=_np.float64)
+    if shape is not None:
+        arr = arr.reshape(shape)
+    return arr
+
+
+class Context:
+    """One GPU, one HIP stream, resident training data (gpe_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        if self.lib.gpe_device_count() <= 0:
+            raise NativeUnavailable("no HIP device visible to libgpemu.so")
+        h = self.lib.gpe_create(int(device))
+        if not h:
+            raise NativeUnavailable("gpe_create failed: " + self.lib.gpe_last_error(None).decode())
+        self._h = h
+        self.device = device
+        self.n = self.d = self.q = 0
+
+    # -- lifetime
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.gpe_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc == GPE_OK:
+            return
+        msg = self.lib.gpe_last_error(self._h).decode()
+        if rc == GPE_NOT_PD:
+            raise NotPositiveDefinite(f"{what}: {msg}")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+    # -- data
+    def set_data(self, X, f, H, r=None):
+        X = _f64(X)
+        if X.ndim == 1:
+            X = X.reshape(-1, 1)
+        n, d = X.shape
+        f = _f64(f, (n,))
+        H = _f64(H)
+        if H.ndim == 1:
+            H = H.reshape(n, -1)
+        q = H.shape[1]
+        rr = None if r is None or _np.isscalar(r) else _f64(r, (n,))
+        self._keep = (X, f, H, rr)
+        self._check(self.lib.gpe_set_data(self._h, n, d, q, _ptr(X), _ptr(f), _ptr(H), _ptr(rr)),
+                    "gpe_set_data")
+        self.n, self.d, self.q = n, d, q
+
+    # -- objective
+    def objective(self, variant, kernel, hp, nu_fixed=0.0, want_grad=True):
+        """Returns (llh, grad or None, sigma2); raises NotPositiveDefinite."""
+        hp = _f64(hp).ravel()
+        llh = _ct.c_double(0.0)
+        s2 = _ct.c_double(0.0)
+        grad = _np.zeros(hp.size) if want_grad else None
+        rc = self.lib.gpe_objective(self._h, int(variant), int(kernel), _ptr(hp), hp.size,
+                                    float(nu_fixed), 1 if want_grad else 0, _ct.byref(llh),
+                                    _ptr(grad), _ct.byref(s2))
+        self._check(rc, "gpe_objective")
+        return llh.value, grad, s2.value
+
+    def factor(self, kernel, delta, nu, s2=1.0, r_scale=0.0):
+        delta = _f64(delta).ravel()
+        self._check(self.lib.gpe_factor(self._h, int(kernel), _ptr(delta), float(nu), float(s2),
+                                        float(r_scale)), "gpe_factor")
+
+    def beta(self):
+        out = _np.zeros(self.q)
+        self._check(self.lib.gpe_beta(self._h, _ptr(out)), "gpe_beta")
+        return out
+
+    def posterior(self, Xs, Hs, beta, sigma, full_var=True):
+        Xs = _f64(Xs)
+        if Xs.ndim == 1:
+            Xs = Xs.reshape(-1, 1)
+        m = Xs.shape[0]
+        Hs = _f64(Hs, (m, self.q))
+        beta = _f64(beta).ravel()
+        mean = _np.zeros(m)
+        var = _np.zeros((m, m)) if full_var else _np.zeros(m)
+        self._check(self.lib.gpe_posterior(self._h, m, _ptr(Xs), _ptr(Hs), _ptr(beta), float(sigma),
+                                           1 if full_var else 0, _ptr(mean), _ptr(var)),
+                    "gpe_posterior")
+        return mean, var
+
+    def kernel_var(self, kernel, delta, nu, X, predict=True, r=None, r_scale=0.0):
+        X = _f64(X)
+        if X.ndim == 1:
+            X = X.reshape(-1, 1)
+        m, d = X.shape
+        delta = _f64(delta).ravel()
+        rr = None if r is None or _np.isscalar(r) else _f64(r, (m,))
+        out = _np.zeros((m, m))
+        self._check(self.lib.gpe_kernel_var(self._h, int(kernel), _ptr(delta), d, float(nu),
+                                            1 if predict else 0, m, _ptr(X), _ptr(rr),
+                                            float(r_scale), _ptr(out)), "gpe_kernel_var")
+        return out
+
+    def kernel_covar(self, kernel, delta, nu, XT, XV):
+        XT = _f64(XT)
+        XV = _f64(XV)
+        if XT.ndim == 1:
+            XT = XT.reshape(-1, 1)
+        if XV.ndim == 1:
+            XV = XV.reshape(-1, 1)
+        n, d = XT.shape
+        m = XV.shape[0]
+        delta = _f64(delta).ravel()
+        out = _np.zeros((n, m))
+        self._check(self.lib.gpe_kernel_covar(self._h, int(kernel), _ptr(delta), d, float(nu), n,
+                                              _ptr(XT), m, _ptr(XV), _ptr(out)), "gpe_kernel_covar")
+        return out
+
+    def cholesky(self, A, want=("L",)):
+        A = _f64(A)
+        m = A.shape[0]
+        outs = {k: _np.zeros((m, m)) for k in want if k in ("L", "Linv", "Ainv")}
+        ld = _ct.c_double(0.0)
+        self._check(self.lib.gpe_cholesky(self._h, m, _ptr(A), _ptr(outs.get("L")),
+                                          _ptr(outs.get("Linv")), _ptr(outs.get("Ainv")),
+                                          _ct.byref(ld)), "gpe_cholesky")
+        outs["logdet"] = ld.value
+        return outs
+
+    def test_gemm(self, A, B, C, alpha=1.0, beta=0.0, trans_a=0, trans_b=0):
+        A = _f64(A)
+        B = _f64(B)
+        C = _f64(C).copy()
+        M, K = A.shape
+        N = B.shape[1]
+        self._check(self.lib.gpe_test_gemm(self._h, int(trans_a), int(trans_b), M, N, K, _ptr(A),
+                                           _ptr(B), _ptr(C), float(alpha), float(beta)),
+                    "gpe_test_gemm")
+        return C
+
+    # -- profiling
+    def set_profiling(self, on=True):
+        self._check(self.lib.gpe_set_profiling(self._h, 1 if on else 0), "gpe_set_profiling")
+
+    def phase_times(self):
+        out = _np.zeros(8)
+        self._check(self.lib.gpe_phase_times(self._h, _ptr(out), 8), "gpe_phase_times")
+        keys = ["kbuild", "cholesky", "trtri", "inverse", "skinny", "contract", "total"]
+        return dict(zip(keys, out[:7].tolist()))
+
+    def gemm_stats(self):
+        ms, nl, fl = _ct.c_double(), _ct.c_double(), _ct.c_double()
+        self._check(self.lib.gpe_gemm_stats(self._h, _ct.byref(ms), _ct.byref(nl), _ct.byref(fl)),
+                    "gpe_gemm_stats")
+        return {"ms": ms.value, "launches": nl.value, "flops": fl.value}
+
+
+_default_ctx = None
+_ctx_lock = _threading.Lock()
+
+
+def default_context() -> Context:
+    """Process-wide context on the GPU chosen by LOCAL_RANK (or 0)."""
+    global _default_ctx
+    with _ctx_lock:
+        if _default_ctx is None:
+            dev = int(_os.environ.get("GPEMU_DEVICE", _os.environ.get("LOCAL_RANK", "0")))
+            _default_ctx = Context(dev)
+        return _default_ctx

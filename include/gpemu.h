@@ -1,0 +1,142 @@
+/*
+ * gpemu.h -- C-ABI of libgpemu.so, the MI355X (gfx950) GP-emulator hot path.
+ *
+ * The reference (MathThyMod/GP_emu_UQSA) is pure Python and has no FFI: its
+ * seams are duck-typed Python objects.  Each entry point below
+ * replaces one of them; the reference interface it stands in for is cited.
+ * The library is bound by the package's own ctypes layer
+ * (gp_emu_uqsa_amd/native.py); INTEGRATION.md shows the binding a reference
+ * maintainer would add.
+ *
+ * Conventions
+ *  - All host buffers are caller-owned, C-contiguous (row-major) fp64 and are
+ *    only read/written during the call.  Device buffers belong to the context.
+ *  - Calls are synchronous: the context's HIP stream is drained before return.
+ *  - One context per host thread, one GPU per context.  No callbacks.
+ *  - Return codes: GPE_OK (0); GPE_NOT_PD (1) = Cholesky met a non-positive or
+ *    NaN pivot -- the host maps it to the reference's `return None`
+ *    (_emulatoroptimise.py:374-376, :489-491); negative = error, text in
+ *    gpe_last_error().
+ *  - Hyperparameters are UNtransformed (delta, nu, sigma); transform /
+ *    untransform x = 2 log(hp) stays on the host (_emulatorkernels.py:31-36).
+ */
+#ifndef GPEMU_H
+#define GPEMU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPE_ABI_VERSION 1
+
+enum gpe_status {
+    GPE_OK = 0,
+    GPE_NOT_PD = 1,
+    GPE_ERR_ARG = -1,
+    GPE_ERR_HIP = -2,
+    GPE_ERR_ALLOC = -3,
+    GPE_ERR_STATE = -4,
+    GPE_ERR_UNSUPPORTED = -5
+};
+
+/* kernel family: _emulatorkernels.py:10 (kernel) and :83 (kernel_alt_nug) */
+enum gpe_kernel { GPE_KERNEL_STD = 0, GPE_KERNEL_ALT_NUG = 1 };
+/* objective: _emulatoroptimise.py:412 (gp4ml) and :305 (mucm) */
+enum gpe_variant { GPE_GP4ML = 0, GPE_MUCM = 1 };
+
+typedef struct gpe_ctx gpe_ctx;
+
+int gpe_abi_version(void);
+int gpe_device_count(void);
+
+/* Create a context on one GPU (device index as HIP sees it). NULL on failure;
+ * the reason is then available from gpe_last_error(NULL). */
+gpe_ctx* gpe_create(int32_t device);
+void gpe_destroy(gpe_ctx* ctx);
+const char* gpe_last_error(const gpe_ctx* ctx);
+
+/* Training data: replaces Data.inputs/.outputs/.H/.r (_emulatorclasses.py:540-550,
+ * :577-584).  X n x d (already active-column-selected and [0,1]-scaled, as
+ * All_Data leaves it), f n, H n x q, r n or NULL (r = 0).  Copies to HBM. */
+int gpe_set_data(gpe_ctx* ctx, int64_t n, int32_t d, int32_t q,
+                 const double* X, const double* f, const double* H, const double* r);
+
+/* Objective: replaces Optimize.loglikelihood_gp4ml (_emulatoroptimise.py:412-493)
+ * and Optimize.loglikelihood_mucm (:305-378).
+ * hp = untransformed [delta(d), nu (if fitted), sigma (gp4ml only)], n_hp its
+ * length; the nugget is fitted iff n_hp == d+2 (gp4ml) / d+1 (mucm), exactly the
+ * reference's `x.size` test (:463, :360).  nu_fixed is used otherwise.
+ * Outputs: *llh_out = the reference's LLH (negative log marginal likelihood);
+ * grad_out (n_hp, may be NULL when want_grad == 0) = its gradient w.r.t.
+ * x = 2 log(hp), including the MUCM sigma-hat^2 scaling the reference applies;
+ * *sigma2_out = sigma^2 (gp4ml) or the analytic sigma-hat^2 (mucm, :324-327). */
+int gpe_objective(gpe_ctx* ctx, int32_t variant, int32_t kernel,
+                  const double* hp, int32_t n_hp, double nu_fixed, int32_t want_grad,
+                  double* llh_out, double* grad_out, double* sigma2_out);
+
+/* Factor A = s2 * K.var(X_train, predict=True) + r_scale * diag(r) and keep the
+ * Cholesky factor and its inverse resident for gpe_beta / gpe_posterior.
+ * Replaces the factorisations inside Optimize.optimalbeta (:497-504) and the
+ * three scipy.linalg.solve(A, .) LU solves of Posterior (_emulatorclasses.py:613,
+ * :623, :628).  r_scale is 1/s2 after training's make_A(s2) and 1 after remake(). */
+int gpe_factor(gpe_ctx* ctx, int32_t kernel, const double* delta, double nu,
+               double s2, double r_scale);
+
+/* GLS beta = Q^-1 H^T A^-1 f with the resident factor (optimalbeta, :497-504). */
+int gpe_beta(gpe_ctx* ctx, double* beta_out);
+
+/* Posterior at m points: replaces Posterior.make_covar/make_mean/make_var
+ * (_emulatorclasses.py:607-631) with the resident factor.  Xs m x d, Hs m x q.
+ * mean_out m; var_out m x m when full_var != 0 (m <= 16384), else its diagonal
+ * (m values).  sigma is par.sigma. */
+int gpe_posterior(gpe_ctx* ctx, int64_t m, const double* Xs, const double* Hs,
+                  const double* beta, double sigma, int32_t full_var,
+                  double* mean_out, double* var_out);
+
+/* K.var(X, predict) materialised (m x m, symmetric): _emulatorkernels.py:39-50 /
+ * :112-123, plus make_A's r/s2 diagonal (r_scale * r, r may be NULL). */
+int gpe_kernel_var(gpe_ctx* ctx, int32_t kernel, const double* delta, int32_t d,
+                   double nu, int32_t predict, int64_t m, const double* X,
+                   const double* r, double r_scale, double* A_out);
+
+/* K.covar(XT, XV) -> n x m row-major: _emulatorkernels.py:75-79 / :148-152. */
+int gpe_kernel_covar(gpe_ctx* ctx, int32_t kernel, const double* delta, int32_t d,
+                     double nu, int64_t n, const double* XT, int64_t m,
+                     const double* XV, double* C_out);
+
+/* Cholesky factor, inverse factor and inverse of an arbitrary SPD matrix
+ * (row-major m x m, lower triangle read).  Replaces the np.linalg.cholesky of the
+ * posterior covariance in posterior_sample (emulatorfunctions.py:283) and serves
+ * as the unit-test entry of the blocked factorisation.  Any output may be NULL.
+ * L_out / Linv_out are lower-triangular with zero upper part. */
+int gpe_cholesky(gpe_ctx* ctx, int64_t m, const double* A, double* L_out,
+                 double* Linv_out, double* Ainv_out, double* logdet_out);
+
+/* Test hook for the grouped MFMA GEMM building block on one problem:
+ * C = alpha * opA x opB + beta * C with opA M x K, opB K x N (row-major host
+ * arrays A (M x K), B (K x N), C (M x N)); trans_a / trans_b choose the device
+ * storage orientation exercised (0: M-/N-contiguous, 1: K-contiguous).
+ * M, N multiples of 128, K multiple of 16. */
+int gpe_test_gemm(gpe_ctx* ctx, int32_t trans_a, int32_t trans_b, int64_t M, int64_t N,
+                  int64_t K, const double* A, const double* B, double* C,
+                  double alpha, double beta);
+
+/* Per-phase device time of the most recent gpe_objective call, in ms:
+ * [0] K-build, [1] Cholesky, [2] triangular inverse, [3] A^-1 (L^-T L^-1),
+ * [4] skinny solves / small algebra, [5] gradient contraction, [6] total.
+ * Only filled when profiling is on. */
+int gpe_set_profiling(gpe_ctx* ctx, int32_t on);
+int gpe_phase_times(gpe_ctx* ctx, double* ms_out, int32_t n);
+
+/* Aggregate device time (ms) and call count of the MFMA GEMM launches of the most
+ * recent objective (profiling on), and their algorithmic flop count. */
+int gpe_gemm_stats(gpe_ctx* ctx, double* ms_out, double* launches_out,
+                   double* flops_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GPEMU_H */

@@ -1,0 +1,267 @@
+"""Generate golden vectors by running the REFERENCE (GP_emu_UQSA) in the build
+container.  The reference never travels: only the .npz outputs are committed.
+
+Run from the repo root:  python tests/golden/make_golden.py [G1 G2 G3 G4 G5]
+
+Fixtures:
+  G1 kernel_*.npz      K.var / covar / grad_delta_A / grad_nugget_A, both kernels
+  G2 objective_*.npz   loglikelihood_gp4ml / _mucm (LLH, grad) incl. a non-PD case
+  G3 posterior_*.npz   reconstructed example emulators: posterior mean/var, beta
+  G4 train_*.npz       seeded toy-sim g.train() trajectory (objective x's, result)
+  G5 scale_4096.npz    n=4096 d=10 gp4ml LLH+grad (X regenerated from the seed)
+Versions of numpy/scipy used are stored in every file ("meta").
+"""
+from __future__ import annotations
+
+import contextlib
+import io
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+import types
+
+import numpy as np
+import scipy
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REF)
+sys.path.insert(0, REPO)
+os.environ.setdefault("MPLBACKEND", "Agg")
+
+with contextlib.redirect_stdout(io.StringIO()):
+    import gp_emu_uqsa as g                              # noqa: E402
+    import gp_emu_uqsa._emulatorkernels as emuk          # noqa: E402
+    import gp_emu_uqsa._emulatorclasses as emuc          # noqa: E402
+    import gp_emu_uqsa._emulatoroptimise as emuo         # noqa: E402
+
+from oracle import gp_oracle as orc                      # noqa: E402  (synthetic data only)
+
+META = json.dumps({"numpy": np.__version__, "scipy": scipy.__version__,
+                   "reference": "GP_emu_UQSA @ /root/reference",
+                   "generated": time.strftime("%Y-%m-%d")})
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, meta=np.array(META), **arrays)
+    print("wrote", path, {k: np.shape(v) for k, v in arrays.items()})
+
+
+def quiet(fn, *a, **k):
+    with contextlib.redirect_stdout(io.StringIO()):
+        return fn(*a, **k)
+
+
+# ---------------------------------------------------------------- helpers
+def ref_kernel(kind, delta, nu):
+    par = types.SimpleNamespace(delta=np.array(delta, float), nugget=nu)
+    cls = emuk.kernel_alt_nug if kind == orc.ALT else emuk.kernel
+    return cls(len(delta), par)
+
+
+def ref_data(X, f, kind, delta, nu, r=None):
+    """A real reference Data object with a linear basis 1, x_0..x_{d-1}."""
+    d = X.shape[1]
+    basis = types.SimpleNamespace(h=[lambda x: 1.0] + [lambda x: x] * d,
+                                  basis_inf=list(range(d)))
+    beliefs = types.SimpleNamespace(alt_nugget="T" if kind == orc.ALT else "F")
+    par = types.SimpleNamespace(beta=np.zeros(d + 1), delta=np.array(delta, float),
+                                nugget=nu, sigma=1.0)
+    K = ref_kernel(kind, delta, nu)
+    data = emuc.Data(X.copy(), f.copy(), basis, par, beliefs, K)
+    if r is not None:
+        data.set_r(np.asarray(r, float), message=False)
+    return data, par
+
+
+def ref_objective(X, f, kind, variant, fit_nugget, hp, nu_fixed, r=None):
+    d = X.shape[1]
+    delta = list(hp[:d])
+    nu = hp[d] if fit_nugget else nu_fixed
+    data, par = ref_data(X, f, kind, delta, nu, r)
+    self = types.SimpleNamespace(data=data, par=par)
+    x = 2.0 * np.log(np.asarray(hp, float))
+    fn = emuo.Optimize.loglikelihood_gp4ml if variant == orc.GP4ML else \
+        emuo.Optimize.loglikelihood_mucm
+    out = quiet(fn, self, x)
+    if out is None:
+        return None
+    llh, grad = out
+    sig2 = par.sigma ** 2
+    return float(llh), np.array(grad, float), float(sig2), data.H.copy()
+
+
+# ---------------------------------------------------------------- G1
+def make_g1():
+    rs = np.random.RandomState(11)
+    X = rs.uniform(size=(64, 3))
+    Xs = rs.uniform(size=(16, 3))
+    delta = np.array([0.7, 0.35, 1.3])
+    for kind, tag in ((orc.STD, "std"), (orc.ALT, "alt")):
+        nu = 0.05
+        K = ref_kernel(kind, delta, nu)
+        A_pred = K.var(X, True).copy()
+        A_est = K.var(X, False).copy()
+        e = K.exp_save.copy()
+        gd = np.stack([K.grad_delta_A(X[:, i], i, 1.7) for i in range(3)])
+        gn = K.grad_nugget_A(X, 1.7)
+        cov = K.covar(X, Xs)
+        save(f"kernel_{tag}.npz", X=X, Xs=Xs, delta=delta, nu=nu, s2=1.7,
+             A_pred=A_pred, A_est=A_est, exp_save=e, grad_delta=gd,
+             grad_nugget=gn, covar=cov)
+
+
+# ---------------------------------------------------------------- G2
+G2_CASES = [
+    # (tag, kind, variant, fit_nugget, use_r)
+    ("std_gp4ml_fitnug", orc.STD, orc.GP4ML, True, False),
+    ("std_gp4ml_fixnug", orc.STD, orc.GP4ML, False, False),
+    ("std_mucm_fitnug", orc.STD, orc.MUCM, True, False),
+    ("std_mucm_fixnug", orc.STD, orc.MUCM, False, False),
+    ("alt_gp4ml_fitnug", orc.ALT, orc.GP4ML, True, False),
+    ("alt_gp4ml_fixnug", orc.ALT, orc.GP4ML, False, False),
+    ("alt_gp4ml_fitnug_r", orc.ALT, orc.GP4ML, True, True),
+]
+
+
+def g2_hp(d, variant, fit_nugget, delta, nu, sigma):
+    hp = list(np.full(d, delta) if np.isscalar(delta) else delta)
+    if fit_nugget:
+        hp.append(nu)
+    if variant == orc.GP4ML:
+        hp.append(sigma)
+    return np.array(hp, float)
+
+
+def make_g2():
+    for (n, d) in ((200, 3), (1024, 10)):
+        X, f, _ = orc.synthetic_problem(n, d, seed=3)
+        rs = np.random.RandomState(5)
+        r = 0.01 * rs.uniform(size=n)
+        out = {"X": X, "f": f, "r": r}
+        points = [(1.0, 1e-3, 1.0), (np.linspace(0.3, 1.2, d), 2e-2, 0.7)]
+        for tag, kind, variant, fitn, use_r in G2_CASES:
+            for pi, (delta, nu, sigma) in enumerate(points):
+                hp = g2_hp(d, variant, fitn, delta, nu, sigma)
+                t0 = time.time()
+                res = ref_objective(X, f, kind, variant, fitn, hp, nu, r if use_r else None)
+                key = f"{tag}_p{pi}"
+                out[key + "_hp"] = hp
+                out[key + "_nufixed"] = np.array(nu)
+                out[key + "_llh"] = np.array(res[0])
+                out[key + "_grad"] = res[1]
+                out[key + "_sig2"] = np.array(res[2])
+                print(f"  n={n} {key} llh={res[0]:.10g} ({time.time()-t0:.1f}s)")
+        # non-PD: huge length scales, zero nugget -> numerically singular A
+        hp = g2_hp(d, orc.GP4ML, False, 200.0, 0.0, 1.0)
+        res = ref_objective(X, f, orc.STD, orc.GP4ML, False, hp, 0.0)
+        assert res is None, "expected the reference to report non-PD"
+        out["nonpd_hp"] = hp
+        save(f"objective_n{n}_d{d}.npz", **out)
+
+
+# ---------------------------------------------------------------- G3
+RECON = [
+    ("toysim", "examples/toy-sim/reconstruct", "toy-sim_config_recon", 2),
+    ("toysim3d_o0", "examples/sensitivity_multi_outputs/sensitivity_recon",
+     "toysim3D_config0_recon", 3),
+    ("toysim3d_o1", "examples/sensitivity_multi_outputs/sensitivity_recon",
+     "toysim3D_config1_recon", 3),
+]
+
+
+def make_g3():
+    for tag, sub, conf, d in RECON:
+        tmp = tempfile.mkdtemp()
+        shutil.copytree(os.path.join(REF, sub), os.path.join(tmp, "w"))
+        cwd = os.getcwd()
+        os.chdir(os.path.join(tmp, "w"))
+        try:
+            E = quiet(g.setup, conf, datashuffle=False, scaleinputs=True)
+            rs = np.random.RandomState(17)
+            xs = rs.uniform(size=(20, d))
+            mean, var = quiet(g.posterior, E, xs)
+            beta_stored = E.par.beta.copy()
+            A = E.training.A.copy()
+            quiet(E.opt_T.optimalbeta)
+            beta_opt = E.par.beta.copy()
+            out = dict(XT=E.training.inputs, fT=E.training.outputs, HT=E.training.H,
+                       xs=xs, mean=mean, var=var, A_trace=np.trace(A), A_sum=A.sum(),
+                       beta=beta_stored, beta_opt=beta_opt,
+                       delta=np.array(E.par.delta, float), nu=np.array(E.par.nugget),
+                       sigma=np.array(E.par.sigma),
+                       alt=np.array(E.beliefs.alt_nugget == "T"),
+                       mucm=np.array(E.beliefs.mucm == "T"),
+                       fix_nugget=np.array(E.beliefs.fix_nugget == "T"))
+            save(f"posterior_{tag}.npz", **out)
+        finally:
+            os.chdir(cwd)
+            shutil.rmtree(tmp)
+
+
+# ---------------------------------------------------------------- G4
+def make_g4():
+    for seed in (0, 1):
+        tmp = tempfile.mkdtemp()
+        shutil.copytree(os.path.join(REF, "examples/toy-sim"), os.path.join(tmp, "w"))
+        cwd = os.getcwd()
+        os.chdir(os.path.join(tmp, "w"))
+        try:
+            np.random.seed(seed)
+            E = quiet(g.setup, "toy-sim_config")
+            calls = []
+            orig = E.opt_T.loglikelihood_mucm
+
+            def rec(x, _orig=orig):
+                res = _orig(x)
+                calls.append((np.array(x, float), None if res is None else res[0]))
+                return res
+            E.opt_T.loglikelihood_mucm = rec
+            log = io.StringIO()
+            with contextlib.redirect_stdout(log):
+                g.train(E, auto=True)
+            xs = np.array([c[0] for c in calls])
+            ll = np.array([np.nan if c[1] is None else c[1] for c in calls])
+            beliefs = {}
+            for fn in sorted(os.listdir(".")):
+                if fn.startswith("toy-sim_beliefs-"):
+                    beliefs[fn] = open(fn).read()
+            rs = np.random.RandomState(23)
+            xs_post = rs.uniform(size=(10, 2))
+            pm, pv = quiet(g.posterior, E, xs_post)
+            save(f"train_toysim_seed{seed}.npz", call_x=xs, call_llh=ll,
+                 delta=np.array(E.par.delta, float), sigma=np.array(E.par.sigma),
+                 nugget=np.array(E.par.nugget), beta=np.array(E.par.beta, float),
+                 n_train=np.array(E.training.inputs.shape[0]),
+                 beliefs_json=np.array(json.dumps(beliefs)),
+                 xs_post=xs_post, post_mean=pm, post_var=pv,
+                 log=np.array(log.getvalue()))
+        finally:
+            os.chdir(cwd)
+            shutil.rmtree(tmp)
+
+
+# ---------------------------------------------------------------- G5
+def make_g5():
+    n, d = 4096, 10
+    X, f, _ = orc.synthetic_problem(n, d, seed=0)
+    hp = g2_hp(d, orc.GP4ML, True, 1.0, 1e-3, 1.0)
+    t0 = time.time()
+    res = ref_objective(X, f, orc.STD, orc.GP4ML, True, hp, 1e-3)
+    dt = time.time() - t0
+    print(f"  G5 llh={res[0]:.12g} in {dt:.1f}s")
+    save("scale_4096.npz", seed=np.array(0), n=np.array(n), d=np.array(d), hp=hp,
+         X_sum=X.sum(), X_sq=(X ** 2).sum(), f_sum=f.sum(), llh=np.array(res[0]),
+         grad=res[1], seconds=np.array(dt))
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["G1", "G2", "G3", "G4", "G5"]
+    for w in which:
+        print("==", w)
+        {"G1": make_g1, "G2": make_g2, "G3": make_g3, "G4": make_g4, "G5": make_g5}[w]()

@@ -1,0 +1,107 @@
+"""GPU parity of the objective (LLH + gradient) against the reference's golden
+vectors (tests/golden, produced by make_golden.py from GP_emu_UQSA itself).
+
+Tolerances (fp64 end to end): LLH relative max(1e-10, 4 eps cond(A)); gradient
+|g - g_ref| <= 1e-7 * (|g_ref| + max|g_ref|)  -- the gradient components are
+differences of O(n) trace terms, so the bound is relative to the largest one.
+The cond(A) term matters only for the alt-nugget point with nu^2 = 1e-6 on the
+diagonal (cond 1.3e8): there LAPACK's own Cholesky of A and of A padded to 256
+(identity block) already differ by 2.6e-10 relative in LLH, so 1e-10 is below
+the problem's rounding floor.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from gp_emu_uqsa_amd import native
+from oracle import gp_oracle as orc
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+CASES = [
+    ("std_gp4ml_fitnug", orc.STD, orc.GP4ML, True, False),
+    ("std_gp4ml_fixnug", orc.STD, orc.GP4ML, False, False),
+    ("std_mucm_fitnug", orc.STD, orc.MUCM, True, False),
+    ("std_mucm_fixnug", orc.STD, orc.MUCM, False, False),
+    ("alt_gp4ml_fitnug", orc.ALT, orc.GP4ML, True, False),
+    ("alt_gp4ml_fixnug", orc.ALT, orc.GP4ML, False, False),
+    ("alt_gp4ml_fitnug_r", orc.ALT, orc.GP4ML, True, True),
+]
+
+
+def _cond(X, hp, kind, variant, fitn, nu_fixed):
+    d = X.shape[1]
+    delta, nu, _ = orc.split_hp(hp, d, variant, fitn)
+    A, _ = orc.kernel_var_ref(X, delta, nu if nu is not None else nu_fixed, kind, True)
+    return np.linalg.cond(A)
+
+
+def _grad_ok(g, gref, tol=1e-7):
+    scale = np.abs(gref) + np.max(np.abs(gref))
+    return np.all(np.abs(g - gref) <= tol * scale), np.max(np.abs(g - gref) / scale)
+
+
+@pytest.mark.parametrize("fname", ["objective_n200_d3.npz", "objective_n1024_d10.npz"])
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("point", [0, 1])
+def test_objective_golden(ctx, fname, case, point):
+    z = np.load(os.path.join(GOLD, fname))
+    tag, kind, variant, fitn, use_r = case
+    X, f = z["X"], z["f"]
+    H = orc.linear_basis(X)
+    ctx.set_data(X, f, H, z["r"] if use_r else None)
+    key = f"{tag}_p{point}"
+    hp = z[key + "_hp"]
+    llh, grad, s2 = ctx.objective(variant, kind, hp, nu_fixed=float(z[key + "_nufixed"]))
+    ref = float(z[key + "_llh"])
+    rtol = max(1e-10, 4 * np.finfo(float).eps * _cond(X, hp, kind, variant, fitn,
+                                                      float(z[key + "_nufixed"])))
+    assert abs(llh - ref) <= rtol * max(1.0, abs(ref)), (llh, ref, rtol)
+    ok, err = _grad_ok(grad, z[key + "_grad"])
+    assert ok, (err, grad, z[key + "_grad"])
+    assert abs(s2 - float(z[key + "_sig2"])) <= 1e-10 * abs(float(z[key + "_sig2"]))
+
+
+@pytest.mark.parametrize("fname", ["objective_n200_d3.npz", "objective_n1024_d10.npz"])
+def test_objective_not_pd(ctx, fname):
+    z = np.load(os.path.join(GOLD, fname))
+    X, f = z["X"], z["f"]
+    ctx.set_data(X, f, orc.linear_basis(X))
+    with pytest.raises(native.NotPositiveDefinite):
+        ctx.objective(orc.GP4ML, orc.STD, z["nonpd_hp"], nu_fixed=0.0)
+
+
+def test_objective_value_only_matches(ctx):
+    X, f, H = orc.synthetic_problem(500, 4, seed=9)
+    ctx.set_data(X, f, H)
+    hp = np.array([0.5, 0.7, 0.9, 1.1, 1e-3, 1.3])
+    a = ctx.objective(orc.GP4ML, orc.STD, hp, want_grad=True)
+    b = ctx.objective(orc.GP4ML, orc.STD, hp, want_grad=False)
+    assert a[0] == b[0] and b[1] is None
+
+
+def test_scale_point_4096(ctx):
+    """G5: n=4096, d=10 gp4ml at the measurement point (reference: ~42 s on CPU)."""
+    z = np.load(os.path.join(GOLD, "scale_4096.npz"))
+    X, f, H = orc.synthetic_problem(int(z["n"]), int(z["d"]), seed=int(z["seed"]))
+    assert abs(X.sum() - float(z["X_sum"])) < 1e-9 and abs(f.sum() - float(z["f_sum"])) < 1e-9
+    ctx.set_data(X, f, H)
+    llh, grad, _ = ctx.objective(orc.GP4ML, orc.STD, z["hp"])
+    assert abs(llh - float(z["llh"])) <= 1e-10 * abs(float(z["llh"])), (llh, float(z["llh"]))
+    ok, err = _grad_ok(grad, z["grad"], tol=1e-6)
+    assert ok, (err, grad, z["grad"])
+
+
+@pytest.mark.parametrize("n,d", [(129, 2), (383, 5), (640, 20)])
+def test_objective_vs_oracle_ragged(ctx, n, d):
+    """Sizes that are not multiples of the 128 tile (padding path), d up to 20."""
+    X, f, H = orc.synthetic_problem(n, d, seed=n)
+    ctx.set_data(X, f, H)
+    hp = np.concatenate([np.linspace(0.4, 1.2, d), [5e-3, 0.8]])
+    llh, grad, _ = ctx.objective(orc.GP4ML, orc.STD, hp)
+    ref = orc.objective_fast(X, f, H, hp, orc.GP4ML, orc.STD, True)
+    assert abs(llh - ref[0]) <= 1e-10 * abs(ref[0])
+    ok, err = _grad_ok(grad, ref[1])
+    assert ok, err

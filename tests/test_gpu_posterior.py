@@ -1,0 +1,60 @@
+"""GPU posterior mean/variance vs the reference's reconstructed emulators (G3).
+North-star tolerance: posterior mean within 1e-8 of SciPy (absolute)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import gp_oracle as orc
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.mark.parametrize("tag", ["toysim", "toysim3d_o0", "toysim3d_o1"])
+@pytest.mark.parametrize("full", [True, False])
+def test_posterior_golden(ctx, tag, full):
+    z = np.load(os.path.join(GOLD, f"posterior_{tag}.npz"))
+    kind = orc.ALT if bool(z["alt"]) else orc.STD
+    ctx.set_data(z["XT"], z["fT"], z["HT"])
+    ctx.factor(kind, z["delta"], float(z["nu"]), 1.0, 0.0)
+    Hs = np.hstack([np.ones((z["xs"].shape[0], 1)), z["xs"]])[:, :z["HT"].shape[1]]
+    mean, var = ctx.posterior(z["xs"], Hs, z["beta"], float(z["sigma"]), full_var=full)
+    assert np.max(np.abs(mean - z["mean"])) < 1e-8
+    vref = z["var"] if full else np.diag(z["var"])
+    assert np.max(np.abs(var - vref)) < 1e-8 * max(1.0, np.max(np.abs(vref)))
+
+
+@pytest.mark.parametrize("tag", ["toysim", "toysim3d_o0"])
+def test_beta_golden(ctx, tag):
+    z = np.load(os.path.join(GOLD, f"posterior_{tag}.npz"))
+    kind = orc.ALT if bool(z["alt"]) else orc.STD
+    ctx.set_data(z["XT"], z["fT"], z["HT"])
+    ctx.factor(kind, z["delta"], float(z["nu"]), 1.0, 0.0)
+    assert np.max(np.abs(ctx.beta() - z["beta_opt"])) < 1e-9 * (1 + np.max(np.abs(z["beta_opt"])))
+
+
+@pytest.mark.parametrize("kind", [orc.STD, orc.ALT])
+def test_kernel_var_covar_golden(ctx, kind):
+    z = np.load(os.path.join(GOLD, "kernel_std.npz" if kind == orc.STD else "kernel_alt.npz"))
+    for pred, key in ((True, "A_pred"), (False, "A_est")):
+        A = ctx.kernel_var(kind, z["delta"], float(z["nu"]), z["X"], predict=pred)
+        assert np.max(np.abs(A - z[key])) < 1e-15 * 4
+    C = ctx.kernel_covar(kind, z["delta"], float(z["nu"]), z["X"], z["Xs"])
+    assert np.max(np.abs(C - z["covar"])) < 1e-15 * 4
+
+
+def test_posterior_large_m_chunked(ctx):
+    X, f, H = orc.synthetic_problem(700, 3, seed=4)
+    ctx.set_data(X, f, H)
+    delta, nu = np.array([0.5, 0.6, 0.7]), 1e-3
+    ctx.factor(orc.STD, delta, nu, 1.0, 0.0)
+    beta = ctx.beta()
+    xs = np.random.RandomState(1).uniform(size=(9000, 3))
+    hs = orc.linear_basis(xs)
+    mean, var = ctx.posterior(xs, hs, beta, 0.8, full_var=False)
+    A, _ = orc.kernel_var_ref(X, delta, nu, orc.STD, True)
+    sel = np.arange(0, 9000, 97)
+    m_ref, v_ref = orc.posterior_ref(X, f, H, A, xs[sel], hs[sel], beta, 0.8, delta, nu, orc.STD)
+    assert np.max(np.abs(mean[sel] - m_ref)) < 1e-8
+    assert np.max(np.abs(var[sel] - np.diag(v_ref))) < 1e-8
