@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -115,6 +116,9 @@ struct gpe_ctx {
   int f_kernel = 0;
   std::vector<double> f_delta;
   double f_nu = 0.0;
+
+  // A/B switch: GPEMU_DIAG=rows selects the register-blocked diagonal kernel
+  bool diag_rows = false;
 
   // profiling
   bool prof = false;
@@ -388,8 +392,12 @@ int kbuild(gpe_ctx* c, int kernel, double nu, double s2, double rscale) {
 int potrf(gpe_ctx* c, Fact& F) {
   const Plan& pl = F.plan;
   for (int kt = 0; kt < F.NB; ++kt) {
-    hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(DIAG_THREADS), 0, c->stream, F.A, (long long)F.n_pad,
-                       kt, F.B, (long long)F.n_pad, F.logdet, c->dinfo);
+    if (c->diag_rows)
+      hipLaunchKernelGGL(k_potrf_diag_rows, dim3(1), dim3(DIAG_ROWS_THREADS), 0, c->stream, F.A,
+                         (long long)F.n_pad, kt, F.B, (long long)F.n_pad, F.logdet, c->dinfo);
+    else
+      hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(DIAG_THREADS), 0, c->stream, F.A, (long long)F.n_pad,
+                         kt, F.B, (long long)F.n_pad, F.logdet, c->dinfo);
     HIPCHK(c, hipGetLastError());
     if (kt + 1 < F.NB) {
       CHK(launch_gemm_range(c, pl.launches[pl.panel[kt]]));
@@ -599,6 +607,10 @@ gpe_ctx* gpe_create(int32_t device) {
   gpe_ctx* c = new gpe_ctx();
   c->device = device;
   c->aux.desc_base = AUX_DESC_BASE;
+  {
+    const char* e = std::getenv("GPEMU_DIAG");
+    c->diag_rows = e && std::string(e) == "rows";
+  }
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     g_create_error = "failed to initialise device/stream";
     delete c;
@@ -1271,5 +1283,57 @@ int gpe_test_gemm(gpe_ctx* c, int32_t trans_a, int32_t trans_b, int64_t M, int64
   return rc;
 }
 
+int gpe_bench_gemm(gpe_ctx* c, int32_t trans_a, int32_t trans_b, int32_t mt, int32_t nt, int32_t K,
+                   int32_t lower, double beta, int32_t reps, double* ms_out) {
+  if (!c || !ms_out || mt <= 0 || nt <= 0 || K <= 0 || K % GK || reps <= 0) return GPE_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  const long long M = (long long)mt * TILE, N = (long long)nt * TILE;
+  double *da = nullptr, *db = nullptr, *dc = nullptr;
+  int rc = dalloc(c, &da, (size_t)M * K);
+  if (rc == GPE_OK) rc = dalloc(c, &db, (size_t)K * N);
+  if (rc == GPE_OK) rc = dalloc(c, &dc, (size_t)M * N);
+  if (rc == GPE_OK) {
+    // deterministic non-trivial fill via the pair kernel is overkill: a memset-free pattern
+    std::vector<double> h((size_t)std::max<long long>(M, N) * 64);
+    for (size_t i = 0; i < h.size(); ++i) h[i] = std::sin(0.37 * (double)i) * 0.5;
+    auto fill = [&](double* dp, size_t cnt) {
+      for (size_t off = 0; off < cnt; off += h.size())
+        (void)hipMemcpy(dp + off, h.data(), std::min(h.size(), cnt - off) * sizeof(double), hipMemcpyHostToDevice);
+    };
+    fill(da, (size_t)M * K);
+    fill(db, (size_t)K * N);
+    fill(dc, (size_t)M * N);
+    const long long lda = trans_a ? K : M, ldb = trans_b ? K : N;
+    GemmProb p = mkprob(da, lda, db, ldb, dc, M, mt, nt, K, lower ? G_CLOWER : 0, -1.0, beta);
+    p.tile_begin = 0;
+    p.ntiles = prob_tiles(p);
+    (void)hipMemcpy(c->dprobs + ADHOC_DESC_BASE + 16, &p, sizeof(GemmProb), hipMemcpyHostToDevice);
+    HIPCHK(c, hipMemsetAsync(c->dinfo, 0, sizeof(int), c->stream));
+    const int kind = trans_a ? (trans_b ? 2 : 1) : (trans_b ? 3 : 0);
+    Launch L{kind, ADHOC_DESC_BASE + 16, 1, p.ntiles, 0.0};
+    const bool prof = c->prof;
+    c->prof = false;
+    rc = launch_gemm_range(c, L);   // warm-up
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, c->stream);
+    for (int r = 0; r < reps && rc == GPE_OK; ++r) rc = launch_gemm_range(c, L);
+    (void)hipEventRecord(e1, c->stream);
+    (void)hipEventSynchronize(e1);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    *ms_out = ms / reps;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    c->prof = prof;
+  }
+  if (da) (void)hipFree(da);
+  if (db) (void)hipFree(db);
+  if (dc) (void)hipFree(dc);
+  return rc;
+}
+
 }  // extern "C"
+
 

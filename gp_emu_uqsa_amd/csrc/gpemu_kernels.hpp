@@ -97,7 +97,224 @@ __global__ void __launch_bounds__(256) k_pairs(PairArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// diagonal-block Cholesky + inverse of one 128x128 tile.
+// diagonal-block Cholesky + inverse of one 128x128 tile, recursive and MFMA-based.
+// In : A tile (kt,kt) lower part.  Out: L_kk (lower, in place), Dinv_kk = L_kk^-1
+// into tile (kt,kt) of the inverse buffer (upper part zeroed), sum log(L_jj) into
+// logdet[kt], info = 1-based global column of the first bad pivot (LAPACK dpotrf
+// convention) on failure.  Pivot test `!(p > 0)` rejects 0, negatives and NaN.
+//
+// The tile lives in LDS (S, column-major, pitch SP): L in the lower triangle and
+// X = L^-1 stored transposed in the strictly-upper triangle (X(i,c) at S[c+i*SP]),
+// X's diagonal in xd.  node<O,SZ> factors and inverts the SZ x SZ diagonal block
+// at offset O:  node(R1); L21 = A21 X11^T; A22 -= L21 L21^T; node(R2);
+// X21 = -X22 (L21 X11) -- the off-diagonal products on v_mfma_f64_16x16x4_f64
+// straight from LDS (16x16 blocks, 4 waves).  16x16 leaves are factored and
+// inverted by one wave with cross-lane shuffles (16 dependent column steps each).
+// ---------------------------------------------------------------------------
+constexpr int SP = TILE + 1;
+constexpr int DIAG_THREADS = 256;
+
+__device__ __forceinline__ double dg_x(const double* S, const double* xd, int i, int c) {
+  return i > c ? S[c + i * SP] : (i == c ? xd[i] : 0.0);
+}
+
+// one wave: factor + invert the 16x16 diagonal leaf at offset o
+__device__ __forceinline__ void dg_leaf(double* S, double* xd, int o, int lane, int* fail) {
+  const int i = lane & 15, g = lane >> 4;
+  double a[4], x[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int k = 4 * g + c;
+    a[c] = (i >= k) ? S[(o + i) + (o + k) * SP] : 0.0;
+    x[c] = (i == k) ? 1.0 : 0.0;
+  }
+  int bad = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int jg = j >> 2, jc = j & 3;
+    const double piv = __shfl(a[jc], j + 16 * jg, 64);
+    if (!(piv > 0.0)) {
+      bad = j + 1;
+      break;  // wave-uniform
+    }
+    const double dj = sqrt(piv), r = 1.0 / dj;
+    const double t = (i > j) ? a[jc] * r : (i == j ? dj : a[jc]);
+    if (g == jg) a[jc] = t;
+    const double lij = __shfl(t, i + 16 * jg, 64);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int k = 4 * g + c;
+      const double lkj = __shfl(t, k + 16 * jg, 64);
+      if (k > j && i >= k) a[c] = fma(-lij, lkj, a[c]);
+    }
+  }
+  if (bad) {
+    if (lane == 0) *fail = o + bad;
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int jg = j >> 2, jc = j & 3;
+    const double rl = 1.0 / __shfl(a[jc], j + 16 * jg, 64);
+    double xs[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int cc = 4 * g + c;
+      xs[c] = (i == j && cc <= j) ? x[c] * rl : x[c];
+      if (i == j) x[c] = xs[c];
+    }
+    const double lij = __shfl(a[jc], i + 16 * jg, 64);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const double xjc = __shfl(xs[c], j + 16 * g, 64);
+      const int cc = 4 * g + c;
+      if (i > j && cc <= j) x[c] = fma(-lij, xjc, x[c]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int k = 4 * g + c;
+    if (i >= k) S[(o + i) + (o + k) * SP] = a[c];
+    if (i > k) S[(o + k) + (o + i) * SP] = x[c];
+    if (i == k) xd[o + i] = x[c];
+  }
+}
+
+// D += A(i0.., k) B(k, j0..) for k in [k0,k1) on one 16x16 block (natural MFMA
+// orientation: lane l, reg r <-> D(i0 + (l>>4) + 4r, j0 + (l&15)))
+template <class FA, class FB>
+__device__ __forceinline__ void dg_mma(d4& acc, FA fa, FB fb, int i0, int j0, int k0, int k1,
+                                       int lane) {
+  for (int k = k0; k < k1; k += 4) {
+    const double av = fa(i0 + (lane & 15), k + (lane >> 4));
+    const double bv = fb(k + (lane >> 4), j0 + (lane & 15));
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+  }
+}
+
+template <int O, int SZ>
+__device__ void dg_node(double* S, double* xd, int* fail, int tid) {
+  const int lane = tid & 63, wave = tid >> 6;
+  if constexpr (SZ == 16) {
+    if (wave == 0) dg_leaf(S, xd, O, lane, fail);
+    __syncthreads();
+  } else {
+    constexpr int H = SZ / 2, NB = H / 16, O2 = O + H;
+    dg_node<O, H>(S, xd, fail, tid);
+    if (*fail) return;
+    auto lget = [S](int i, int k) { return S[i + k * SP]; };
+    // 1. L21 = A21 X11^T  (X11(c,k) != 0 only for k <= c)
+    {
+      constexpr int PER = (NB * NB + 3) / 4;
+      d4 acc[PER];
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int b = wave + 4 * u;
+        acc[u] = d4{0.0, 0.0, 0.0, 0.0};
+        if (b < NB * NB) {
+          const int ib = b % NB, cb = b / NB;
+          dg_mma(acc[u], lget, [S, xd](int k, int n) { return dg_x(S, xd, n, k); }, O2 + ib * 16,
+                 O + cb * 16, O, O + (cb + 1) * 16, lane);
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int b = wave + 4 * u;
+        if (b < NB * NB) {
+          const int ib = b % NB, cb = b / NB;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            S[(O2 + ib * 16 + (lane >> 4) + 4 * r) + (O + cb * 16 + (lane & 15)) * SP] = acc[u][r];
+        }
+      }
+      __syncthreads();
+    }
+    // 2. A22 -= L21 L21^T  (lower blocks)
+    {
+      constexpr int NLOW = NB * (NB + 1) / 2;
+      for (int b = wave; b < NLOW; b += 4) {
+        int ib = 0;
+        while ((ib + 1) * (ib + 2) / 2 <= b) ++ib;
+        const int jb = b - ib * (ib + 1) / 2;
+        d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+        dg_mma(acc, lget, [S](int k, int n) { return S[n + k * SP]; }, O2 + ib * 16, O2 + jb * 16, O,
+               O2, lane);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          S[(O2 + ib * 16 + (lane >> 4) + 4 * r) + (O2 + jb * 16 + (lane & 15)) * SP] -= acc[r];
+      }
+      __syncthreads();
+    }
+    dg_node<O2, H>(S, xd, fail, tid);
+    if (*fail) return;
+    // 3. X21 = -X22 T, T = L21 X11; wave w owns column block w of T and X21.
+    //    The f64 accumulator layout of T(kb, cb) is the B fragment of k-steps 0..3.
+    if (wave < NB) {
+      const int cb = wave;
+      d4 T[NB];
+#pragma unroll
+      for (int ib = 0; ib < NB; ++ib) {
+        T[ib] = d4{0.0, 0.0, 0.0, 0.0};
+        dg_mma(T[ib], lget, [S, xd](int k, int n) { return dg_x(S, xd, k, n); }, O2 + ib * 16,
+               O + cb * 16, O + cb * 16, O + H, lane);
+      }
+#pragma unroll
+      for (int ib = 0; ib < NB; ++ib) {
+        d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kb = 0; kb <= ib; ++kb)
+#pragma unroll
+          for (int st = 0; st < 4; ++st) {
+            const double av = dg_x(S, xd, O2 + ib * 16 + (lane & 15), O2 + kb * 16 + 4 * st + (lane >> 4));
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, T[kb][st], acc, 0, 0, 0);
+          }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          S[(O + cb * 16 + (lane & 15)) + (O2 + ib * 16 + (lane >> 4) + 4 * r) * SP] = -acc[r];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(DIAG_THREADS) k_potrf_diag(double* A, long long lda, int kt,
+                                                             double* Dinv, long long ldd,
+                                                             double* logdet, int* info) {
+  __shared__ double S[TILE * SP];
+  __shared__ double xd[TILE];
+  __shared__ double red[4];
+  __shared__ int fail;
+  if (*info) return;
+  const int t = threadIdx.x;
+  double* Akk = A + (long long)kt * TILE * (lda + 1);
+  for (int e = t; e < TILE * TILE; e += DIAG_THREADS) {
+    const int i = e & (TILE - 1), k = e >> 7;
+    S[i + k * SP] = Akk[i + (long long)k * lda];
+  }
+  if (t == 0) fail = 0;
+  __syncthreads();
+  dg_node<0, TILE>(S, xd, &fail, t);
+  __syncthreads();
+  if (fail) {
+    if (t == 0) atomicCAS(info, 0, kt * TILE + fail);
+    return;
+  }
+  double lg = (t < TILE) ? log(S[t + t * SP]) : 0.0;
+  for (int off = 32; off > 0; off >>= 1) lg += __shfl_down(lg, off, 64);
+  if ((t & 63) == 0) red[t >> 6] = lg;
+  __syncthreads();
+  if (t == 0) logdet[kt] = (red[0] + red[1]) + (red[2] + red[3]);
+  double* Dkk = Dinv + (long long)kt * TILE * (ldd + 1);
+  for (int e = t; e < TILE * TILE; e += DIAG_THREADS) {
+    const int i = e & (TILE - 1), k = e >> 7;
+    if (i >= k) Akk[i + (long long)k * lda] = S[i + k * SP];
+    Dkk[i + (long long)k * ldd] = dg_x(S, xd, i, k);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// (A/B reference) register-blocked diagonal-block Cholesky + inverse.
 // In : A tile (kt,kt) lower part.  Out: L_kk (lower, in place), Dinv_kk = L_kk^-1
 // into tile (kt,kt) of the inverse buffer (upper part zeroed), sum log(L_jj) into
 // logdet[kt], info = 1-based global column of the first bad pivot (LAPACK dpotrf
@@ -108,9 +325,9 @@ __global__ void __launch_bounds__(256) k_pairs(PairArgs a) {
 // right-looking factorisation, two per column for the forward-substitution
 // inverse [L | I] -> [I | L^-1].
 // ---------------------------------------------------------------------------
-constexpr int DIAG_THREADS = 1024;
+constexpr int DIAG_ROWS_THREADS = 1024;
 
-__global__ void __launch_bounds__(DIAG_THREADS) k_potrf_diag(double* A, long long lda, int kt,
+__global__ void __launch_bounds__(DIAG_ROWS_THREADS) k_potrf_diag_rows(double* A, long long lda, int kt,
                                                              double* Dinv, long long ldd,
                                                              double* logdet, int* info) {
   __shared__ double colbuf[TILE];
@@ -279,6 +496,66 @@ constexpr int G_LDS_DOUBLES = 2 * 2 * GK * GP;   // 9216 doubles = 73,728 B
 // MFMA f64 16x16x4 accumulator layout: lane l, register r -> (row, col) of D
 __device__ inline int mfma64_row(int lane, int r) { return (lane >> 4) + 4 * r; }
 
+// K-stage staging of the grouped GEMM: each of the 256 threads moves four 16-byte
+// pieces of the A tile (128 x 16) and four of the B tile into registers, then
+// into the [k][m] LDS image (pitch GP).
+template <bool AK, bool BK>
+__device__ __forceinline__ void gemm_gload(const double* __restrict__ Ab,
+                                           const double* __restrict__ Bb, long long lda,
+                                           long long ldb, int k0, int tid, double (&ra)[8],
+                                           double (&rb)[8]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int c = tid + 256 * s;
+    double2 va, vb;
+    if (!AK) {
+      const int kk = c >> 6, mm = (c & 63) * 2;
+      va = *reinterpret_cast<const double2*>(Ab + mm + (long long)(k0 + kk) * lda);
+    } else {
+      const int mm = c >> 3, kk = (c & 7) * 2;
+      va = *reinterpret_cast<const double2*>(Ab + (long long)mm * lda + k0 + kk);
+    }
+    if (!BK) {
+      const int kk = c >> 6, nn = (c & 63) * 2;
+      vb = *reinterpret_cast<const double2*>(Bb + nn + (long long)(k0 + kk) * ldb);
+    } else {
+      const int nn = c >> 3, kk = (c & 7) * 2;
+      vb = *reinterpret_cast<const double2*>(Bb + (long long)nn * ldb + k0 + kk);
+    }
+    ra[2 * s] = va.x;
+    ra[2 * s + 1] = va.y;
+    rb[2 * s] = vb.x;
+    rb[2 * s + 1] = vb.y;
+  }
+}
+
+template <bool AK, bool BK>
+__device__ __forceinline__ void gemm_sstore(double* lds, int buf, int tid, const double (&ra)[8],
+                                            const double (&rb)[8]) {
+  double* As = lds + buf * (2 * GK * GP);
+  double* Bs = As + GK * GP;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int c = tid + 256 * s;
+    if (!AK) {
+      const int kk = c >> 6, mm = (c & 63) * 2;
+      *reinterpret_cast<double2*>(As + kk * GP + mm) = make_double2(ra[2 * s], ra[2 * s + 1]);
+    } else {
+      const int mm = c >> 3, kk = (c & 7) * 2;
+      As[kk * GP + mm] = ra[2 * s];
+      As[(kk + 1) * GP + mm] = ra[2 * s + 1];
+    }
+    if (!BK) {
+      const int kk = c >> 6, nn = (c & 63) * 2;
+      *reinterpret_cast<double2*>(Bs + kk * GP + nn) = make_double2(rb[2 * s], rb[2 * s + 1]);
+    } else {
+      const int nn = c >> 3, kk = (c & 7) * 2;
+      Bs[kk * GP + nn] = rb[2 * s];
+      Bs[(kk + 1) * GP + nn] = rb[2 * s + 1];
+    }
+  }
+}
+
 template <bool AK, bool BK>
 __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restrict__ probs, int nprob,
                                                   const int* __restrict__ abort_flag) {
@@ -327,59 +604,14 @@ __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restrict__ pr
       for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
   }
 
-  double2 ra[4], rb[4];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int c = tid + 256 * s;
-      if (!AK) {
-        const int kk = c >> 6, mm = (c & 63) * 2;
-        ra[s] = *reinterpret_cast<const double2*>(Ab + mm + (long long)(k0 + kk) * P.lda);
-      } else {
-        const int mm = c >> 3, kk = (c & 7) * 2;
-        ra[s] = *reinterpret_cast<const double2*>(Ab + (long long)mm * P.lda + k0 + kk);
-      }
-      if (!BK) {
-        const int kk = c >> 6, nn = (c & 63) * 2;
-        rb[s] = *reinterpret_cast<const double2*>(Bb + nn + (long long)(k0 + kk) * P.ldb);
-      } else {
-        const int nn = c >> 3, kk = (c & 7) * 2;
-        rb[s] = *reinterpret_cast<const double2*>(Bb + (long long)nn * P.ldb + k0 + kk);
-      }
-    }
-  };
-  auto sstore = [&](int buf) {
-    double* As = lds + buf * (2 * GK * GP);
-    double* Bs = As + GK * GP;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int c = tid + 256 * s;
-      if (!AK) {
-        const int kk = c >> 6, mm = (c & 63) * 2;
-        *reinterpret_cast<double2*>(As + kk * GP + mm) = ra[s];
-      } else {
-        const int mm = c >> 3, kk = (c & 7) * 2;
-        As[kk * GP + mm] = ra[s].x;
-        As[(kk + 1) * GP + mm] = ra[s].y;
-      }
-      if (!BK) {
-        const int kk = c >> 6, nn = (c & 63) * 2;
-        *reinterpret_cast<double2*>(Bs + kk * GP + nn) = rb[s];
-      } else {
-        const int nn = c >> 3, kk = (c & 7) * 2;
-        Bs[kk * GP + nn] = rb[s].x;
-        Bs[(kk + 1) * GP + nn] = rb[s].y;
-      }
-    }
-  };
-
+  double ra[8], rb[8];
   const int nk = (kend - kbeg) / GK;
   if (nk > 0) {
-    gload(kbeg);
-    sstore(0);
+    gemm_gload<AK, BK>(Ab, Bb, P.lda, P.ldb, kbeg, tid, ra, rb);
+    gemm_sstore<AK, BK>(lds, 0, tid, ra, rb);
     __syncthreads();
     for (int s = 0; s < nk; ++s) {
-      if (s + 1 < nk) gload(kbeg + (s + 1) * GK);
+      if (s + 1 < nk) gemm_gload<AK, BK>(Ab, Bb, P.lda, P.ldb, kbeg + (s + 1) * GK, tid, ra, rb);
       const double* As = lds + (s & 1) * (2 * GK * GP);
       const double* Bs = As + GK * GP;
 #pragma unroll
@@ -396,7 +628,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restrict__ pr
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(bf[j], af[i], acc[i][j], 0, 0, 0);
       }
-      if (s + 1 < nk) sstore((s + 1) & 1);
+      if (s + 1 < nk) gemm_sstore<AK, BK>(lds, (s + 1) & 1, tid, ra, rb);
       __syncthreads();
     }
   }

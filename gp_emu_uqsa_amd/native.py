@@ -46,6 +46,8 @@ SIGNATURES = {
     "gpe_cholesky": (_ct.c_int, [_VP, _ct.c_int64, _D, _D, _D, _D, _D]),
     "gpe_test_gemm": (_ct.c_int, [_VP, _ct.c_int32, _ct.c_int32, _ct.c_int64, _ct.c_int64,
                                   _ct.c_int64, _D, _D, _D, _ct.c_double, _ct.c_double]),
+    "gpe_bench_gemm": (_ct.c_int, [_VP, _ct.c_int32, _ct.c_int32, _ct.c_int32, _ct.c_int32,
+                                   _ct.c_int32, _ct.c_int32, _ct.c_double, _ct.c_int32, _D]),
     "gpe_set_profiling": (_ct.c_int, [_VP, _ct.c_int32]),
     "gpe_phase_times": (_ct.c_int, [_VP, _D, _ct.c_int32]),
     "gpe_gemm_stats": (_ct.c_int, [_VP, _D, _D, _D]),
@@ -234,6 +236,13 @@ class Context:
                                            _ptr(B), _ptr(C), float(alpha), float(beta)),
                     "gpe_test_gemm")
         return C
+
+    def bench_gemm(self, mt, nt, K, trans_a=0, trans_b=0, lower=False, beta=1.0, reps=5):
+        ms = _ct.c_double()
+        self._check(self.lib.gpe_bench_gemm(self._h, int(trans_a), int(trans_b), int(mt), int(nt),
+                                            int(K), 1 if lower else 0, float(beta), int(reps),
+                                            _ct.byref(ms)), "gpe_bench_gemm")
+        return ms.value
 
     # -- profiling
     def set_profiling(self, on=True):

@@ -123,6 +123,13 @@ int gpe_test_gemm(gpe_ctx* ctx, int32_t trans_a, int32_t trans_b, int64_t M, int
                   int64_t K, const double* A, const double* B, double* C,
                   double alpha, double beta);
 
+/* Benchmark hook: time `reps` launches of the grouped GEMM on device-resident
+ * random operands: C (mt*128 x nt*128, lower tiles only if lower) += -A B^T-style
+ * update with K, in storage orientation (trans_a, trans_b).  Returns average
+ * ms per launch in *ms_out.  Uses its own device buffers. */
+int gpe_bench_gemm(gpe_ctx* ctx, int32_t trans_a, int32_t trans_b, int32_t mt, int32_t nt,
+                   int32_t K, int32_t lower, double beta, int32_t reps, double* ms_out);
+
 /* Per-phase device time of the most recent gpe_objective call, in ms:
  * [0] K-build, [1] Cholesky, [2] triangular inverse, [3] A^-1 (L^-T L^-1),
  * [4] skinny solves / small algebra, [5] gradient contraction, [6] total.
