@@ -42,8 +42,9 @@ struct Plan {
   long long n_pad = 0;
   const double* a_ptr = nullptr;   // buffers the descriptors point into
   const double* b_ptr = nullptr;
-  // potrf: per step kt the panel launch and the syrk launch (index into launches or -1)
-  std::vector<int> panel, syrk;
+  // potrf with depth-1 look-ahead: per step kt the panel launch, the update of
+  // column block kt+1 (critical path) and the rest of the trailing update
+  std::vector<int> panel, colupd, rest;
   std::vector<int> trtri;   // launches in order
   int lauum = -1;
   std::vector<Launch> launches;
@@ -119,6 +120,11 @@ struct gpe_ctx {
 
   // A/B switch: GPEMU_DIAG=rows selects the register-blocked diagonal kernel
   bool diag_rows = false;
+
+  // look-ahead stream and events
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  std::vector<hipEvent_t> ev_panel, ev_rest;
 
   // profiling
   bool prof = false;
@@ -198,7 +204,8 @@ int launch_pairs(gpe_ctx* c, const PairArgs& a, int nblocks) {
   return GPE_OK;
 }
 
-int launch_gemm_range(gpe_ctx* c, const Launch& L) {
+int launch_gemm_range(gpe_ctx* c, const Launch& L, hipStream_t st = nullptr) {
+  if (!st) st = c->stream;
   const size_t lds = G_LDS_DOUBLES * sizeof(double);
   const GemmProb* pr = c->dprobs + L.first;
   if (c->prof) {
@@ -207,17 +214,17 @@ int launch_gemm_range(gpe_ctx* c, const Launch& L) {
     HIPCHK(c, hipEventCreate(&e1));
     c->gev.push_back(e0);
     c->gev.push_back(e1);
-    HIPCHK(c, hipEventRecord(e0, c->stream));
+    HIPCHK(c, hipEventRecord(e0, st));
   }
   switch (L.kind) {
-    case 0: hipLaunchKernelGGL((k_gemm<false, false>), dim3(L.tiles), dim3(256), lds, c->stream, pr, L.count, c->dinfo); break;
-    case 1: hipLaunchKernelGGL((k_gemm<true, false>), dim3(L.tiles), dim3(256), lds, c->stream, pr, L.count, c->dinfo); break;
-    case 2: hipLaunchKernelGGL((k_gemm<true, true>), dim3(L.tiles), dim3(256), lds, c->stream, pr, L.count, c->dinfo); break;
-    default: hipLaunchKernelGGL((k_gemm<false, true>), dim3(L.tiles), dim3(256), lds, c->stream, pr, L.count, c->dinfo); break;
+    case 0: hipLaunchKernelGGL((k_gemm<false, false>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, c->dinfo); break;
+    case 1: hipLaunchKernelGGL((k_gemm<true, false>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, c->dinfo); break;
+    case 2: hipLaunchKernelGGL((k_gemm<true, true>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, c->dinfo); break;
+    default: hipLaunchKernelGGL((k_gemm<false, true>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, c->dinfo); break;
   }
   HIPCHK(c, hipGetLastError());
   if (c->prof) {
-    HIPCHK(c, hipEventRecord(c->gev.back(), c->stream));
+    HIPCHK(c, hipEventRecord(c->gev.back(), st));
     c->gemm_launches += 1.0;
     c->gemm_flops += L.flops;
   }
@@ -273,7 +280,8 @@ int build_plan(gpe_ctx* c, Fact& F) {
   auto tile = [&](double* M, int i, int j) { return M + (long long)i * TILE + (long long)j * TILE * ld; };
   // --- Cholesky (right-looking, 128-column steps)
   pl.panel.assign(NB, -1);
-  pl.syrk.assign(NB, -1);
+  pl.colupd.assign(NB, -1);
+  pl.rest.assign(NB, -1);
   for (int kt = 0; kt + 1 < NB; ++kt) {
     const int m = NB - kt - 1;
     // L(kt+1:, kt) = A(kt+1:, kt) * Dinv_kt^T     (opB(k,n) = Dinv(n,k): N-contiguous)
@@ -282,12 +290,20 @@ int build_plan(gpe_ctx* c, Fact& F) {
                {mkprob(tile(A, kt + 1, kt), ld, tile(B, kt, kt), ld, tile(A, kt + 1, kt), ld, m, 1,
                        TILE, 0, 1.0, 0.0)},
                (double)m * T * T * T);
-    // A(kt+1:, kt+1:) -= L(kt+1:, kt) L(kt+1:, kt)^T   (lower tiles)
-    pl.syrk[kt] = (int)pl.launches.size();
+    // column block kt+1: A(kt+1:, kt+1) -= L(kt+1:, kt) L(kt+1, kt)^T
+    pl.colupd[kt] = (int)pl.launches.size();
     add_launch(pl, 0,
                {mkprob(tile(A, kt + 1, kt), ld, tile(A, kt + 1, kt), ld, tile(A, kt + 1, kt + 1), ld,
-                       m, m, TILE, G_CLOWER, -1.0, 1.0)},
-               (double)m * T * ((double)m * T + 1.0) * T);
+                       m, 1, TILE, 0, -1.0, 1.0)},
+               (double)m * T * T * T * 2.0 - T * T * T);
+    // the rest: A(kt+2:, kt+2:) -= L(kt+2:, kt) L(kt+2:, kt)^T   (lower tiles)
+    if (m >= 2) {
+      pl.rest[kt] = (int)pl.launches.size();
+      add_launch(pl, 0,
+                 {mkprob(tile(A, kt + 2, kt), ld, tile(A, kt + 2, kt), ld, tile(A, kt + 2, kt + 2), ld,
+                         m - 1, m - 1, TILE, G_CLOWER, -1.0, 1.0)},
+                 (double)(m - 1) * T * ((double)(m - 1) * T + 1.0) * T);
+    }
   }
   // --- triangular inverse X = L^-1 in B (diagonal tiles already hold Dinv)
   for (int s = 2; s / 2 < NB; s *= 2) {
@@ -389,21 +405,49 @@ int kbuild(gpe_ctx* c, int kernel, double nu, double s2, double rscale) {
   return launch_pairs(c, a, c->NB * (c->NB + 1) / 2);
 }
 
+// Right-looking blocked Cholesky with depth-1 look-ahead on two streams.
+//   aux  : wait rest(k-2) | diag(k) | panel(k) | rec ev_panel[k] | wait rest(k-1) | colupd(k)
+//   main : wait ev_panel[k] | rest(k) | rec ev_rest[k]
+// diag/panel/colupd of the next step run while the big trailing update runs.
 int potrf(gpe_ctx* c, Fact& F) {
   const Plan& pl = F.plan;
-  for (int kt = 0; kt < F.NB; ++kt) {
-    if (c->diag_rows)
-      hipLaunchKernelGGL(k_potrf_diag_rows, dim3(1), dim3(DIAG_ROWS_THREADS), 0, c->stream, F.A,
-                         (long long)F.n_pad, kt, F.B, (long long)F.n_pad, F.logdet, c->dinfo);
-    else
-      hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(DIAG_THREADS), 0, c->stream, F.A, (long long)F.n_pad,
-                         kt, F.B, (long long)F.n_pad, F.logdet, c->dinfo);
-    HIPCHK(c, hipGetLastError());
-    if (kt + 1 < F.NB) {
-      CHK(launch_gemm_range(c, pl.launches[pl.panel[kt]]));
-      CHK(launch_gemm_range(c, pl.launches[pl.syrk[kt]]));
+  const int NB = F.NB;
+  if ((int)c->ev_panel.size() < NB) {
+    for (auto& e : c->ev_panel) (void)hipEventDestroy(e);
+    for (auto& e : c->ev_rest) (void)hipEventDestroy(e);
+    c->ev_panel.assign(NB, nullptr);
+    c->ev_rest.assign(NB, nullptr);
+    for (int i = 0; i < NB; ++i) {
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_panel[i], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_rest[i], hipEventDisableTiming));
     }
   }
+  hipStream_t aux = c->stream2, mainst = c->stream;
+  HIPCHK(c, hipEventRecord(c->ev_fork, mainst));
+  HIPCHK(c, hipStreamWaitEvent(aux, c->ev_fork, 0));
+  for (int kt = 0; kt < NB; ++kt) {
+    if (kt >= 2 && pl.rest[kt - 2] >= 0) HIPCHK(c, hipStreamWaitEvent(aux, c->ev_rest[kt - 2], 0));
+    if (c->diag_rows)
+      hipLaunchKernelGGL(k_potrf_diag_rows, dim3(1), dim3(DIAG_ROWS_THREADS), 0, aux, F.A,
+                         (long long)F.n_pad, kt, F.B, (long long)F.n_pad, F.logdet, c->dinfo);
+    else
+      hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(DIAG_THREADS), 0, aux, F.A, (long long)F.n_pad,
+                         kt, F.B, (long long)F.n_pad, F.logdet, c->dinfo);
+    HIPCHK(c, hipGetLastError());
+    if (kt + 1 < NB) {
+      CHK(launch_gemm_range(c, pl.launches[pl.panel[kt]], aux));
+      HIPCHK(c, hipEventRecord(c->ev_panel[kt], aux));
+      if (kt >= 1 && pl.rest[kt - 1] >= 0) HIPCHK(c, hipStreamWaitEvent(aux, c->ev_rest[kt - 1], 0));
+      CHK(launch_gemm_range(c, pl.launches[pl.colupd[kt]], aux));
+      if (pl.rest[kt] >= 0) {
+        HIPCHK(c, hipStreamWaitEvent(mainst, c->ev_panel[kt], 0));
+        CHK(launch_gemm_range(c, pl.launches[pl.rest[kt]], mainst));
+        HIPCHK(c, hipEventRecord(c->ev_rest[kt], mainst));
+      }
+    }
+  }
+  HIPCHK(c, hipEventRecord(c->ev_join, aux));
+  HIPCHK(c, hipStreamWaitEvent(mainst, c->ev_join, 0));
   return GPE_OK;
 }
 
@@ -582,6 +626,14 @@ int factor_and_invert(gpe_ctx* c, int kernel, const double* delta, double nu, do
 
 }  // namespace
 
+// the look-ahead stream gets the highest priority so the critical-path kernels
+// are dispatched ahead of queued trailing-update workgroups
+bool create_priority_stream(hipStream_t* st) {
+  int lo = 0, hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return false;
+  return hipStreamCreateWithPriority(st, hipStreamNonBlocking, hi) == hipSuccess;
+}
+
 // =====================================================================  C-ABI
 extern "C" {
 
@@ -611,7 +663,10 @@ gpe_ctx* gpe_create(int32_t device) {
     const char* e = std::getenv("GPEMU_DIAG");
     c->diag_rows = e && std::string(e) == "rows";
   }
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      !create_priority_stream(&c->stream2) ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
     g_create_error = "failed to initialise device/stream";
     delete c;
     return nullptr;
@@ -652,8 +707,16 @@ void gpe_destroy(gpe_ctx* c) {
   if (c->hpin) hipHostFree(c->hpin);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
-  for (auto& e : c->gev) hipEventDestroy(e);
-  if (c->stream) hipStreamDestroy(c->stream);
+  for (auto& e : c->gev) (void)hipEventDestroy(e);
+  for (auto& e : c->ev_panel) (void)hipEventDestroy(e);
+  for (auto& e : c->ev_rest) (void)hipEventDestroy(e);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->stream2) {
+    (void)hipStreamSynchronize(c->stream2);
+    (void)hipStreamDestroy(c->stream2);
+  }
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
 

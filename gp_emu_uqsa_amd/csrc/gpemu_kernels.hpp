@@ -118,65 +118,70 @@ __device__ __forceinline__ double dg_x(const double* S, const double* xd, int i,
   return i > c ? S[c + i * SP] : (i == c ? xd[i] : 0.0);
 }
 
-// one wave: factor + invert the 16x16 diagonal leaf at offset o
+// wave-uniform broadcast of lane `src`'s double (src a compile-time constant)
+__device__ __forceinline__ double dg_bcast(double v, int src) {
+  const unsigned long long b = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, src);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), src);
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+// 1/sqrt(p) from the hardware estimate plus one Newton step (< 1 ulp off the
+// correctly rounded value); sqrt(p) = p * rsq.  p > 0 is checked by the caller.
+__device__ __forceinline__ double dg_rsq(double p) {
+  double r = __builtin_amdgcn_rsq(p);
+  return r * fma(-0.5 * p * r, r, 1.5);
+}
+
+// one wave: factor + invert the 16x16 diagonal leaf at offset o.
+// Lane i (< 16) holds row i of L (a[]) and of X = L^-1 (x[]); column j of L and
+// row j of X are broadcast with v_readlane (no LDS round trip).
 __device__ __forceinline__ void dg_leaf(double* S, double* xd, int o, int lane, int* fail) {
-  const int i = lane & 15, g = lane >> 4;
-  double a[4], x[4];
+  const int i = lane;
+  const bool row = i < 16;
+  double a[16], x[16];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int k = 4 * g + c;
-    a[c] = (i >= k) ? S[(o + i) + (o + k) * SP] : 0.0;
-    x[c] = (i == k) ? 1.0 : 0.0;
+  for (int k = 0; k < 16; ++k) {
+    a[k] = (row && k <= i) ? S[(o + i) + (o + k) * SP] : 0.0;
+    x[k] = (k == i) ? 1.0 : 0.0;
   }
-  int bad = 0;
+  double rdiag[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const int jg = j >> 2, jc = j & 3;
-    const double piv = __shfl(a[jc], j + 16 * jg, 64);
+    const double piv = dg_bcast(a[j], j);
     if (!(piv > 0.0)) {
-      bad = j + 1;
-      break;  // wave-uniform
+      if (lane == 0) *fail = o + j + 1;
+      return;  // wave-uniform
     }
-    const double dj = sqrt(piv), r = 1.0 / dj;
-    const double t = (i > j) ? a[jc] * r : (i == j ? dj : a[jc]);
-    if (g == jg) a[jc] = t;
-    const double lij = __shfl(t, i + 16 * jg, 64);
+    const double r = dg_rsq(piv);
+    rdiag[j] = r;
+    a[j] = (i > j) ? a[j] * r : (i == j ? piv * r : a[j]);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int k = 4 * g + c;
-      const double lkj = __shfl(t, k + 16 * jg, 64);
-      if (k > j && i >= k) a[c] = fma(-lij, lkj, a[c]);
+    for (int k = j + 1; k < 16; ++k) {
+      const double lkj = dg_bcast(a[j], k);
+      if (k <= i) a[k] = fma(-a[j], lkj, a[k]);
     }
   }
-  if (bad) {
-    if (lane == 0) *fail = o + bad;
-    return;
-  }
+  // X = L^-1: row j of X is final once scaled by 1/L(j,j); rows below get
+  // X(i,c) -= L(i,j) X(j,c)
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const int jg = j >> 2, jc = j & 3;
-    const double rl = 1.0 / __shfl(a[jc], j + 16 * jg, 64);
-    double xs[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int cc = 4 * g + c;
-      xs[c] = (i == j && cc <= j) ? x[c] * rl : x[c];
-      if (i == j) x[c] = xs[c];
-    }
-    const double lij = __shfl(a[jc], i + 16 * jg, 64);
+    for (int c = 0; c <= j; ++c)
+      if (i == j) x[c] *= rdiag[j];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const double xjc = __shfl(xs[c], j + 16 * g, 64);
-      const int cc = 4 * g + c;
-      if (i > j && cc <= j) x[c] = fma(-lij, xjc, x[c]);
+    for (int c = 0; c <= j; ++c) {
+      const double xjc = dg_bcast(x[c], j);
+      if (i > j) x[c] = fma(-a[j], xjc, x[c]);
     }
   }
+  if (row) {
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int k = 4 * g + c;
-    if (i >= k) S[(o + i) + (o + k) * SP] = a[c];
-    if (i > k) S[(o + k) + (o + i) * SP] = x[c];
-    if (i == k) xd[o + i] = x[c];
+    for (int k = 0; k < 16; ++k) {
+      if (k <= i) S[(o + i) + (o + k) * SP] = a[k];
+      if (k < i) S[(o + k) + (o + i) * SP] = x[k];
+      if (k == i) xd[o + i] = x[k];
+    }
   }
 }
 
@@ -185,10 +190,16 @@ __device__ __forceinline__ void dg_leaf(double* S, double* xd, int o, int lane, 
 template <class FA, class FB>
 __device__ __forceinline__ void dg_mma(d4& acc, FA fa, FB fb, int i0, int j0, int k0, int k1,
                                        int lane) {
-  for (int k = k0; k < k1; k += 4) {
-    const double av = fa(i0 + (lane & 15), k + (lane >> 4));
-    const double bv = fb(k + (lane >> 4), j0 + (lane & 15));
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+  // k ranges are multiples of 16: fetch a 16-deep slab of both operands, then 4 MFMAs
+  for (int k = k0; k < k1; k += 16) {
+    double av[4], bv[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      av[s] = fa(i0 + (lane & 15), k + 4 * s + (lane >> 4));
+      bv[s] = fb(k + 4 * s + (lane >> 4), j0 + (lane & 15));
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
   }
 }
 
@@ -196,12 +207,18 @@ template <int O, int SZ>
 __device__ void dg_node(double* S, double* xd, int* fail, int tid) {
   const int lane = tid & 63, wave = tid >> 6;
   if constexpr (SZ == 16) {
+#if !defined(DG_ABLATE) || (DG_ABLATE != 2 && DG_ABLATE != 3)
     if (wave == 0) dg_leaf(S, xd, O, lane, fail);
+#endif
     __syncthreads();
   } else {
     constexpr int H = SZ / 2, NB = H / 16, O2 = O + H;
     dg_node<O, H>(S, xd, fail, tid);
     if (*fail) return;
+#if defined(DG_ABLATE) && (DG_ABLATE == 1 || DG_ABLATE == 3)
+    dg_node<O2, H>(S, xd, fail, tid);
+    return;
+#endif
     auto lget = [S](int i, int k) { return S[i + k * SP]; };
     // 1. L21 = A21 X11^T  (X11(c,k) != 0 only for k <= c)
     {
@@ -278,7 +295,7 @@ __device__ void dg_node(double* S, double* xd, int* fail, int tid) {
   }
 }
 
-__global__ void __launch_bounds__(DIAG_THREADS) k_potrf_diag(double* A, long long lda, int kt,
+__global__ void __launch_bounds__(DIAG_THREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_potrf_diag(double* A, long long lda, int kt,
                                                              double* Dinv, long long ldd,
                                                              double* logdet, int* info) {
   __shared__ double S[TILE * SP];
@@ -288,9 +305,21 @@ __global__ void __launch_bounds__(DIAG_THREADS) k_potrf_diag(double* A, long lon
   if (*info) return;
   const int t = threadIdx.x;
   double* Akk = A + (long long)kt * TILE * (lda + 1);
-  for (int e = t; e < TILE * TILE; e += DIAG_THREADS) {
-    const int i = e & (TILE - 1), k = e >> 7;
-    S[i + k * SP] = Akk[i + (long long)k * lda];
+  // batched copy-in: 16 loads in flight per thread before the LDS stores
+  constexpr int PER = TILE * TILE / DIAG_THREADS;   // 64
+#pragma unroll
+  for (int b = 0; b < PER; b += 16) {
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + DIAG_THREADS * (b + u);
+      v[u] = Akk[(e & (TILE - 1)) + (long long)(e >> 7) * lda];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + DIAG_THREADS * (b + u);
+      S[(e & (TILE - 1)) + (e >> 7) * SP] = v[u];
+    }
   }
   if (t == 0) fail = 0;
   __syncthreads();
@@ -306,10 +335,13 @@ __global__ void __launch_bounds__(DIAG_THREADS) k_potrf_diag(double* A, long lon
   __syncthreads();
   if (t == 0) logdet[kt] = (red[0] + red[1]) + (red[2] + red[3]);
   double* Dkk = Dinv + (long long)kt * TILE * (ldd + 1);
-  for (int e = t; e < TILE * TILE; e += DIAG_THREADS) {
+#pragma unroll 16
+  for (int b = 0; b < PER; ++b) {
+    const int e = t + DIAG_THREADS * b;
     const int i = e & (TILE - 1), k = e >> 7;
-    if (i >= k) Akk[i + (long long)k * lda] = S[i + k * SP];
-    Dkk[i + (long long)k * ldd] = dg_x(S, xd, i, k);
+    const double lv = S[i + k * SP], xv = dg_x(S, xd, i, k);
+    if (i >= k) Akk[i + (long long)k * lda] = lv;
+    Dkk[i + (long long)k * ldd] = xv;
   }
 }
 

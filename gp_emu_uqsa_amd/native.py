@@ -8,6 +8,7 @@ _emulatorclasses.py) is replaced here, not mirrored.
 from __future__ import annotations
 
 import ctypes as _ct
+import hashlib as _hashlib
 import os as _os
 import threading as _threading
 
@@ -112,6 +113,8 @@ class Context:
         self._h = h
         self.device = device
         self.n = self.d = self.q = 0
+        self._data_key = None
+        self._factor_key = None
 
     # -- lifetime
     def close(self):
@@ -146,9 +149,39 @@ class Context:
         q = H.shape[1]
         rr = None if r is None or _np.isscalar(r) else _f64(r, (n,))
         self._keep = (X, f, H, rr)
+        self._data_key = None
+        self._factor_key = None
         self._check(self.lib.gpe_set_data(self._h, n, d, q, _ptr(X), _ptr(f), _ptr(H), _ptr(rr)),
                     "gpe_set_data")
         self.n, self.d, self.q = n, d, q
+
+    @staticmethod
+    def _digest(*arrays):
+        h = _hashlib.blake2b(digest_size=16)
+        for a in arrays:
+            if a is None:
+                h.update(b"-")
+            else:
+                a = _np.ascontiguousarray(a, dtype=_np.float64)
+                h.update(str(a.shape).encode())
+                h.update(a.tobytes())
+        return h.hexdigest()
+
+    def ensure_data(self, X, f, H, r=None):
+        """set_data unless this exact (X, f, H, r) is already resident."""
+        key = self._digest(X, f, H, r)
+        if key != self._data_key:
+            self.set_data(X, f, H, r)
+            self._data_key = key
+
+    def ensure_factor(self, kernel, delta, nu, s2=1.0, r_scale=0.0):
+        """factor() unless the same factor of the resident data is already held."""
+        key = (int(kernel), tuple(_np.asarray(delta, float).ravel().tolist()), float(nu), float(s2),
+               float(r_scale), self._data_key)
+        if key != self._factor_key or self._data_key is None:
+            self._factor_key = None
+            self.factor(kernel, delta, nu, s2, r_scale)
+            self._factor_key = key
 
     # -- objective
     def objective(self, variant, kernel, hp, nu_fixed=0.0, want_grad=True):
@@ -157,6 +190,7 @@ class Context:
         llh = _ct.c_double(0.0)
         s2 = _ct.c_double(0.0)
         grad = _np.zeros(hp.size) if want_grad else None
+        self._factor_key = None            # the objective reuses the factor buffers
         rc = self.lib.gpe_objective(self._h, int(variant), int(kernel), _ptr(hp), hp.size,
                                     float(nu_fixed), 1 if want_grad else 0, _ct.byref(llh),
                                     _ptr(grad), _ct.byref(s2))
@@ -164,6 +198,7 @@ class Context:
         return llh.value, grad, s2.value
 
     def factor(self, kernel, delta, nu, s2=1.0, r_scale=0.0):
+        self._factor_key = None
         delta = _f64(delta).ravel()
         self._check(self.lib.gpe_factor(self._h, int(kernel), _ptr(delta), float(nu), float(s2),
                                         float(r_scale)), "gpe_factor")

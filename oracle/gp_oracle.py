@@ -64,7 +64,8 @@ def kernel_covar_ref(XT, XV, delta, nu, kind):
 def grad_delta_ref(xcol, delta_i, nu, exp_save, s2, kind):
     """dA/d(2 log delta_i), dense n x n.  _emulatorkernels.py:53-63 / :126-136."""
     n = xcol.size
-    p = _dist.pdist((xcol / delta_i).reshape(n, 1), "sqeuclidean")
+    w = 1.0 / delta_i
+    p = _dist.pdist((xcol * w).reshape(n, 1), "sqeuclidean")
     pref = s2 if kind == ALT else (1.0 - nu) * s2
     return _dist.squareform(pref * p * exp_save)
 

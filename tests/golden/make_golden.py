@@ -9,6 +9,7 @@ Fixtures:
   G3 posterior_*.npz   reconstructed example emulators: posterior mean/var, beta
   G4 train_*.npz       seeded toy-sim g.train() trajectory (objective x's, result)
   G5 scale_4096.npz    n=4096 d=10 gp4ml LLH+grad (X regenerated from the seed)
+  G6 host_*.npz        host-side setup() state: shuffle, T/V split, H, bounds, RNG
 Versions of numpy/scipy used are stored in every file ("meta").
 """
 from __future__ import annotations
@@ -246,6 +247,27 @@ def make_g4():
             shutil.rmtree(tmp)
 
 
+# ---------------------------------------------------------------- G6 (host logic)
+def make_g6():
+    """Host-side state of setup(): shuffled data, T/V split, H, bounds, guess grid."""
+    tmp = tempfile.mkdtemp()
+    shutil.copytree(os.path.join(REF, "examples/toy-sim"), os.path.join(tmp, "w"))
+    cwd = os.getcwd()
+    os.chdir(os.path.join(tmp, "w"))
+    try:
+        np.random.seed(0)
+        E = quiet(g.setup, "toy-sim_config")
+        guess = np.random.random_sample(10)
+        save("host_toysim_seed0.npz", x_full=E.all_data.x_full, y_full=E.all_data.y_full,
+             minmax=E.all_data.minmax, XT=E.training.inputs, fT=E.training.outputs,
+             HT=E.training.H, XV=E.validation.inputs, bounds=np.array(E.config.bounds, float),
+             cons=np.array([[np.nan if v is None else v for v in c] for c in E.opt_T.cons], float),
+             next_random=guess)
+    finally:
+        os.chdir(cwd)
+        shutil.rmtree(tmp)
+
+
 # ---------------------------------------------------------------- G5
 def make_g5():
     n, d = 4096, 10
@@ -261,7 +283,8 @@ def make_g5():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["G1", "G2", "G3", "G4", "G5"]
+    which = sys.argv[1:] or ["G1", "G2", "G3", "G4", "G5", "G6"]
     for w in which:
         print("==", w)
-        {"G1": make_g1, "G2": make_g2, "G3": make_g3, "G4": make_g4, "G5": make_g5}[w]()
+        {"G1": make_g1, "G2": make_g2, "G3": make_g3, "G4": make_g4, "G5": make_g5,
+         "G6": make_g6}[w]()

@@ -1,0 +1,43 @@
+"""CPU checks of the C-ABI library and the host logic (no GPU compute)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from gp_emu_uqsa_amd import native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    text = open(os.path.join(ROOT, "include", "gpemu.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|gpe_ctx\*|const char\*)\s+\*?(gpe_\w+)\s*\(",
+                                 text, flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(native.LIB_PATH)
+    names = _declared_symbols()
+    assert len(names) >= 15
+    for name in names:
+        assert hasattr(lib, name), name
+    assert set(names) == set(native.SIGNATURES), set(names) ^ set(native.SIGNATURES)
+
+
+def test_abi_version_and_no_device_fails_loudly():
+    lib = native.load_library()
+    assert lib.gpe_abi_version() == 1
+    if lib.gpe_device_count() == 0:
+        with pytest.raises(native.NativeUnavailable):
+            native.Context(0)
+        assert lib.gpe_create(0) is None
+        assert b"device" in lib.gpe_last_error(None)
+
+
+def test_literal_parser_accepts_numpy2_reprs():
+    from gp_emu_uqsa_amd.files import literal
+    assert literal("[[np.float64(0.0157), np.float64(0.9854)], [0.1, 2]]") == [[0.0157, 0.9854], [0.1, 2]]
+    assert literal("[ ]") == []
+    assert literal("[[0.05,1.0],[0.05,10.00]]") == [[0.05, 1.0], [0.05, 10.0]]

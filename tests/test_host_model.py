@@ -1,0 +1,84 @@
+"""Host-side drop-in surface on CPU: config/beliefs parsing, data shuffle and
+T/V split, basis matrix, bounds and RNG consumption vs the reference (G6)."""
+import os
+import shutil
+
+import numpy as np
+import pytest
+
+from gp_emu_uqsa_amd import files, model
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+EX = os.path.join(GOLD, "examples")
+
+
+@pytest.fixture()
+def toysim_dir(tmp_path, monkeypatch):
+    d = tmp_path / "toy"
+    shutil.copytree(os.path.join(EX, "toy-sim"), d)
+    monkeypatch.chdir(d)
+    return d
+
+
+def test_config_and_beliefs(toysim_dir):
+    c = files.Config("toy-sim_config")
+    assert c.tv_config == [10, 0, 2] and c.tries == 10 and c.constraints == "none"
+    assert c.delta_bounds == [] and c.bounds == ()
+    b = files.Beliefs(c.beliefs)
+    assert b.active == [] and b.basis_str == ["1.0", "x"] and b.basis_inf == [0]
+    assert b.fix_nugget == "T" and b.mucm == "T" and b.alt_nugget == "F"
+    assert b.delta == [1.0, 1.0] and b.nugget == 0.01
+
+
+def test_reconstruct_beliefs_minmax(tmp_path, monkeypatch):
+    monkeypatch.chdir(os.path.join(EX, "toy-sim", "reconstruct"))
+    b = files.Beliefs("toy-sim_beliefs-2f")
+    assert np.allclose(b.input_minmax, [[0.0157, 0.9854], [0.0133, 0.9981]])
+    assert b.fix_nugget == "F"
+
+
+def test_missing_key_exits(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    (tmp_path / "cfg").write_text("beliefs b\ninputs i\n")
+    with pytest.raises(SystemExit):
+        files.Config("cfg")
+
+
+def test_setup_state_matches_reference(toysim_dir):
+    """All_Data shuffle/scale/split, H and the RNG stream after setup (G6)."""
+    z = np.load(os.path.join(GOLD, "host_toysim_seed0.npz"))
+    np.random.seed(0)
+    c = files.Config("toy-sim_config")
+    b = files.Beliefs(c.beliefs)
+    par = model.Hyperparams(b)
+    basis = model.Basis(b)
+    tv = model.TV_config(*c.tv_config)
+    ad = model.All_Data(c.inputs, c.outputs, tv, b, par, True, True)
+    np.testing.assert_array_equal(ad.x_full, z["x_full"])
+    np.testing.assert_array_equal(ad.y_full, z["y_full"])
+    np.testing.assert_array_equal(ad.minmax, z["minmax"])
+    XT, fT = ad.choose_T()
+    XV, _ = ad.choose_V()
+    np.testing.assert_array_equal(XT, z["XT"])
+    np.testing.assert_array_equal(fT, z["fT"])
+    np.testing.assert_array_equal(XV, z["XV"])
+    np.testing.assert_array_equal(basis.design_matrix(XT), z["HT"])
+    # the reference's setup() consumes no further random numbers
+    np.testing.assert_array_equal(np.random.random_sample(10), z["next_random"])
+
+
+def test_final_beliefs_roundtrip(toysim_dir):
+    import types
+    c = files.Config("toy-sim_config")
+    b = files.Beliefs(c.beliefs)
+    E = types.SimpleNamespace(config=c, tv_conf=types.SimpleNamespace(no_of_trains=2),
+                              par=types.SimpleNamespace(beta=np.array([0.5, 2.8]),
+                                                        delta=np.array([0.2, 0.16]),
+                                                        sigma=np.float64(0.61), nugget=0.03),
+                              all_data=types.SimpleNamespace(input_minmax=[[np.float64(0.01), 0.98],
+                                                                           [0.013, 0.99]]))
+    b.final_beliefs(E, final=True)
+    b2 = files.Beliefs("toy-sim_beliefs-2f")
+    assert b2.delta == [0.2, 0.16] and b2.beta == [0.5, 2.8] and b2.sigma == 0.61
+    assert b2.input_minmax == [[0.01, 0.98], [0.013, 0.99]]
+    assert b2.active_index == [0, 1] and b2.output_index == 0
