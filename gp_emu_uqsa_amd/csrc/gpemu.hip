@@ -129,7 +129,8 @@ struct gpe_ctx {
   // profiling
   bool prof = false;
   hipEvent_t ev[16] = {};
-  std::vector<hipEvent_t> gev;  // pairs around GEMM launches
+  std::vector<hipEvent_t> gev;  // pool of event pairs around GEMM launches
+  size_t gev_used = 0;
   double phase_ms[8] = {0};
   double gemm_ms = 0.0, gemm_launches = 0.0, gemm_flops = 0.0;
 };
@@ -209,12 +210,14 @@ int launch_gemm_range(gpe_ctx* c, const Launch& L, hipStream_t st = nullptr) {
   const size_t lds = G_LDS_DOUBLES * sizeof(double);
   const GemmProb* pr = c->dprobs + L.first;
   if (c->prof) {
-    hipEvent_t e0, e1;
-    HIPCHK(c, hipEventCreate(&e0));
-    HIPCHK(c, hipEventCreate(&e1));
-    c->gev.push_back(e0);
-    c->gev.push_back(e1);
-    HIPCHK(c, hipEventRecord(e0, st));
+    if (c->gev_used + 2 > c->gev.size()) {
+      for (int i = 0; i < 256; ++i) {
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreate(&e));
+        c->gev.push_back(e);
+      }
+    }
+    HIPCHK(c, hipEventRecord(c->gev[c->gev_used], st));
   }
   switch (L.kind) {
     case 0: hipLaunchKernelGGL((k_gemm<false, false>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, c->dinfo); break;
@@ -224,7 +227,8 @@ int launch_gemm_range(gpe_ctx* c, const Launch& L, hipStream_t st = nullptr) {
   }
   HIPCHK(c, hipGetLastError());
   if (c->prof) {
-    HIPCHK(c, hipEventRecord(c->gev.back(), st));
+    HIPCHK(c, hipEventRecord(c->gev[c->gev_used + 1], st));
+    c->gev_used += 2;
     c->gemm_launches += 1.0;
     c->gemm_flops += L.flops;
   }
@@ -809,8 +813,7 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
   const double rscale = (gp4ml && kernel == GPE_KERNEL_ALT_NUG) ? 1.0 : 0.0;
   c->factor_valid = false;
   if (c->prof) {
-    for (auto& e : c->gev) hipEventDestroy(e);
-    c->gev.clear();
+    c->gev_used = 0;
     c->gemm_launches = c->gemm_flops = c->gemm_ms = 0.0;
   }
 
@@ -913,7 +916,7 @@ done:
       c->phase_ms[i] = ms;
     }
     double g = 0.0;
-    for (size_t i = 0; i + 1 < c->gev.size(); i += 2) {
+    for (size_t i = 0; i + 1 < c->gev_used; i += 2) {
       ms = 0.f;
       (void)hipEventElapsedTime(&ms, c->gev[i], c->gev[i + 1]);
       g += ms;
