@@ -36,6 +36,7 @@ struct Launch {       // one grouped GEMM launch of the cached schedule
   int first, count;   // descriptor range
   int tiles;
   double flops;       // algorithmic flops
+  long long list = -1;  // offset of its tile list in the device list array (-1: implicit order)
 };
 
 struct Plan {
@@ -49,6 +50,7 @@ struct Plan {
   int lauum = -1;
   std::vector<Launch> launches;
   std::vector<GemmProb> probs;
+  std::vector<unsigned> tiles;   // concatenated tile lists
 };
 
 // A factorisation workspace: two n_pad x n_pad buffers and their GEMM schedule.
@@ -95,6 +97,8 @@ struct gpe_ctx {
   size_t cpart_cap = 0;
   double* dcsum = nullptr;   // d+2
   GemmProb* dprobs = nullptr;
+  unsigned* dtiles = nullptr;    // tile lists: training plan [0, cap/2), aux plan [cap/2, cap)
+  size_t tiles_cap = 0;
 
   // posterior workspace
   double* dW1 = nullptr;
@@ -209,6 +213,7 @@ int launch_gemm_range(gpe_ctx* c, const Launch& L, hipStream_t st = nullptr) {
   if (!st) st = c->stream;
   const size_t lds = G_LDS_DOUBLES * sizeof(double);
   const GemmProb* pr = c->dprobs + L.first;
+  const unsigned* tl = (L.list >= 0) ? c->dtiles + L.list : nullptr;
   if (c->prof) {
     if (c->gev_used + 2 > c->gev.size()) {
       for (int i = 0; i < 256; ++i) {
@@ -220,10 +225,10 @@ int launch_gemm_range(gpe_ctx* c, const Launch& L, hipStream_t st = nullptr) {
     HIPCHK(c, hipEventRecord(c->gev[c->gev_used], st));
   }
   switch (L.kind) {
-    case 0: hipLaunchKernelGGL((k_gemm<false, false>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, c->dinfo); break;
-    case 1: hipLaunchKernelGGL((k_gemm<true, false>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, c->dinfo); break;
-    case 2: hipLaunchKernelGGL((k_gemm<true, true>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, c->dinfo); break;
-    default: hipLaunchKernelGGL((k_gemm<false, true>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, c->dinfo); break;
+    case 0: hipLaunchKernelGGL((k_gemm<false, false>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, tl, c->dinfo); break;
+    case 1: hipLaunchKernelGGL((k_gemm<true, false>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, tl, c->dinfo); break;
+    case 2: hipLaunchKernelGGL((k_gemm<true, true>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, tl, c->dinfo); break;
+    default: hipLaunchKernelGGL((k_gemm<false, true>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, tl, c->dinfo); break;
   }
   HIPCHK(c, hipGetLastError());
   if (c->prof) {
@@ -240,20 +245,69 @@ int prob_tiles(const GemmProb& p) {
   return (p.flags & G_CLOWER) ? p.mt * (p.mt + 1) / 2 : p.mt * p.nt;
 }
 
+// Order the tiles of one launch: rows (problem, ti) sorted longest-first, greedily
+// packed into 8 bins of equal work (one per XCD under round-robin dispatch, so a
+// row's A panel stays in one XCD's L2), bins interleaved block by block.
+std::vector<unsigned> order_tiles(const std::vector<GemmProb>& probs) {
+  struct Row { int p, ti; double w; std::vector<int> tj; };
+  std::vector<Row> rows;
+  for (int p = 0; p < (int)probs.size(); ++p) {
+    const GemmProb& P = probs[p];
+    for (int ti = 0; ti < P.mt; ++ti) {
+      int kb = 0, ke = P.K;
+      if (P.flags & G_KBEG_TI) kb = ti * TILE;
+      if (P.flags & G_KEND_TI) ke = std::min(ke, (ti + 1) * TILE);
+      const double wt = (double)std::max(ke - kb, 0) + 2.0 * GK;   // + fixed per-tile cost
+      Row r{p, ti, 0.0, {}};
+      const int tjmax = (P.flags & G_CLOWER) ? ti : P.nt - 1;
+      for (int tj = 0; tj <= tjmax; ++tj) r.tj.push_back(tj);
+      r.w = wt * (double)r.tj.size();
+      if (!r.tj.empty()) rows.push_back(std::move(r));
+    }
+  }
+  std::stable_sort(rows.begin(), rows.end(), [](const Row& a, const Row& b) {
+    return a.w / a.tj.size() > b.w / b.tj.size();   // longest tiles first
+  });
+  constexpr int NX = 8;
+  std::vector<std::vector<unsigned>> bins(NX);
+  std::vector<double> load(NX, 0.0);
+  for (const Row& r : rows) {
+    int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    load[x] += r.w;
+    for (int tj : r.tj) bins[x].push_back(((unsigned)r.p << 24) | ((unsigned)r.ti << 12) | (unsigned)tj);
+  }
+  std::vector<unsigned> out;
+  size_t longest = 0;
+  for (auto& b : bins) longest = std::max(longest, b.size());
+  for (size_t j = 0; j < longest; ++j)
+    for (int x = 0; x < NX; ++x)
+      if (j < bins[x].size()) out.push_back(bins[x][j]);
+  return out;
+}
+
 void add_launch(Plan& pl, int kind, std::vector<GemmProb> probs, double flops) {
   Launch L;
   L.kind = kind;
   L.first = (int)pl.probs.size();
   L.count = (int)probs.size();
   int t = 0;
+  bool listable = probs.size() < 256;
   for (auto& p : probs) {
     p.tile_begin = t;
     p.ntiles = prob_tiles(p);
     t += p.ntiles;
+    listable = listable && p.mt <= 4096 && p.nt <= 4096;
     pl.probs.push_back(p);
   }
   L.tiles = t;
   L.flops = flops;
+  if (listable) {
+    std::vector<unsigned> tl = order_tiles(probs);
+    if ((int)tl.size() == t) {
+      L.list = (long long)pl.tiles.size();
+      pl.tiles.insert(pl.tiles.end(), tl.begin(), tl.end());
+    }
+  }
   pl.launches.push_back(L);
 }
 
@@ -346,6 +400,23 @@ int build_plan(gpe_ctx* c, Fact& F) {
   for (auto& L : pl.launches) L.first += F.desc_base;
   HIPCHK(c, hipMemcpy(c->dprobs + F.desc_base, pl.probs.data(), pl.probs.size() * sizeof(GemmProb),
                       hipMemcpyHostToDevice));
+  // tile lists: each workspace owns half of the list array
+  const size_t half = pl.tiles.size() + 1;
+  const size_t need = 2 * half;
+  if (need > c->tiles_cap) {
+    // growing invalidates the other plan's uploaded lists: force its rebuild
+    CHK(dalloc(c, &c->dtiles, need));
+    c->tiles_cap = need;
+    Fact& other = (&F == &c->tr) ? c->aux : c->tr;
+    other.plan = Plan();
+  }
+  const size_t base = (F.desc_base == 0) ? 0 : c->tiles_cap / 2;
+  if (pl.tiles.size() > c->tiles_cap / 2) return fail(c, GPE_ERR_STATE, "tile list overflow");
+  for (auto& L : pl.launches)
+    if (L.list >= 0) L.list += (long long)base;
+  if (!pl.tiles.empty())
+    HIPCHK(c, hipMemcpy(c->dtiles + base, pl.tiles.data(), pl.tiles.size() * sizeof(unsigned),
+                        hipMemcpyHostToDevice));
   return GPE_OK;
 }
 
@@ -708,6 +779,7 @@ void gpe_destroy(gpe_ctx* c) {
     if (b) hipFree(b);
   if (c->dinfo) hipFree(c->dinfo);
   if (c->dprobs) hipFree(c->dprobs);
+  if (c->dtiles) hipFree(c->dtiles);
   if (c->hpin) hipHostFree(c->hpin);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);

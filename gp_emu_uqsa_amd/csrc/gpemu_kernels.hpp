@@ -522,8 +522,11 @@ struct GemmProb {
 };
 
 constexpr int GK = 16;
-constexpr int GP = 144;
-constexpr int G_LDS_DOUBLES = 2 * 2 * GK * GP;   // 9216 doubles = 73,728 B
+constexpr int GP = 144;    // [k][m] image of an M-contiguous operand: pitch 144 doubles
+constexpr int GQ = 18;     // [m][k] image of a K-contiguous operand: pitch 18 doubles
+                           // (16-B aligned rows, conflict-free fragment reads)
+constexpr int G_OPND = GK * GP;                  // 2304 doubles >= 128 * GQ
+constexpr int G_LDS_DOUBLES = 2 * 2 * G_OPND;    // 9216 doubles = 73,728 B
 
 // MFMA f64 16x16x4 accumulator layout: lane l, register r -> (row, col) of D
 __device__ inline int mfma64_row(int lane, int r) { return (lane >> 4) + 4 * r; }
@@ -564,8 +567,8 @@ __device__ __forceinline__ void gemm_gload(const double* __restrict__ Ab,
 template <bool AK, bool BK>
 __device__ __forceinline__ void gemm_sstore(double* lds, int buf, int tid, const double (&ra)[8],
                                             const double (&rb)[8]) {
-  double* As = lds + buf * (2 * GK * GP);
-  double* Bs = As + GK * GP;
+  double* As = lds + buf * (2 * G_OPND);
+  double* Bs = As + G_OPND;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int c = tid + 256 * s;
@@ -574,33 +577,46 @@ __device__ __forceinline__ void gemm_sstore(double* lds, int buf, int tid, const
       *reinterpret_cast<double2*>(As + kk * GP + mm) = make_double2(ra[2 * s], ra[2 * s + 1]);
     } else {
       const int mm = c >> 3, kk = (c & 7) * 2;
-      As[kk * GP + mm] = ra[2 * s];
-      As[(kk + 1) * GP + mm] = ra[2 * s + 1];
+      *reinterpret_cast<double2*>(As + mm * GQ + kk) = make_double2(ra[2 * s], ra[2 * s + 1]);
     }
     if (!BK) {
       const int kk = c >> 6, nn = (c & 63) * 2;
       *reinterpret_cast<double2*>(Bs + kk * GP + nn) = make_double2(rb[2 * s], rb[2 * s + 1]);
     } else {
       const int nn = c >> 3, kk = (c & 7) * 2;
-      Bs[kk * GP + nn] = rb[2 * s];
-      Bs[(kk + 1) * GP + nn] = rb[2 * s + 1];
+      *reinterpret_cast<double2*>(Bs + nn * GQ + kk) = make_double2(rb[2 * s], rb[2 * s + 1]);
     }
   }
 }
 
+// Optional tile list: entry = problem (8 bits) | ti (12 bits) | tj (12 bits), one per
+// workgroup, in the order the host chose (longest-first, rows grouped per XCD under
+// round-robin dispatch).  Speed only: any order gives the same result.
+__device__ __forceinline__ void tile_unpack(unsigned v, int& p, int& ti, int& tj) {
+  p = (int)(v >> 24);
+  ti = (int)((v >> 12) & 0xfffu);
+  tj = (int)(v & 0xfffu);
+}
+
 template <bool AK, bool BK>
 __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restrict__ probs, int nprob,
+                                                  const unsigned* __restrict__ tiles,
                                                   const int* __restrict__ abort_flag) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   if (abort_flag && *abort_flag) return;
-  int p = 0;
-  for (int i = 1; i < nprob; ++i)
-    if ((int)blockIdx.x >= probs[i].tile_begin) p = i;
+  int p = 0, ti, tj;
+  if (tiles) {
+    tile_unpack(tiles[blockIdx.x], p, ti, tj);
+  } else {
+    for (int i = 1; i < nprob; ++i)
+      if ((int)blockIdx.x >= probs[i].tile_begin) p = i;
+  }
   const GemmProb P = probs[p];
-  const int local = blockIdx.x - P.tile_begin;
-  int ti, tj;
-  if (P.flags & G_CLOWER) tri_decode(local, ti, tj);
-  else { ti = local % P.mt; tj = local / P.mt; }
+  if (!tiles) {
+    const int local = blockIdx.x - P.tile_begin;
+    if (P.flags & G_CLOWER) tri_decode(local, ti, tj);
+    else { ti = local % P.mt; tj = local / P.mt; }
+  }
   int kbeg = 0, kend = P.K;
   if (P.flags & G_KBEG_TI) kbeg = ti * TILE;
   if (P.flags & G_KEND_TI) kend = min(kend, (ti + 1) * TILE);
@@ -644,16 +660,22 @@ __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restrict__ pr
     __syncthreads();
     for (int s = 0; s < nk; ++s) {
       if (s + 1 < nk) gemm_gload<AK, BK>(Ab, Bb, P.lda, P.ldb, kbeg + (s + 1) * GK, tid, ra, rb);
-      const double* As = lds + (s & 1) * (2 * GK * GP);
-      const double* Bs = As + GK * GP;
+      const double* As = lds + (s & 1) * (2 * G_OPND);
+      const double* Bs = As + G_OPND;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const int krow = ks * 4 + (lane >> 4);
         double af[4], bf[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = As[krow * GP + wm + i * 16 + (lane & 15)];
+        for (int i = 0; i < 4; ++i) {
+          const int m = wm + i * 16 + (lane & 15);
+          af[i] = AK ? As[m * GQ + krow] : As[krow * GP + m];
+        }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bf[j] = Bs[krow * GP + wn + j * 16 + (lane & 15)];
+        for (int j = 0; j < 4; ++j) {
+          const int n = wn + j * 16 + (lane & 15);
+          bf[j] = BK ? Bs[n * GQ + krow] : Bs[krow * GP + n];
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
