@@ -145,7 +145,11 @@ __device__ __forceinline__ void dg_leaf(double* S, double* xd, int o, int lane, 
     a[k] = (row && k <= i) ? S[(o + i) + (o + k) * SP] : 0.0;
     x[k] = (k == i) ? 1.0 : 0.0;
   }
-  double rdiag[16];
+  // Column j of L is final after factor step j, so inverse step j (row j of
+  // X = L^-1 scaled by 1/L(j,j), then X(i,c) -= L(i,j) X(j,c) below) runs right
+  // behind it.  Updates are unconditional (no selects): the factor's rank-1 update
+  // only spoils a[k] for k > i (the never-read upper part), and the inverse uses a
+  // zero coefficient on rows i <= j so their final X rows stay exact.
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const double piv = dg_bcast(a[j], j);
@@ -154,26 +158,16 @@ __device__ __forceinline__ void dg_leaf(double* S, double* xd, int o, int lane, 
       return;  // wave-uniform
     }
     const double r = dg_rsq(piv);
-    rdiag[j] = r;
-    a[j] = (i > j) ? a[j] * r : (i == j ? piv * r : a[j]);
+    const double lij = (i > j) ? a[j] * r : (i == j ? piv * r : 0.0);
+    a[j] = (i >= j) ? lij : a[j];
 #pragma unroll
-    for (int k = j + 1; k < 16; ++k) {
-      const double lkj = dg_bcast(a[j], k);
-      if (k <= i) a[k] = fma(-a[j], lkj, a[k]);
-    }
-  }
-  // X = L^-1: row j of X is final once scaled by 1/L(j,j); rows below get
-  // X(i,c) -= L(i,j) X(j,c)
+    for (int k = j + 1; k < 16; ++k) a[k] = fma(-lij, dg_bcast(lij, k), a[k]);
+    const double sj = (i == j) ? r : 1.0;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
+    for (int c = 0; c <= j; ++c) x[c] *= sj;
+    const double coef = (i > j) ? lij : 0.0;
 #pragma unroll
-    for (int c = 0; c <= j; ++c)
-      if (i == j) x[c] *= rdiag[j];
-#pragma unroll
-    for (int c = 0; c <= j; ++c) {
-      const double xjc = dg_bcast(x[c], j);
-      if (i > j) x[c] = fma(-a[j], xjc, x[c]);
-    }
+    for (int c = 0; c <= j; ++c) x[c] = fma(-coef, dg_bcast(x[c], j), x[c]);
   }
   if (row) {
 #pragma unroll
@@ -335,13 +329,17 @@ __global__ void __launch_bounds__(DIAG_THREADS, 1) __attribute__((amdgpu_waves_p
   __syncthreads();
   if (t == 0) logdet[kt] = (red[0] + red[1]) + (red[2] + red[3]);
   double* Dkk = Dinv + (long long)kt * TILE * (ldd + 1);
-#pragma unroll 16
-  for (int b = 0; b < PER; ++b) {
-    const int e = t + DIAG_THREADS * b;
-    const int i = e & (TILE - 1), k = e >> 7;
-    const double lv = S[i + k * SP], xv = dg_x(S, xd, i, k);
-    if (i >= k) Akk[i + (long long)k * lda] = lv;
-    Dkk[i + (long long)k * ldd] = xv;
+  // copy-out as 16-byte stores: thread -> (row pair, column)
+#pragma unroll 8
+  for (int b = 0; b < PER / 2; ++b) {
+    const int e = t + DIAG_THREADS * b;          // 0 .. 8191
+    const int i = (e & 63) * 2, k = e >> 6;
+    const double l0 = S[i + k * SP], l1 = S[i + 1 + k * SP];
+    const double x0 = dg_x(S, xd, i, k), x1 = dg_x(S, xd, i + 1, k);
+    double* ap = Akk + i + (long long)k * lda;
+    if (i >= k) *reinterpret_cast<double2*>(ap) = make_double2(l0, l1);
+    else if (i + 1 >= k) ap[1] = l1;
+    *reinterpret_cast<double2*>(Dkk + i + (long long)k * ldd) = make_double2(x0, x1);
   }
 }
 
