@@ -46,6 +46,10 @@ struct Plan {
   // potrf with depth-1 look-ahead: per step kt the panel launch, the update of
   // column block kt+1 (critical path) and the rest of the trailing update
   std::vector<int> panel, colupd, rest;
+  // fused schedule (default): diag0, then per step panel(kt) and
+  // fused(kt) = { diag tile kt+1 (factored in-kernel), column kt+1, rest }
+  int diag0 = -1;
+  std::vector<int> fused;
   std::vector<int> trtri;   // launches in order
   int lauum = -1;
   std::vector<Launch> launches;
@@ -61,6 +65,7 @@ struct Fact {
   double* B = nullptr;   // Dinv tiles -> L^-1 (strictly-upper tiles: scratch)
   size_t cap = 0;
   double* logdet = nullptr;  // NB per-block log-determinant parts
+  int* flags = nullptr;      // NB diagonal-inverse ready flags (fused Cholesky)
   int desc_base = 0;         // first slot of its descriptors in the device array
   Plan plan;
 };
@@ -124,6 +129,9 @@ struct gpe_ctx {
 
   // A/B switch: GPEMU_DIAG=rows selects the register-blocked diagonal kernel
   bool diag_rows = false;
+  // A/B switch: GPEMU_POTRF=lookahead selects the two-stream look-ahead schedule
+  // with the standalone diagonal kernel instead of the fused one
+  bool potrf_lookahead = false;
 
   // look-ahead stream and events
   hipStream_t stream2 = nullptr;
@@ -211,7 +219,7 @@ int launch_pairs(gpe_ctx* c, const PairArgs& a, int nblocks) {
 
 int launch_gemm_range(gpe_ctx* c, const Launch& L, hipStream_t st = nullptr) {
   if (!st) st = c->stream;
-  const size_t lds = G_LDS_DOUBLES * sizeof(double);
+  const size_t lds = G_LDS_LAUNCH_DOUBLES * sizeof(double);
   const GemmProb* pr = c->dprobs + L.first;
   const unsigned* tl = (L.list >= 0) ? c->dtiles + L.list : nullptr;
   if (c->prof) {
@@ -251,8 +259,14 @@ int prob_tiles(const GemmProb& p) {
 std::vector<unsigned> order_tiles(const std::vector<GemmProb>& probs) {
   struct Row { int p, ti; double w; std::vector<int> tj; };
   std::vector<Row> rows;
+  std::vector<unsigned> tail;   // G_PANEL tiles wait on the G_DIAG tile: dispatch them last
   for (int p = 0; p < (int)probs.size(); ++p) {
     const GemmProb& P = probs[p];
+    if (P.flags & G_PANEL) {
+      for (int ti = 0; ti < P.mt; ++ti)
+        for (int tj = 0; tj < P.nt; ++tj) tail.push_back(((unsigned)p << 24) | ((unsigned)ti << 12) | (unsigned)tj);
+      continue;
+    }
     for (int ti = 0; ti < P.mt; ++ti) {
       int kb = 0, ke = P.K;
       if (P.flags & G_KBEG_TI) kb = ti * TILE;
@@ -277,11 +291,17 @@ std::vector<unsigned> order_tiles(const std::vector<GemmProb>& probs) {
     for (int tj : r.tj) bins[x].push_back(((unsigned)r.p << 24) | ((unsigned)r.ti << 12) | (unsigned)tj);
   }
   std::vector<unsigned> out;
+  for (int p = 0; p < (int)probs.size(); ++p)   // a factored diagonal tile starts first
+    if (probs[p].flags & G_DIAG) {
+      out.push_back((unsigned)p << 24);
+      for (auto& b : bins) b.erase(std::remove(b.begin(), b.end(), (unsigned)p << 24), b.end());
+    }
   size_t longest = 0;
   for (auto& b : bins) longest = std::max(longest, b.size());
   for (size_t j = 0; j < longest; ++j)
     for (int x = 0; x < NX; ++x)
       if (j < bins[x].size()) out.push_back(bins[x][j]);
+  out.insert(out.end(), tail.begin(), tail.end());
   return out;
 }
 
@@ -319,6 +339,7 @@ GemmProb mkprob(const double* A, long long lda, const double* B, long long ldb, 
   p.mt = mt; p.nt = nt; p.K = K; p.flags = flags;
   p.alpha = alpha; p.beta = beta;
   p.tile_begin = 0; p.ntiles = 0;
+  p.X = nullptr; p.ldx = 0; p.logdet = nullptr; p.diag_col0 = 0; p.flag = nullptr;
   return p;
 }
 
@@ -340,7 +361,47 @@ int build_plan(gpe_ctx* c, Fact& F) {
   pl.panel.assign(NB, -1);
   pl.colupd.assign(NB, -1);
   pl.rest.assign(NB, -1);
+  pl.fused.assign(NB, -1);
+  // fused schedule: launch kt (kt = -1 .. NB-2) = { diagonal tile t = kt+1 updated,
+  // factored and inverted in-kernel (G_DIAG); panel tiles (i, t), i > t, updated and
+  // then multiplied by X_t^T once the diagonal workgroup releases flags[t] (G_PANEL);
+  // the rest of the trailing update, tiles (i, j), i >= j > t }
+  auto diagprob = [&](int t, const double* Lp, int K, double alpha) {
+    GemmProb p = mkprob(Lp, ld, Lp, ld, tile(A, t, t), ld, 1, 1, K, G_DIAG, alpha, 1.0);
+    p.X = tile(B, t, t);
+    p.ldx = ld;
+    p.logdet = F.logdet + t;
+    p.diag_col0 = t * TILE;
+    p.flag = F.flags + t;
+    return p;
+  };
+  auto panelprob = [&](int t, const double* Lp, const double* Lt, int K, double alpha) {
+    GemmProb p = mkprob(Lp, ld, Lt, ld, tile(A, t + 1, t), ld, NB - t - 1, 1, K, G_PANEL, alpha, 1.0);
+    p.X = tile(B, t, t);
+    p.ldx = ld;
+    p.flag = F.flags + t;
+    return p;
+  };
+  if (!c->potrf_lookahead) {
+    std::vector<GemmProb> d0 = {diagprob(0, nullptr, 0, 1.0)};
+    if (NB >= 2) d0.push_back(panelprob(0, nullptr, nullptr, 0, 1.0));
+    pl.diag0 = (int)pl.launches.size();
+    add_launch(pl, 0, d0, (double)(NB - 1) * T * T * T);
+  }
   for (int kt = 0; kt + 1 < NB; ++kt) {
+    const int m = NB - kt - 1;
+    if (c->potrf_lookahead) break;
+    std::vector<GemmProb> fp = {diagprob(kt + 1, tile(A, kt + 1, kt), TILE, -1.0)};
+    if (m >= 2) {
+      fp.push_back(panelprob(kt + 1, tile(A, kt + 2, kt), tile(A, kt + 1, kt), TILE, -1.0));
+      fp.push_back(mkprob(tile(A, kt + 2, kt), ld, tile(A, kt + 2, kt), ld, tile(A, kt + 2, kt + 2), ld,
+                          m - 1, m - 1, TILE, G_CLOWER, -1.0, 1.0));
+    }
+    pl.fused[kt] = (int)pl.launches.size();
+    add_launch(pl, 0, fp, (double)m * T * ((double)m * T + 1.0) * T + (double)(m - 1) * T * T * T);
+  }
+  for (int kt = 0; kt + 1 < NB; ++kt) {
+    if (!c->potrf_lookahead) break;
     const int m = NB - kt - 1;
     // L(kt+1:, kt) = A(kt+1:, kt) * Dinv_kt^T     (opB(k,n) = Dinv(n,k): N-contiguous)
     pl.panel[kt] = (int)pl.launches.size();
@@ -435,6 +496,7 @@ int ensure_fact(gpe_ctx* c, Fact& F, long long n_pad) {
     F.n_pad = n_pad;
     F.NB = (int)(n_pad / TILE);
     CHK(dalloc(c, &F.logdet, (size_t)F.NB));
+    CHK(dalloc(c, &F.flags, (size_t)F.NB));
     F.plan = Plan();
   }
   return GPE_OK;
@@ -487,6 +549,14 @@ int kbuild(gpe_ctx* c, int kernel, double nu, double s2, double rscale) {
 int potrf(gpe_ctx* c, Fact& F) {
   const Plan& pl = F.plan;
   const int NB = F.NB;
+  if (!c->potrf_lookahead) {
+    // fused: one launch per step; the diagonal tile kt+1 is factored by the first
+    // workgroup of the trailing-update launch kt and its panel follows in-launch
+    HIPCHK(c, hipMemsetAsync(F.flags, 0, (size_t)NB * sizeof(int), c->stream));
+    CHK(launch_gemm_range(c, pl.launches[pl.diag0]));
+    for (int kt = 0; kt + 1 < NB; ++kt) CHK(launch_gemm_range(c, pl.launches[pl.fused[kt]]));
+    return GPE_OK;
+  }
   if ((int)c->ev_panel.size() < NB) {
     for (auto& e : c->ev_panel) (void)hipEventDestroy(e);
     for (auto& e : c->ev_rest) (void)hipEventDestroy(e);
@@ -667,6 +737,8 @@ int read_info_logdet(gpe_ctx* c, const Fact& F, int* info, double* logdetA) {
   HIPCHK(c, hipMemcpyAsync(c->hpin + F.NB, c->dinfo, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   std::memcpy(info, c->hpin + F.NB, sizeof(int));
+  if (*info == GEMM_WAIT_TIMEOUT)
+    return fail(c, GPE_ERR_HIP, "internal error: Cholesky panel wait timed out");
   double s = 0.0;
   for (int k = 0; k < F.NB; ++k) s += c->hpin[k];
   *logdetA = 2.0 * s;
@@ -737,6 +809,8 @@ gpe_ctx* gpe_create(int32_t device) {
   {
     const char* e = std::getenv("GPEMU_DIAG");
     c->diag_rows = e && std::string(e) == "rows";
+    const char* e2 = std::getenv("GPEMU_POTRF");
+    c->potrf_lookahead = e2 && std::string(e2) == "lookahead";
   }
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       !create_priority_stream(&c->stream2) ||
@@ -778,6 +852,8 @@ void gpe_destroy(gpe_ctx* c) {
   for (double* b : bufs)
     if (b) hipFree(b);
   if (c->dinfo) hipFree(c->dinfo);
+  if (c->tr.flags) hipFree(c->tr.flags);
+  if (c->aux.flags) hipFree(c->aux.flags);
   if (c->dprobs) hipFree(c->dprobs);
   if (c->dtiles) hipFree(c->dtiles);
   if (c->hpin) hipHostFree(c->hpin);

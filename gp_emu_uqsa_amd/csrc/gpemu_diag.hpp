@@ -1,0 +1,283 @@
+// gpemu_diag.hpp -- 128x128 diagonal-block Cholesky + inverse inside 72 KB of LDS.
+//
+// Used by the special first workgroup of each trailing-update launch (k_gemm with
+// a DIAG tile entry) and by k_potrf_diag_bp for the first block: the factorisation
+// of tile (k+1,k+1) then overlaps the rest of the update instead of following it.
+//
+// LDS: L in block-packed form -- the 36 lower 16x16 blocks (bi >= bk), block
+// bi*(bi+1)/2 + bk at 256*blk doubles, column-major inside the block -- exactly
+// 73,728 B, the GEMM's staging space; plus a 2 KB scratch for the current leaf
+// inverse.  After L is written out, X = L^-1 is assembled in place of it (X21
+// overwrites L21 once T = L21 X11 is in registers) and written out.
+//
+// Algorithm (16-wide right-looking inside the tile, depth-1 look-ahead):
+//   for jb: panel    -- L(ib,jb) = A(ib,jb) X_jb^T   (MFMA, ib > jb)
+//           wave 0   -- update block (jb+1,jb+1), then factor + invert it (leaf)
+//           waves 1-3-- the rest of A(ib,kb) -= L(ib,jb) L(kb,jb)^T (MFMA)
+//   X assembly: X21 = -X22 (L21 X11) at 32, 64, 128 (MFMA, accumulator of T
+//   reused as the B fragments of the second product).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace gpe {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int DB_LDS_DOUBLES = 36 * 256 + 256;   // block-packed L + leaf-inverse scratch
+constexpr int DB_EXTRA_DOUBLES = 128 + 8;        // X diagonal, reduction slots, flag
+
+// dev-tool phase timing (tools/hip/db_bench.hip): -DDB_TIMING
+#ifdef DB_TIMING
+__device__ unsigned long long db_tsc[8];
+#define DB_T(slot) do { if (threadIdx.x == 0) db_tsc[slot] += wall_clock64(); } while (0)
+#define DB_TN(slot) do { if (threadIdx.x == 0) db_tsc[slot] -= wall_clock64(); } while (0)
+#else
+#define DB_T(slot) do {} while (0)
+#define DB_TN(slot) do {} while (0)
+#endif
+
+__device__ __forceinline__ int db_off(int i, int k) {   // i >= k
+  const int bi = i >> 4, bk = k >> 4;
+  return (bi * (bi + 1) / 2 + bk) * 256 + (i & 15) + (k & 15) * 16;
+}
+
+__device__ __forceinline__ double db_bcast(double v, int src) {
+  const unsigned long long b = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, src);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), src);
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+__device__ __forceinline__ double db_rsq(double p) {
+  double r = __builtin_amdgcn_rsq(p);
+  return r * fma(-0.5 * p * r, r, 1.5);
+}
+
+// One wave factors and inverts diagonal block jb (16 x 16).  Lane i holds row i of
+// the block (a[k]) and column i of X = L^-1 (xc[r] = X(r, i)); per column j the
+// broadcasts of L(k, j), k > j, drive both the rank-1 update of a and the forward
+// substitution of every column of X.  L -> lower part of the block, X strictly-
+// lower -> upper part transposed (X(r,c) at (c,r)), X diagonal -> xdiag, X -> xs.
+// Sets *flag to the 1-based tile column of the first bad pivot.
+__device__ __forceinline__ void db_leaf(double* lb, double* xs, double* xdiag, int jb, int* flag) {
+  const int lane = threadIdx.x & 63;
+  const int i = lane;
+  const bool row = i < 16;
+  const int base = (jb * (jb + 1) / 2 + jb) * 256;
+  double a[16], xc[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    a[k] = (row && k <= i) ? lb[base + i + k * 16] : 0.0;
+    xc[k] = (k == i) ? 1.0 : 0.0;
+  }
+  int bad = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const double piv = db_bcast(a[j], j);
+    if (!(piv > 0.0) && bad == 0) bad = j + 1;   // wave-uniform; later columns are NaN garbage
+    const double r = db_rsq(piv);
+    const double lij = (i > j) ? a[j] * r : (i == j ? piv * r : 0.0);
+    a[j] = (i >= j) ? lij : a[j];
+    xc[j] *= r;
+#pragma unroll
+    for (int k = j + 1; k < 16; ++k) {
+      const double lkj = db_bcast(lij, k);
+      a[k] = fma(-lij, lkj, a[k]);
+      xc[k] = fma(-lkj, xc[j], xc[k]);
+    }
+  }
+  if (bad) {
+    if (lane == 0) *flag = jb * 16 + bad;
+  } else if (row) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (k <= i) lb[base + i + k * 16] = a[k];
+      if (k > i) lb[base + i + k * 16] = xc[k];     // X(k,i) at (i,k)
+      xs[k + i * 16] = xc[k];                       // column i of X (zero above)
+    }
+    xdiag[jb * 16 + i] = xc[i];
+  }
+}
+
+// A(po) -= L(pa) L(pb)^T for 16 x 16 blocks at LDS offsets pa, pb, po (one wave)
+__device__ __forceinline__ void db_syrk_block(double* lb, int pa, int pb, int po) {
+  const int lane = threadIdx.x & 63;
+  d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+  double av[4], bv[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int k = 4 * s + (lane >> 4);
+    av[s] = lb[pa + (lane & 15) + k * 16];
+    bv[s] = lb[pb + (lane & 15) + k * 16];        // L(kb,jb)^T(k, n) = L(kb,jb)(n, k)
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) lb[po + ((lane >> 4) + 4 * r) + (lane & 15) * 16] -= acc[r];
+}
+
+// X-level of the in-place inverse: for each instance of size 2h (offset o, o2 = o+h),
+// X21 = -X22 (L21 X11), X21 written over L21.  Work item = (instance, column block).
+template <int H>
+__device__ __forceinline__ void db_xlevel(double* lb) {
+  constexpr int NBH = H / 16, NINST = 128 / (2 * H);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // diagonal blocks hold X in their lower part only
+  auto xop = [&](int bi, int bk, int r, int c) -> double {
+    const int off = (bi * (bi + 1) / 2 + bk) * 256 + r + c * 16;
+    return (bi > bk || r >= c) ? lb[off] : 0.0;
+  };
+  constexpr int ITEMS = NINST * NBH;   // 4 for every level
+  static_assert(ITEMS == 4, "one item per wave");
+  const int inst = wave / NBH, cb = wave % NBH;
+  const int ob = inst * 2 * NBH, ob2 = ob + NBH;      // block offsets
+  d4 T[NBH];
+#pragma unroll
+  for (int ib = 0; ib < NBH; ++ib) {
+    T[ib] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kb = 0; kb < NBH; ++kb) {
+      if (kb < cb) continue;
+      double av[4], bv[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int k = 4 * s + (lane >> 4);
+        const int bi = ob2 + ib, bk = ob + kb;
+        av[s] = lb[(bi * (bi + 1) / 2 + bk) * 256 + (lane & 15) + k * 16];   // L21(m, k)
+        bv[s] = xop(ob + kb, ob + cb, k, lane & 15);                          // X11(k, n)
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) T[ib] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], T[ib], 0, 0, 0);
+    }
+  }
+  __syncthreads();    // every L21 read before any X21 write
+#pragma unroll
+  for (int ib = 0; ib < NBH; ++ib) {
+    d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kb = 0; kb <= ib; ++kb) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const double av = xop(ob2 + ib, ob2 + kb, lane & 15, 4 * s + (lane >> 4));   // X22(m, k)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, T[kb][s], acc, 0, 0, 0);
+      }
+    }
+    const int bi = ob2 + ib, bk = ob + cb;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      lb[(bi * (bi + 1) / 2 + bk) * 256 + ((lane >> 4) + 4 * r) + (lane & 15) * 16] = -acc[r];
+  }
+  __syncthreads();
+}
+
+// Factor + invert the tile held block-packed in lb[0 .. 36*256).  Writes L (lower)
+// to Lg, X = L^-1 (full tile, zero upper) to Xg, returns 0 or the 1-based column
+// of the first bad pivot; *logdet_out (thread 0) = sum log L_jj.
+// LDS: lb[0, DB_LDS_DOUBLES) plus DB_EXTRA_DOUBLES after it.
+__device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long long ldl, double* Xg,
+                                                long long ldx, double* logdet_out) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double* xs = lb + 36 * 256;             // current leaf inverse, column-major 16 x 16
+  double* xdiag = lb + DB_LDS_DOUBLES;    // 128 diagonal entries of X
+  double* red = xdiag + 128;              // 4
+  int* flag = reinterpret_cast<int*>(red + 4);
+  if (tid == 0) *flag = 0;
+  __syncthreads();
+  DB_TN(0);
+  DB_TN(1);
+  if (wave == 0) db_leaf(lb, xs, xdiag, 0, flag);
+  __syncthreads();
+  DB_T(1);
+  for (int jb = 0; jb < 8; ++jb) {
+    if (*flag) return *flag;
+    DB_TN(2);
+    // ---- panel: L(ib,jb) = A(ib,jb) X_jb^T, one 16x16 block per wave
+    for (int ib = jb + 1 + wave; ib < 8; ib += 4) {
+      const int bo = (ib * (ib + 1) / 2 + jb) * 256;
+      d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+      double av[4], bv[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int k = 4 * s + (lane >> 4);
+        av[s] = lb[bo + (lane & 15) + k * 16];        // A(ib,jb)(m, k)
+        bv[s] = xs[(lane & 15) + k * 16];             // X^T(k, n) = X(n, k)
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lb[bo + ((lane >> 4) + 4 * r) + (lane & 15) * 16] = acc[r];
+    }
+    __syncthreads();
+    DB_T(2);
+    if (jb == 7) break;
+    // ---- wave 0: update diagonal block jb+1 and factor it (look-ahead);
+    //      waves 1-3: the rest of the trailing update A(ib,kb) -= L(ib,jb) L(kb,jb)^T
+    DB_TN(1);
+    if (wave == 0) {
+      const int p1 = ((jb + 1) * (jb + 2) / 2 + jb) * 256;
+      DB_TN(6);
+      db_syrk_block(lb, p1, p1, ((jb + 1) * (jb + 2) / 2 + jb + 1) * 256);
+      DB_T(6);
+      DB_TN(5);
+      db_leaf(lb, xs, xdiag, jb + 1, flag);
+      DB_T(5);
+    } else {
+      const int m = 7 - jb, cnt = m * (m + 1) / 2;
+      for (int b = wave; b < cnt; b += 3) {          // b = 0 is the diagonal block (wave 0)
+        int rr = 0;
+        while ((rr + 1) * (rr + 2) / 2 <= b) ++rr;
+        const int ib = jb + 1 + rr, kb = jb + 1 + (b - rr * (rr + 1) / 2);
+        db_syrk_block(lb, (ib * (ib + 1) / 2 + jb) * 256, (kb * (kb + 1) / 2 + jb) * 256,
+                      (ib * (ib + 1) / 2 + kb) * 256);
+      }
+    }
+    __syncthreads();
+    DB_T(1);
+  }
+  DB_TN(4);
+  // ---- L out (lower part), log-determinant
+  for (int e = tid; e < 64 * 128; e += 256) {
+    const int i = (e & 63) * 2, k = e >> 6;
+    if (i + 1 < k) continue;
+    double* lp = Lg + i + (long long)k * ldl;
+    const double l1 = lb[db_off(i + 1, k)];
+    if (i >= k) *reinterpret_cast<double2*>(lp) = make_double2(lb[db_off(i, k)], l1);
+    else lp[1] = l1;
+  }
+  double lg = (tid < 128) ? log(lb[db_off(tid, tid)]) : 0.0;
+  for (int off = 32; off > 0; off >>= 1) lg += __shfl_down(lg, off, 64);
+  if ((tid & 63) == 0) red[tid >> 6] = lg;
+  __syncthreads();
+  if (tid == 0) *logdet_out = (red[0] + red[1]) + (red[2] + red[3]);
+  // ---- diagonal blocks -> X leaves (lower part): X(i,c) stored at (c,i), diag in xdiag
+  {
+    const int jb = tid >> 5, t = tid & 31;          // 8 blocks x 32 threads
+    const int base = (jb * (jb + 1) / 2 + jb) * 256;
+    for (int e = t; e < 256; e += 32) {
+      const int i = e & 15, c = e >> 4;
+      if (i > c) lb[base + i + c * 16] = lb[base + c + i * 16];
+      else if (i == c) lb[base + i + c * 16] = xdiag[jb * 16 + i];
+    }
+  }
+  __syncthreads();
+  DB_T(4);
+  DB_TN(3);
+  db_xlevel<16>(lb);
+  db_xlevel<32>(lb);
+  db_xlevel<64>(lb);
+  DB_T(3);
+  DB_TN(4);
+  // ---- X out: full tile, zero above the diagonal
+  for (int e = tid; e < 64 * 128; e += 256) {
+    const int i = (e & 63) * 2, k = e >> 6;
+    double x0 = 0.0, x1 = 0.0;
+    if (i >= k) x0 = lb[db_off(i, k)];
+    if (i + 1 >= k) x1 = lb[db_off(i + 1, k)];
+    *reinterpret_cast<double2*>(Xg + i + (long long)k * ldx) = make_double2(x0, x1);
+  }
+  DB_T(4);
+  DB_T(0);
+  return 0;
+}
+
+}  // namespace gpe

@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "gpemu_diag.hpp"
+
 namespace gpe {
 
 constexpr int TILE = 128;
@@ -507,7 +509,12 @@ __global__ void __launch_bounds__(DIAG_ROWS_THREADS) k_potrf_diag_rows(double* A
 // 4x4 v_mfma_f64_16x16x4_f64 accumulators.  K staged 16 deep, double-buffered
 // LDS ([k][m], pitch 144 doubles: conflict-free fragment reads).
 // ---------------------------------------------------------------------------
-enum : int { G_CLOWER = 1, G_KBEG_TI = 2, G_KEND_TI = 4 };
+// G_DIAG: a single diagonal tile whose updated value is then factored and inverted
+// in LDS by the same workgroup (gpemu_diag.hpp): L over C, L^-1 into X,
+// sum log L_jj into *logdet, info = diag_col0 + bad column on failure.
+// G_PANEL: a panel tile updated like any other, then (after the G_DIAG workgroup of
+// the same launch released *flag) multiplied by X^T: L = (C - L L^T) X^T.
+enum : int { G_CLOWER = 1, G_KBEG_TI = 2, G_KEND_TI = 4, G_DIAG = 8, G_PANEL = 16 };
 
 struct GemmProb {
   const double* A;
@@ -517,6 +524,11 @@ struct GemmProb {
   int mt, nt, K, flags;
   double alpha, beta;
   int tile_begin, ntiles;
+  double* X;          // G_DIAG only
+  long long ldx;
+  double* logdet;
+  int diag_col0;
+  int* flag;          // G_DIAG releases, G_PANEL waits
 };
 
 constexpr int GK = 16;
@@ -525,6 +537,10 @@ constexpr int GQ = 18;     // [m][k] image of a K-contiguous operand: pitch 18 d
                            // (16-B aligned rows, conflict-free fragment reads)
 constexpr int G_OPND = GK * GP;                  // 2304 doubles >= 128 * GQ
 constexpr int G_LDS_DOUBLES = 2 * 2 * G_OPND;    // 9216 doubles = 73,728 B
+// launch size: also holds the G_DIAG factorisation (block-packed L + scratch +
+// flag/reduction slots) -- 2 workgroups per CU still fit in 160 KB
+constexpr int G_LDS_LAUNCH_DOUBLES = DB_LDS_DOUBLES + DB_EXTRA_DOUBLES;
+static_assert(G_LDS_LAUNCH_DOUBLES >= G_LDS_DOUBLES, "LDS");
 
 // MFMA f64 16x16x4 accumulator layout: lane l, register r -> (row, col) of D
 __device__ inline int mfma64_row(int lane, int r) { return (lane >> 4) + 4 * r; }
@@ -596,10 +612,78 @@ __device__ __forceinline__ void tile_unpack(unsigned v, int& p, int& ti, int& tj
   tj = (int)(v & 0xfffu);
 }
 
+// K loop of one 128x128 output tile: acc += opA(Ab) opB(Bb) over nk stages of GK
+template <bool AK, bool BK>
+__device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
+                                           long long lda, long long ldb, int kbeg, int nk, double* lds,
+                                           d4 (&acc)[4][4]) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  double ra[8], rb[8];
+  gemm_gload<AK, BK>(Ab, Bb, lda, ldb, kbeg, tid, ra, rb);
+  gemm_sstore<AK, BK>(lds, 0, tid, ra, rb);
+  __syncthreads();
+  for (int s = 0; s < nk; ++s) {
+    if (s + 1 < nk) gemm_gload<AK, BK>(Ab, Bb, lda, ldb, kbeg + (s + 1) * GK, tid, ra, rb);
+    const double* As = lds + (s & 1) * (2 * G_OPND);
+    const double* Bs = As + G_OPND;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int krow = ks * 4 + (lane >> 4);
+      double af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = wm + i * 16 + (lane & 15);
+        af[i] = AK ? As[m * GQ + krow] : As[krow * GP + m];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = wn + j * 16 + (lane & 15);
+        bf[j] = BK ? Bs[n * GQ + krow] : Bs[krow * GP + n];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(bf[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (s + 1 < nk) gemm_sstore<AK, BK>(lds, (s + 1) & 1, tid, ra, rb);
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void gemm_store(double* Cb, long long ldc, double alpha, const d4 (&acc)[4][4]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = wm + i * 16 + (lane & 15);
+        const int n = wn + j * 16 + mfma64_row(lane, r);
+        Cb[m + (long long)n * ldc] = alpha * acc[i][j][r];
+      }
+}
+
+// bounded wait for a G_DIAG workgroup's release of *flag (1 = ready, 2 = failed);
+// returns the flag, or 0 after ~seconds (never expected: reported as an error)
+__device__ __forceinline__ int gemm_wait_flag(const int* flag) {
+  for (long it = 0; it < (1l << 22); ++it) {
+    const int v = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (v) return v;
+    __builtin_amdgcn_s_sleep(4);
+  }
+  return 0;
+}
+
+constexpr int GEMM_WAIT_TIMEOUT = 0x7fffffff;   // info value after a flag wait timed out
+
 template <bool AK, bool BK>
 __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restrict__ probs, int nprob,
                                                   const unsigned* __restrict__ tiles,
-                                                  const int* __restrict__ abort_flag) {
+                                                  int* __restrict__ abort_flag) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   if (abort_flag && *abort_flag) return;
   int p = 0, ti, tj;
@@ -650,50 +734,57 @@ __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restrict__ pr
       for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
   }
 
-  double ra[8], rb[8];
   const int nk = (kend - kbeg) / GK;
-  if (nk > 0) {
-    gemm_gload<AK, BK>(Ab, Bb, P.lda, P.ldb, kbeg, tid, ra, rb);
-    gemm_sstore<AK, BK>(lds, 0, tid, ra, rb);
-    __syncthreads();
-    for (int s = 0; s < nk; ++s) {
-      if (s + 1 < nk) gemm_gload<AK, BK>(Ab, Bb, P.lda, P.ldb, kbeg + (s + 1) * GK, tid, ra, rb);
-      const double* As = lds + (s & 1) * (2 * G_OPND);
-      const double* Bs = As + G_OPND;
+  if (nk > 0) gemm_kloop<AK, BK>(Ab, Bb, P.lda, P.ldb, kbeg, nk, lds, acc);
+
+  if constexpr (!AK && !BK) {
+    if (P.flags & G_DIAG) {
+      // updated diagonal tile -> block-packed LDS (lower half), then factor + invert;
+      // then release the panel workgroups of this launch waiting on *P.flag
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int krow = ks * 4 + (lane >> 4);
-        double af[4], bf[4];
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = wm + i * 16 + (lane & 15);
-          af[i] = AK ? As[m * GQ + krow] : As[krow * GP + m];
-        }
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int n = wn + j * 16 + (lane & 15);
-          bf[j] = BK ? Bs[n * GQ + krow] : Bs[krow * GP + n];
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(bf[j], af[i], acc[i][j], 0, 0, 0);
-      }
-      if (s + 1 < nk) gemm_sstore<AK, BK>(lds, (s + 1) & 1, tid, ra, rb);
+          for (int r = 0; r < 4; ++r) {
+            const int m = wm + i * 16 + (lane & 15);
+            const int n = wn + j * 16 + mfma64_row(lane, r);
+            if (m >= n) lds[db_off(m, n)] = P.alpha * acc[i][j][r];
+          }
       __syncthreads();
+      const int bad = db_factor_invert(lds, Cb, P.ldc, P.X, P.ldx, P.logdet);
+      if (bad && tid == 0 && abort_flag) atomicCAS(abort_flag, 0, P.diag_col0 + bad);
+      if (P.flag) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's L / X stores done
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(P.flag, bad ? 2 : 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    if (P.flags & G_PANEL) {
+      // updated panel tile -> C; wait for the diagonal inverse X of this launch;
+      // then L = C X^T over the same tile
+      gemm_store(Cb, P.ldc, P.alpha, acc);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      int* ready = reinterpret_cast<int*>(lds + G_LDS_LAUNCH_DOUBLES - 1);   // staging is idle here
+      if (tid == 0) *ready = gemm_wait_flag(P.flag);
+      __syncthreads();
+      const int st = *ready;
+      __syncthreads();
+      if (st != 1) {
+        if (st == 0 && tid == 0 && abort_flag) atomicCAS(abort_flag, 0, GEMM_WAIT_TIMEOUT);
+        return;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+      gemm_kloop<false, false>(Cb, P.X, P.ldc, P.ldx, 0, TILE / GK, lds, acc);
+      gemm_store(Cb, P.ldc, 1.0, acc);
+      return;
     }
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = wm + i * 16 + (lane & 15);
-        const int n = wn + j * 16 + mfma64_row(lane, r);
-        Cb[m + (long long)n * P.ldc] = P.alpha * acc[i][j][r];
-      }
+  gemm_store(Cb, P.ldc, P.alpha, acc);
 }
 
 // ---------------------------------------------------------------------------
