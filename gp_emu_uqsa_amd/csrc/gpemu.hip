@@ -46,9 +46,7 @@ struct Plan {
   // potrf with depth-1 look-ahead: per step kt the panel launch, the update of
   // column block kt+1 (critical path) and the rest of the trailing update
   std::vector<int> panel, colupd, rest;
-  // fused schedule (default): diag0, then per step panel(kt) and
-  // fused(kt) = { diag tile kt+1 (factored in-kernel), column kt+1, rest }
-  int diag0 = -1;
+  // fused schedule (default): one launch per column block (see build_plan)
   std::vector<int> fused;
   std::vector<int> trtri;   // launches in order
   int lauum = -1;
@@ -132,6 +130,9 @@ struct gpe_ctx {
   // A/B switch: GPEMU_POTRF=lookahead selects the two-stream look-ahead schedule
   // with the standalone diagonal kernel instead of the fused one
   bool potrf_lookahead = false;
+  // column-group widths of the fused Cholesky: {width, min remaining columns}, first
+  // match wins, else 1 (GPEMU_POTRF_W="4:64,2:32" style)
+  std::vector<std::pair<int, int>> potrf_groups = {{4, 80}, {2, 40}};
 
   // look-ahead stream and events
   hipStream_t stream2 = nullptr;
@@ -362,10 +363,16 @@ int build_plan(gpe_ctx* c, Fact& F) {
   pl.colupd.assign(NB, -1);
   pl.rest.assign(NB, -1);
   pl.fused.assign(NB, -1);
-  // fused schedule: launch kt (kt = -1 .. NB-2) = { diagonal tile t = kt+1 updated,
-  // factored and inverted in-kernel (G_DIAG); panel tiles (i, t), i > t, updated and
-  // then multiplied by X_t^T once the diagonal workgroup releases flags[t] (G_PANEL);
-  // the rest of the trailing update, tiles (i, j), i >= j > t }
+  // Fused schedule, one launch per column block t.  Columns are grouped (widths from
+  // potrf_groups: wide groups while the trailing matrix is large, width 1 at the end).
+  // Launch t, t at position h of group g:
+  //   critical: tile (t,t) updated by its pending columns [p0, t) -- the previous
+  //             group when h = 0, else the earlier columns of g -- then factored and
+  //             inverted in-kernel (G_DIAG); panel tiles (i,t), i > t, updated the
+  //             same way and multiplied by X_t^T once flags[t] is released (G_PANEL);
+  //   bulk:     part h of the trailing update by the previous group (K = its width
+  //             x 128) over columns j > start(g): part h holds column start(g)+h+1
+  //             (factored next) plus a balanced share of the columns after g.
   auto diagprob = [&](int t, const double* Lp, int K, double alpha) {
     GemmProb p = mkprob(Lp, ld, Lp, ld, tile(A, t, t), ld, 1, 1, K, G_DIAG, alpha, 1.0);
     p.X = tile(B, t, t);
@@ -382,23 +389,68 @@ int build_plan(gpe_ctx* c, Fact& F) {
     p.flag = F.flags + t;
     return p;
   };
-  if (!c->potrf_lookahead) {
-    std::vector<GemmProb> d0 = {diagprob(0, nullptr, 0, 1.0)};
-    if (NB >= 2) d0.push_back(panelprob(0, nullptr, nullptr, 0, 1.0));
-    pl.diag0 = (int)pl.launches.size();
-    add_launch(pl, 0, d0, (double)(NB - 1) * T * T * T);
-  }
-  for (int kt = 0; kt + 1 < NB; ++kt) {
-    const int m = NB - kt - 1;
-    if (c->potrf_lookahead) break;
-    std::vector<GemmProb> fp = {diagprob(kt + 1, tile(A, kt + 1, kt), TILE, -1.0)};
-    if (m >= 2) {
-      fp.push_back(panelprob(kt + 1, tile(A, kt + 2, kt), tile(A, kt + 1, kt), TILE, -1.0));
-      fp.push_back(mkprob(tile(A, kt + 2, kt), ld, tile(A, kt + 2, kt), ld, tile(A, kt + 2, kt + 2), ld,
-                          m - 1, m - 1, TILE, G_CLOWER, -1.0, 1.0));
+  // bulk problems: tiles (i, j), i >= j, j in [a, b), updated by columns [g0, g0 + K/128)
+  auto bulk = [&](std::vector<GemmProb>& fp, double& fl, int a, int b, int g0, int K) {
+    if (a >= b) return;
+    fp.push_back(mkprob(tile(A, a, g0), ld, tile(A, a, g0), ld, tile(A, a, a), ld, b - a, b - a, K,
+                        G_CLOWER, -1.0, 1.0));
+    fl += (double)(b - a) * T * ((double)(b - a) * T + 1.0) * K;
+    if (b < NB) {
+      fp.push_back(mkprob(tile(A, b, g0), ld, tile(A, a, g0), ld, tile(A, b, a), ld, NB - b, b - a, K, 0,
+                          -1.0, 1.0));
+      fl += 2.0 * (NB - b) * T * (double)(b - a) * T * K;
     }
-    pl.fused[kt] = (int)pl.launches.size();
-    add_launch(pl, 0, fp, (double)m * T * ((double)m * T + 1.0) * T + (double)(m - 1) * T * T * T);
+  };
+  std::vector<int> gs;   // group starts, then NB
+  for (int g = 0; g < NB;) {
+    gs.push_back(g);
+    int w = 1;
+    for (const auto& r : c->potrf_groups)
+      if (NB - g > r.second) { w = r.first; break; }
+    g += std::max(1, std::min(w, NB - g));
+  }
+  gs.push_back(NB);
+  for (int gi = 0; gi + 1 < (int)gs.size() && !c->potrf_lookahead; ++gi) {
+    const int gb = gs[gi], ge = gs[gi + 1], W1 = ge - gb;
+    // previous group's bulk: columns [gb+1, NB) split into W1 parts
+    std::vector<std::pair<int, int>> rng(W1, {0, 0});   // share of [ge, NB) per part
+    if (gi > 0) {
+      std::vector<double> load(W1, 0.0);
+      for (int h = 0; h + 1 < W1; ++h) load[h] = NB - (gb + h + 1);
+      double tot = 0.0;
+      for (int h = 0; h < W1; ++h) tot += load[h];
+      for (int j = ge; j < NB; ++j) tot += NB - j;
+      int j = ge;
+      for (int h = 0; h < W1; ++h) {
+        const int a = j;
+        const double target = tot * (h + 1) / W1;
+        double cum = 0.0;
+        for (int u = 0; u <= h; ++u) cum += load[u];
+        for (int u = ge; u < a; ++u) cum += NB - u;
+        while (j < NB && (h == W1 - 1 || cum + 0.5 * (NB - j) <= target)) cum += NB - j++;
+        rng[h] = {a, j};
+      }
+    }
+    for (int h = 0; h < W1; ++h) {
+      const int t = gb + h;
+      const int p0 = (h == 0) ? (gi > 0 ? gs[gi - 1] : 0) : gb;
+      const int K = (t - p0) * TILE;
+      const double al = K ? -1.0 : 1.0;
+      const int m = NB - t - 1;
+      std::vector<GemmProb> fp = {diagprob(t, K ? tile(A, t, p0) : nullptr, K, al)};
+      double fl = T * (T + 1.0) * K;
+      if (m >= 1) {
+        fp.push_back(panelprob(t, K ? tile(A, t + 1, p0) : nullptr, K ? tile(A, t, p0) : nullptr, K, al));
+        fl += 2.0 * m * T * T * K + (double)m * T * T * T;
+      }
+      if (gi > 0) {
+        const int g0 = gs[gi - 1], Kb = (gb - g0) * TILE;
+        if (h + 1 < W1) bulk(fp, fl, t + 1, t + 2, g0, Kb);   // the column factored next
+        bulk(fp, fl, rng[h].first, rng[h].second, g0, Kb);
+      }
+      pl.fused[t] = (int)pl.launches.size();
+      add_launch(pl, 0, fp, fl);
+    }
   }
   for (int kt = 0; kt + 1 < NB; ++kt) {
     if (!c->potrf_lookahead) break;
@@ -553,8 +605,7 @@ int potrf(gpe_ctx* c, Fact& F) {
     // fused: one launch per step; the diagonal tile kt+1 is factored by the first
     // workgroup of the trailing-update launch kt and its panel follows in-launch
     HIPCHK(c, hipMemsetAsync(F.flags, 0, (size_t)NB * sizeof(int), c->stream));
-    CHK(launch_gemm_range(c, pl.launches[pl.diag0]));
-    for (int kt = 0; kt + 1 < NB; ++kt) CHK(launch_gemm_range(c, pl.launches[pl.fused[kt]]));
+    for (int t = 0; t < NB; ++t) CHK(launch_gemm_range(c, pl.launches[pl.fused[t]]));
     return GPE_OK;
   }
   if ((int)c->ev_panel.size() < NB) {
@@ -811,6 +862,21 @@ gpe_ctx* gpe_create(int32_t device) {
     c->diag_rows = e && std::string(e) == "rows";
     const char* e2 = std::getenv("GPEMU_POTRF");
     c->potrf_lookahead = e2 && std::string(e2) == "lookahead";
+    if (const char* e3 = std::getenv("GPEMU_POTRF_W")) {
+      c->potrf_groups.clear();
+      std::string spec(e3);
+      size_t pos = 0;
+      while (pos < spec.size()) {
+        size_t end = spec.find(',', pos);
+        if (end == std::string::npos) end = spec.size();
+        const std::string item = spec.substr(pos, end - pos);
+        const size_t colon = item.find(':');
+        const int w = std::atoi(item.substr(0, colon).c_str());
+        const int lim = colon == std::string::npos ? 0 : std::atoi(item.substr(colon + 1).c_str());
+        if (w >= 1 && w <= 8) c->potrf_groups.push_back({w, lim});
+        pos = end + 1;
+      }
+    }
   }
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       !create_priority_stream(&c->stream2) ||

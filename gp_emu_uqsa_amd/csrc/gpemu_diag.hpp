@@ -53,49 +53,66 @@ __device__ __forceinline__ double db_rsq(double p) {
   return r * fma(-0.5 * p * r, r, 1.5);
 }
 
-// One wave factors and inverts diagonal block jb (16 x 16).  Lane i holds row i of
-// the block (a[k]) and column i of X = L^-1 (xc[r] = X(r, i)); per column j the
-// broadcasts of L(k, j), k > j, drive both the rank-1 update of a and the forward
-// substitution of every column of X.  L -> lower part of the block, X strictly-
-// lower -> upper part transposed (X(r,c) at (c,r)), X diagonal -> xdiag, X -> xs.
-// Sets *flag to the 1-based tile column of the first bad pivot.
+__device__ __forceinline__ double db_perm(double v, int src_lane) {
+  const unsigned long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(unsigned)b);
+  const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(unsigned)(b >> 32));
+  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// One wave factors and inverts diagonal block jb (16 x 16) with all 64 lanes:
+// lane = i + 16 q holds row i of the block at columns k = 4k'+q (a[k']) and rows
+// r = 4r'+q of column i of X = L^-1 (xc[r']).  Per column j the owners of column j
+// compute L(., j) and two permutes hand every lane its row's multiplier L(i, j) and
+// the four L(k, j) it needs; the same values drive the forward substitution of X.
+// L -> lower part of the block, X strictly-lower -> upper part transposed
+// (X(r,c) at (c,r)), X diagonal -> xdiag, X -> xs.  *flag = 1-based tile column
+// of the first bad pivot.
 __device__ __forceinline__ void db_leaf(double* lb, double* xs, double* xdiag, int jb, int* flag) {
   const int lane = threadIdx.x & 63;
-  const int i = lane;
-  const bool row = i < 16;
+  const int i = lane & 15, q = lane >> 4;
   const int base = (jb * (jb + 1) / 2 + jb) * 256;
-  double a[16], xc[16];
+  double a[4], xc[4];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    a[k] = (row && k <= i) ? lb[base + i + k * 16] : 0.0;
-    xc[k] = (k == i) ? 1.0 : 0.0;
+  for (int kk = 0; kk < 4; ++kk) {
+    const int k = 4 * kk + q;
+    a[kk] = (k <= i) ? lb[base + i + k * 16] : 0.0;
+    xc[kk] = (k == i) ? 1.0 : 0.0;
   }
   int bad = 0;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const double piv = db_bcast(a[j], j);
+    const int qj = j & 3, kj = j >> 2;
+    const double piv = db_bcast(a[kj], j + 16 * qj);
     if (!(piv > 0.0) && bad == 0) bad = j + 1;   // wave-uniform; later columns are NaN garbage
     const double r = db_rsq(piv);
-    const double lij = (i > j) ? a[j] * r : (i == j ? piv * r : 0.0);
-    a[j] = (i >= j) ? lij : a[j];
-    xc[j] *= r;
+    // owners of column j (q == qj): L(i, j) for i >= j, 0 above
+    const double v = (i > j) ? a[kj] * r : (i == j ? piv * r : 0.0);
+    if (q == qj) a[kj] = (i >= j) ? v : a[kj];
+    const double lij = db_perm(v, i + 16 * qj);                  // L(i, j)
+    double lk[4];
 #pragma unroll
-    for (int k = j + 1; k < 16; ++k) {
-      const double lkj = db_bcast(lij, k);
-      a[k] = fma(-lij, lkj, a[k]);
-      xc[k] = fma(-lkj, xc[j], xc[k]);
+    for (int kk = 0; kk < 4; ++kk) lk[kk] = db_perm(v, 4 * kk + q + 16 * qj);   // L(4kk+q, j)
+    if (q == qj) xc[kj] *= r;                                    // X(j, i) final
+    const double xji = db_perm(xc[kj], i + 16 * qj);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const bool below = 4 * kk + q > j;
+      const double c = below ? lk[kk] : 0.0;
+      a[kk] = fma(-lij, c, a[kk]);
+      xc[kk] = fma(-c, xji, xc[kk]);
     }
   }
   if (bad) {
     if (lane == 0) *flag = jb * 16 + bad;
-  } else if (row) {
+    return;
+  }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      if (k <= i) lb[base + i + k * 16] = a[k];
-      if (k > i) lb[base + i + k * 16] = xc[k];     // X(k,i) at (i,k)
-      xs[k + i * 16] = xc[k];                       // column i of X (zero above)
-    }
-    xdiag[jb * 16 + i] = xc[i];
+  for (int kk = 0; kk < 4; ++kk) {
+    const int k = 4 * kk + q;
+    lb[base + i + k * 16] = (k <= i) ? a[kk] : xc[kk];   // L lower / X(k,i) at (i,k) upper
+    xs[k + i * 16] = xc[kk];                             // X(k, i), zero for k < i
+    if (k == i) xdiag[jb * 16 + i] = xc[kk];
   }
 }
 

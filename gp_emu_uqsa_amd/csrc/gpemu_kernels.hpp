@@ -667,15 +667,27 @@ __device__ __forceinline__ void gemm_store(double* Cb, long long ldc, double alp
       }
 }
 
-// bounded wait for a G_DIAG workgroup's release of *flag (1 = ready, 2 = failed);
+// Cross-workgroup hand-off inside one launch (MI355X guide, inter-workgroup
+// visibility): producer = plain stores, every storing wave s_waitcnt vmcnt(0),
+// barrier, one lane: agent release fence, s_waitcnt, relaxed sc1 flag store;
+// consumer = relaxed sc1 poll, one agent acquire fence, s_waitcnt, barrier.
+__device__ __forceinline__ void gemm_publish_flag(int* flag, int v) {   // one lane, after the barrier
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// bounded wait (one lane) for a G_DIAG workgroup's flag (1 = ready, 2 = failed);
 // returns the flag, or 0 after ~seconds (never expected: reported as an error)
 __device__ __forceinline__ int gemm_wait_flag(const int* flag) {
-  for (long it = 0; it < (1l << 22); ++it) {
-    const int v = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    if (v) return v;
-    __builtin_amdgcn_s_sleep(4);
+  int v = 0;
+  for (long it = 0; it < (1l << 22) && v == 0; ++it) {
+    v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v == 0) __builtin_amdgcn_s_sleep(8);
   }
-  return 0;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return v;
 }
 
 constexpr int GEMM_WAIT_TIMEOUT = 0x7fffffff;   // info value after a flag wait timed out
@@ -757,7 +769,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restrict__ pr
       if (P.flag) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's L / X stores done
         __syncthreads();
-        if (tid == 0) __hip_atomic_store(P.flag, bad ? 2 : 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) gemm_publish_flag(P.flag, bad ? 2 : 1);
       }
       return;
     }
