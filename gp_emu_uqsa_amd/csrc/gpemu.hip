@@ -130,6 +130,7 @@ struct gpe_ctx {
   // A/B switch: GPEMU_POTRF=lookahead selects the two-stream look-ahead schedule
   // with the standalone diagonal kernel instead of the fused one
   bool potrf_lookahead = false;
+  bool skinny_valu = false;   // GPEMU_SKINNY=valu: the VALU skinny kernels (A/B)
   // column-group widths of the fused Cholesky: {width, min remaining columns}, first
   // match wins, else 1 (GPEMU_POTRF_W="4:64,2:32" style)
   std::vector<std::pair<int, int>> potrf_groups = {{4, 80}, {2, 40}};
@@ -669,14 +670,25 @@ int skinny(gpe_ctx* c, bool transposed, const double* M, long long ldm, int ntr,
   a.abort_flag = c->dinfo;
   const int pm = pmax_bucket(P);
   dim3 grid(nit * nch);
-  if (!transposed) {
-    if (pm == 8) hipLaunchKernelGGL(k_trmm_skinny_n<8>, grid, dim3(256), 0, c->stream, a);
-    else if (pm == 16) hipLaunchKernelGGL(k_trmm_skinny_n<16>, grid, dim3(256), 0, c->stream, a);
-    else hipLaunchKernelGGL(k_trmm_skinny_n<32>, grid, dim3(256), 0, c->stream, a);
+  if (c->skinny_valu) {
+    if (!transposed) {
+      if (pm == 8) hipLaunchKernelGGL(k_trmm_skinny_n<8>, grid, dim3(256), 0, c->stream, a);
+      else if (pm == 16) hipLaunchKernelGGL(k_trmm_skinny_n<16>, grid, dim3(256), 0, c->stream, a);
+      else hipLaunchKernelGGL(k_trmm_skinny_n<32>, grid, dim3(256), 0, c->stream, a);
+    } else {
+      if (pm == 8) hipLaunchKernelGGL(k_trmm_skinny_t<8>, grid, dim3(256), 0, c->stream, a);
+      else if (pm == 16) hipLaunchKernelGGL(k_trmm_skinny_t<16>, grid, dim3(256), 0, c->stream, a);
+      else hipLaunchKernelGGL(k_trmm_skinny_t<32>, grid, dim3(256), 0, c->stream, a);
+    }
   } else {
-    if (pm == 8) hipLaunchKernelGGL(k_trmm_skinny_t<8>, grid, dim3(256), 0, c->stream, a);
-    else if (pm == 16) hipLaunchKernelGGL(k_trmm_skinny_t<16>, grid, dim3(256), 0, c->stream, a);
-    else hipLaunchKernelGGL(k_trmm_skinny_t<32>, grid, dim3(256), 0, c->stream, a);
+    const bool p16 = P <= 16;
+    if (!transposed) {
+      if (p16) hipLaunchKernelGGL((k_skinny_mfma<16, false>), grid, dim3(256), 0, c->stream, a);
+      else hipLaunchKernelGGL((k_skinny_mfma<32, false>), grid, dim3(256), 0, c->stream, a);
+    } else {
+      if (p16) hipLaunchKernelGGL((k_skinny_mfma<16, true>), grid, dim3(256), 0, c->stream, a);
+      else hipLaunchKernelGGL((k_skinny_mfma<32, true>), grid, dim3(256), 0, c->stream, a);
+    }
   }
   HIPCHK(c, hipGetLastError());
   const int mode = lower ? (transposed ? 1 : 0) : 2;
@@ -860,6 +872,8 @@ gpe_ctx* gpe_create(int32_t device) {
   {
     const char* e = std::getenv("GPEMU_DIAG");
     c->diag_rows = e && std::string(e) == "rows";
+    const char* es = std::getenv("GPEMU_SKINNY");
+    c->skinny_valu = es && std::string(es) == "valu";
     const char* e2 = std::getenv("GPEMU_POTRF");
     c->potrf_lookahead = e2 && std::string(e2) == "lookahead";
     if (const char* e3 = std::getenv("GPEMU_POTRF_W")) {
@@ -1265,9 +1279,15 @@ int gpe_posterior(gpe_ctx* c, int64_t m, const double* Xs, const double* Hs, con
       a.pstride = mp * P; a.P = P; a.ntr = c->NB; a.lower = 0; a.nit = mt; a.abort_flag = nullptr;
       const int pm = pmax_bucket(P);
       dim3 grid(mt * nch);
-      if (pm == 8) hipLaunchKernelGGL(k_trmm_skinny_t<8>, grid, dim3(256), 0, c->stream, a);
-      else if (pm == 16) hipLaunchKernelGGL(k_trmm_skinny_t<16>, grid, dim3(256), 0, c->stream, a);
-      else hipLaunchKernelGGL(k_trmm_skinny_t<32>, grid, dim3(256), 0, c->stream, a);
+      if (c->skinny_valu) {
+        if (pm == 8) hipLaunchKernelGGL(k_trmm_skinny_t<8>, grid, dim3(256), 0, c->stream, a);
+        else if (pm == 16) hipLaunchKernelGGL(k_trmm_skinny_t<16>, grid, dim3(256), 0, c->stream, a);
+        else hipLaunchKernelGGL(k_trmm_skinny_t<32>, grid, dim3(256), 0, c->stream, a);
+      } else if (P <= 16) {
+        hipLaunchKernelGGL((k_skinny_mfma<16, true>), grid, dim3(256), 0, c->stream, a);
+      } else {
+        hipLaunchKernelGGL((k_skinny_mfma<32, true>), grid, dim3(256), 0, c->stream, a);
+      }
       HIPCHK(c, hipGetLastError());
       const long long tot = mp * P;
       hipLaunchKernelGGL(k_reduce_chunks, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,

@@ -920,6 +920,129 @@ __global__ void __launch_bounds__(256) k_trmm_skinny_t(SkinnyArgs a) {
   }
 }
 
+// MFMA form of the skinny products (same grid, chunks and partial layout as the
+// VALU kernels above): D(p, i) = sum_k R(k, p) op(M)(k, i) on v_mfma_f64_16x16x4_f64,
+// p = rows of the MFMA tile (P <= PM, zero-padded), i = 128 output rows per
+// workgroup (32 per wave).  TR: op(M)(k,i) = M(k,i) (k contiguous: LDS image [i][k],
+// pitch 34); else op(M)(k,i) = M(i,k) (i contiguous: image [k][i], pitch 144).
+// 32 k per stage, registers prefetch the next stage.  HBM-bound by design.
+constexpr int SKM_GK = 32;
+constexpr int SKM_PT = 34;     // [i][k] / [p][k] pitch (doubles)
+constexpr int SKM_PN = 144;    // [k][i] pitch (doubles)
+
+template <int PM, bool TR>
+__device__ __forceinline__ void skm_gload(const double* Mb, long long ldm, const double* R, long long ldr,
+                                          int P, int k0, int tid, double (&mv)[16], double (&rv)[PM / 8]) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int c = tid + 256 * u;
+    if (TR) {   // column i = c >> 4, k pair (c & 15) * 2
+      const int i = c >> 4, kk = (c & 15) * 2;
+      const double2 v = *reinterpret_cast<const double2*>(Mb + (long long)i * ldm + k0 + kk);
+      mv[2 * u] = v.x;
+      mv[2 * u + 1] = v.y;
+    } else {    // row k = c >> 6, i pair (c & 63) * 2
+      const int kk = c >> 6, i = (c & 63) * 2;
+      const double2 v = *reinterpret_cast<const double2*>(Mb + i + (long long)(k0 + kk) * ldm);
+      mv[2 * u] = v.x;
+      mv[2 * u + 1] = v.y;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < PM / 8; ++u) {
+    const int e = tid + 256 * u;           // PM * 32 entries
+    const int kk = e & (SKM_GK - 1), pp = e >> 5;
+    rv[u] = (pp < P) ? R[(long long)(k0 + kk) + (long long)pp * ldr] : 0.0;
+  }
+}
+
+template <int PM, bool TR>
+__device__ __forceinline__ void skm_sstore(double* Ms, double* Rs, int tid, const double (&mv)[16],
+                                           const double (&rv)[PM / 8]) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int c = tid + 256 * u;
+    if (TR) {
+      const int i = c >> 4, kk = (c & 15) * 2;
+      *reinterpret_cast<double2*>(Ms + i * SKM_PT + kk) = make_double2(mv[2 * u], mv[2 * u + 1]);
+    } else {
+      const int kk = c >> 6, i = (c & 63) * 2;
+      *reinterpret_cast<double2*>(Ms + kk * SKM_PN + i) = make_double2(mv[2 * u], mv[2 * u + 1]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < PM / 8; ++u) {
+    const int e = tid + 256 * u;
+    const int kk = e & (SKM_GK - 1), pp = e >> 5;
+    Rs[pp * SKM_PT + kk] = rv[u];
+  }
+}
+
+template <int PM, bool TR>
+__global__ void __launch_bounds__(256) k_skinny_mfma(SkinnyArgs a) {
+  constexpr int MIMG = TR ? TILE * SKM_PT : SKM_GK * SKM_PN;
+  __shared__ __attribute__((aligned(16))) double Ms[MIMG];
+  __shared__ __attribute__((aligned(16))) double Rs[PM * SKM_PT];
+  if (a.abort_flag && *a.abort_flag) return;
+  const int it = blockIdx.x % a.nit, ch = blockIdx.x / a.nit;
+  int kt0, kt1;
+  if (TR) {
+    const int kbase = a.lower ? it : 0;
+    kt0 = kbase + ch * SK_CH;
+    if (kt0 >= a.ntr) return;
+    kt1 = min(kt0 + SK_CH, a.ntr);
+  } else {
+    const int kend = a.lower ? it + 1 : a.ntr;
+    kt0 = ch * SK_CH;
+    if (kt0 >= kend) return;
+    kt1 = min(kt0 + SK_CH, kend);
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int P = a.P;
+  const double* Mb = TR ? a.M + (long long)(it * TILE) * a.ldm : a.M + (long long)it * TILE;
+  constexpr int NPT = PM / 16;
+  d4 acc[NPT][2];
+#pragma unroll
+  for (int u = 0; u < NPT; ++u) acc[u][0] = acc[u][1] = d4{0.0, 0.0, 0.0, 0.0};
+  double mv[16];
+  double rv[PM / 8];
+  const int kb = kt0 * TILE, ke = kt1 * TILE;
+  skm_gload<PM, TR>(Mb, a.ldm, a.R, a.ldr, P, kb, tid, mv, rv);
+  for (int k0 = kb; k0 < ke; k0 += SKM_GK) {
+    __syncthreads();
+    skm_sstore<PM, TR>(Ms, Rs, tid, mv, rv);
+    __syncthreads();
+    if (k0 + SKM_GK < ke) skm_gload<PM, TR>(Mb, a.ldm, a.R, a.ldr, P, k0 + SKM_GK, tid, mv, rv);
+#pragma unroll
+    for (int s = 0; s < SKM_GK / 4; ++s) {
+      const int kk = 4 * s + (lane >> 4);
+      double bf[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int i = wave * 32 + j * 16 + (lane & 15);
+        bf[j] = TR ? Ms[i * SKM_PT + kk] : Ms[kk * SKM_PN + i];
+      }
+#pragma unroll
+      for (int u = 0; u < NPT; ++u) {
+        const double af = Rs[(u * 16 + (lane & 15)) * SKM_PT + kk];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[u][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af, bf[j], acc[u][j], 0, 0, 0);
+      }
+    }
+  }
+  double* out = a.part + (long long)ch * a.pstride + it * TILE;
+#pragma unroll
+  for (int u = 0; u < NPT; ++u)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int pp = u * 16 + mfma64_row(lane, r);
+        const int i = wave * 32 + j * 16 + (lane & 15);
+        if (pp < P) out[i + (long long)pp * a.ldp] = acc[u][j][r];
+      }
+}
+
 // out[i + p*ldp] = sum_{ch < nch(i)} part[ch][i + p*ldp], fixed order
 // nch(i) for the n-kernel (lower): ceil((it+1)/CH); t-kernel lower: ceil((ntr-it)/CH)
 __global__ void k_reduce_chunks(const double* part, long long pstride, double* out,
