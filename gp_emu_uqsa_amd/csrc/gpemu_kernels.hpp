@@ -1177,34 +1177,45 @@ __global__ void __launch_bounds__(256) k_contract(const double* Ainv, long long 
   __syncthreads();
   if (gi < n_valid) {
     const double* acol = Ainv + gi + (long long)tj * TILE * lda;
-    const int cend = (ti == tj) ? r + 1 : TILE;
-    for (int c = (tid >> 7); c < cend; c += 2) {
-      const int gj = tj * TILE + c;
-      if (gj >= n_valid) break;
-      double mij = acol[(long long)c * lda];
+    const int cend = min((ti == tj) ? r + 1 : TILE, n_valid - tj * TILE);
+    // columns c = (tid >> 7) + 2u, four loads in flight ahead of the arithmetic
+    for (int c0 = (tid >> 7); c0 < cend; c0 += 8) {
+      double mv[4];
 #pragma unroll
-      for (int k = 0; k < QMAX; ++k)
-        if (k < q1) mij = fma(-wi[k], ws[c * QMAX + k], mij);
-      if (gj == gi) {
-        accT += mij;
-      } else {
-        double df2[DMAX];
-        double s = 0.0;
+      for (int u = 0; u < 4; ++u) {
+        const int c = c0 + 2 * u;
+        mv[u] = (c < cend) ? acol[(long long)c * lda] : 0.0;
+      }
 #pragma unroll
-        for (int k = 0; k < DMAX; ++k) {
-          if (k < d) {
-            double df = xi[k] - xs[c * DMAX + k];
-            df2[k] = df * df;
-            s += df2[k];
-          } else {
-            df2[k] = 0.0;
+      for (int u = 0; u < 4; ++u) {
+        const int c = c0 + 2 * u;
+        if (c >= cend) break;
+        const int gj = tj * TILE + c;
+        double mij = mv[u];
+#pragma unroll
+        for (int k = 0; k < QMAX; ++k)
+          if (k < q1) mij = fma(-wi[k], ws[c * QMAX + k], mij);
+        if (gj == gi) {
+          accT += mij;
+        } else {
+          double df2[DMAX];
+          double s = 0.0;
+#pragma unroll
+          for (int k = 0; k < DMAX; ++k) {
+            if (k < d) {
+              double df = xi[k] - xs[c * DMAX + k];
+              df2[k] = df * df;
+              s += df2[k];
+            } else {
+              df2[k] = 0.0;
+            }
           }
-        }
-        const double me = mij * exp(-s);
-        accE += me;
+          const double me = mij * exp(-s);
+          accE += me;
 #pragma unroll
-        for (int k = 0; k < DMAX; ++k)
-          if (k < d) acc[k] = fma(me, df2[k], acc[k]);
+          for (int k = 0; k < DMAX; ++k)
+            if (k < d) acc[k] = fma(me, df2[k], acc[k]);
+        }
       }
     }
   }
