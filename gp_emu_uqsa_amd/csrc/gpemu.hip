@@ -1609,7 +1609,8 @@ int gpe_bench_gemm(gpe_ctx* c, int32_t trans_a, int32_t trans_b, int32_t mt, int
     fill(da, (size_t)M * K);
     fill(db, (size_t)K * N);
     fill(dc, (size_t)M * N);
-    const long long lda = trans_a ? K : M, ldb = trans_b ? K : N;
+    long long lda = trans_a ? K : M, ldb = trans_b ? K : N;
+    if (std::getenv("GPEMU_BENCH_HOT")) lda = ldb = 0;   // diagnostic: cache-resident operands
     GemmProb p = mkprob(da, lda, db, ldb, dc, M, mt, nt, K, lower ? G_CLOWER : 0, -1.0, beta);
     p.tile_begin = 0;
     p.ntiles = prob_tiles(p);

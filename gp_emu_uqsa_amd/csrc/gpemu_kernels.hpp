@@ -548,6 +548,21 @@ __device__ inline int mfma64_row(int lane, int r) { return (lane >> 4) + 4 * r; 
 // K-stage staging of the grouped GEMM: each of the 256 threads moves four 16-byte
 // pieces of the A tile (128 x 16) and four of the B tile into registers, then
 // into the [k][m] LDS image (pitch GP).
+// operands live in global memory: address space 1 gives global_load (vmcnt only)
+// instead of flat_load, whose lgkmcnt share would make every LDS-fragment wait
+// also wait for the next stage's HBM loads
+typedef double gvec2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double2 gld2(const double* p) {
+  const gvec2 v = *(__attribute__((address_space(1))) const gvec2*)(p);
+  return make_double2(v.x, v.y);
+}
+__device__ __forceinline__ double gld1(const double* p) {
+  return *(__attribute__((address_space(1))) const double*)(p);
+}
+__device__ __forceinline__ void gst1(double* p, double v) {
+  *(__attribute__((address_space(1))) double*)(p) = v;
+}
+
 template <bool AK, bool BK>
 __device__ __forceinline__ void gemm_gload(const double* __restrict__ Ab,
                                            const double* __restrict__ Bb, long long lda,
@@ -559,17 +574,17 @@ __device__ __forceinline__ void gemm_gload(const double* __restrict__ Ab,
     double2 va, vb;
     if (!AK) {
       const int kk = c >> 6, mm = (c & 63) * 2;
-      va = *reinterpret_cast<const double2*>(Ab + mm + (long long)(k0 + kk) * lda);
+      va = gld2(Ab + mm + (long long)(k0 + kk) * lda);
     } else {
       const int mm = c >> 3, kk = (c & 7) * 2;
-      va = *reinterpret_cast<const double2*>(Ab + (long long)mm * lda + k0 + kk);
+      va = gld2(Ab + (long long)mm * lda + k0 + kk);
     }
     if (!BK) {
       const int kk = c >> 6, nn = (c & 63) * 2;
-      vb = *reinterpret_cast<const double2*>(Bb + nn + (long long)(k0 + kk) * ldb);
+      vb = gld2(Bb + nn + (long long)(k0 + kk) * ldb);
     } else {
       const int nn = c >> 3, kk = (c & 7) * 2;
-      vb = *reinterpret_cast<const double2*>(Bb + (long long)nn * ldb + k0 + kk);
+      vb = gld2(Bb + (long long)nn * ldb + k0 + kk);
     }
     ra[2 * s] = va.x;
     ra[2 * s + 1] = va.y;
@@ -612,7 +627,36 @@ __device__ __forceinline__ void tile_unpack(unsigned v, int& p, int& ti, int& tj
   tj = (int)(v & 0xfffu);
 }
 
-// K loop of one 128x128 output tile: acc += opA(Ab) opB(Bb) over nk stages of GK
+// fragments of k-step ks (4 deep) from the LDS stage at As/Bs
+template <bool AK, bool BK>
+__device__ __forceinline__ void gemm_frags(const double* As, const double* Bs, int ks, int lane, int wm,
+                                           int wn, double (&af)[4], double (&bf)[4]) {
+  const int krow = ks * 4 + (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = wm + i * 16 + (lane & 15);
+    af[i] = AK ? As[m * GQ + krow] : As[krow * GP + m];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = wn + j * 16 + (lane & 15);
+    bf[j] = BK ? Bs[n * GQ + krow] : Bs[krow * GP + n];
+  }
+}
+
+// MFMAs u0 <= u < u1 of one k-step (u = 4 i + j); operands swapped: D = (A B)^T
+template <int U0, int U1>
+__device__ __forceinline__ void gemm_mfmas(d4 (&acc)[4][4], const double (&af)[4], const double (&bf)[4]) {
+#pragma unroll
+  for (int u = U0; u < U1; ++u)
+    acc[u >> 2][u & 3] = __builtin_amdgcn_mfma_f64_16x16x4f64(bf[u & 3], af[u >> 2], acc[u >> 2][u & 3], 0, 0, 0);
+}
+
+// K loop of one 128x128 output tile: acc += opA(Ab) opB(Bb) over nk stages of GK.
+// Software pipeline: the fragments of the next k-step are read while the 16 MFMAs
+// of the current one issue; at a stage boundary the last 4 MFMAs are held back
+// until the next stage's first fragments are in flight (sched_barrier keeps the
+// compiler from regrouping).
 template <bool AK, bool BK>
 __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
                                            long long lda, long long ldb, int kbeg, int nk, double* lds,
@@ -620,36 +664,38 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   double ra[8], rb[8];
+  double fa0[4], fb0[4], fa1[4], fb1[4];
   gemm_gload<AK, BK>(Ab, Bb, lda, ldb, kbeg, tid, ra, rb);
   gemm_sstore<AK, BK>(lds, 0, tid, ra, rb);
   __syncthreads();
+  gemm_frags<AK, BK>(lds, lds + G_OPND, 0, lane, wm, wn, fa0, fb0);
   for (int s = 0; s < nk; ++s) {
-    if (s + 1 < nk) gemm_gload<AK, BK>(Ab, Bb, lda, ldb, kbeg + (s + 1) * GK, tid, ra, rb);
+    const bool more = s + 1 < nk;
+    if (more) gemm_gload<AK, BK>(Ab, Bb, lda, ldb, kbeg + (s + 1) * GK, tid, ra, rb);
     const double* As = lds + (s & 1) * (2 * G_OPND);
     const double* Bs = As + G_OPND;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int krow = ks * 4 + (lane >> 4);
-      double af[4], bf[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = wm + i * 16 + (lane & 15);
-        af[i] = AK ? As[m * GQ + krow] : As[krow * GP + m];
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = wn + j * 16 + (lane & 15);
-        bf[j] = BK ? Bs[n * GQ + krow] : Bs[krow * GP + n];
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(bf[j], af[i], acc[i][j], 0, 0, 0);
+    gemm_frags<AK, BK>(As, Bs, 1, lane, wm, wn, fa1, fb1);
+    gemm_mfmas<0, 16>(acc, fa0, fb0);
+    __builtin_amdgcn_sched_barrier(0);
+    gemm_frags<AK, BK>(As, Bs, 2, lane, wm, wn, fa0, fb0);
+    gemm_mfmas<0, 16>(acc, fa1, fb1);
+    __builtin_amdgcn_sched_barrier(0);
+    gemm_frags<AK, BK>(As, Bs, 3, lane, wm, wn, fa1, fb1);
+    gemm_mfmas<0, 16>(acc, fa0, fb0);
+    __builtin_amdgcn_sched_barrier(0);
+    gemm_mfmas<0, 12>(acc, fa1, fb1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) {
+      gemm_sstore<AK, BK>(lds, (s + 1) & 1, tid, ra, rb);
+      __syncthreads();
+      const double* An = lds + ((s + 1) & 1) * (2 * G_OPND);
+      gemm_frags<AK, BK>(An, An + G_OPND, 0, lane, wm, wn, fa0, fb0);
     }
-    if (s + 1 < nk) gemm_sstore<AK, BK>(lds, (s + 1) & 1, tid, ra, rb);
-    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+    gemm_mfmas<12, 16>(acc, fa1, fb1);
+    __builtin_amdgcn_sched_barrier(0);
   }
+  __syncthreads();   // callers reuse the staging LDS
 }
 
 __device__ __forceinline__ void gemm_store(double* Cb, long long ldc, double alpha, const d4 (&acc)[4][4]) {
@@ -663,7 +709,7 @@ __device__ __forceinline__ void gemm_store(double* Cb, long long ldc, double alp
       for (int r = 0; r < 4; ++r) {
         const int m = wm + i * 16 + (lane & 15);
         const int n = wn + j * 16 + mfma64_row(lane, r);
-        Cb[m + (long long)n * ldc] = alpha * acc[i][j][r];
+        gst1(Cb + m + (long long)n * ldc, alpha * acc[i][j][r]);
       }
 }
 
@@ -737,7 +783,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restrict__ pr
         for (int r = 0; r < 4; ++r) {
           const int m = wm + i * 16 + (lane & 15);
           const int n = wn + j * 16 + mfma64_row(lane, r);
-          acc[i][j][r] = sc * Cb[m + (long long)n * P.ldc];
+          acc[i][j][r] = sc * gld1(Cb + m + (long long)n * P.ldc);
         }
   } else {
 #pragma unroll
