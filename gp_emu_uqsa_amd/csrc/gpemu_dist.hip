@@ -1,0 +1,688 @@
+// gpemu_dist.hip -- row-block distributed value objective over RCCL (include/gpemu_dist.h).
+//
+// Partition: 128-row tile rows dealt cyclically, tile row t on rank t mod P (the
+// trailing matrix shrinks evenly on every rank); rank r stores its tile rows of
+// the lower triangle in one column-major buffer (local tile row li <-> global
+// t = li P + r).  Tile row NB (below the n_pad x n_pad matrix) holds [f H]^T: the
+// sweep turns it into (L^-1 [f H])^T and its diagonal tile into -Gram.
+//
+// Step k (k = 0 .. NB-1), every rank, one HIP stream:
+//   owner(k): A(k,k) -> L_kk (in place), Dinv = L_kk^-1   (k_gemm G_DIAG, 1 workgroup)
+//   RCCL broadcast of Dinv from owner(k)                    (128 KB)
+//   panel:   L(i,k) = A(i,k) Dinv^T for its rows i > k      (k_gemm)
+//   pack its panel tiles, RCCL all-gather, unpermute into the panel column
+//   update:  A(i,j) -= L(i,k) L(j,k)^T, its rows i > k, k < j <= i (k_gemm, tile list)
+// Loopback transport: all P ranks in this process on one GPU (separate local
+// buffers, one shared Dinv and panel column), copies instead of RCCL.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gpemu.h"
+#include "../../include/gpemu_dist.h"
+#include "gpemu_kernels.hpp"
+#include "gpemu_small.hpp"
+
+using namespace gpe;
+
+namespace {
+
+struct DistPairArgs {
+  const double* xw;   // scaled points, n_pad x d row-major (zero rows >= n)
+  const double* F;    // [f H], n_pad x Pc column-major (zero rows >= n)
+  const double* r;    // nugget vector or null
+  double* out;        // local tile rows, column-major
+  long long ld, ldF;
+  int d, n_valid, NB, nranks, rank, nloc, Pc;
+  double s2, coff, cdiag, rscale;
+};
+
+// K-build of one rank's tile rows: tile (li, tj), tj <= t = li P + rank; the
+// training matrix s2 coff exp(-|x_i - x_j|^2), diagonal s2 cdiag + rscale r_i,
+// identity on padded rows; tile row NB = [f H]^T (zero beyond Pc rows, (NB,NB) = 0).
+template <int DMAX>
+__global__ void __launch_bounds__(256) k_dist_kbuild(DistPairArgs a) {
+  __shared__ double xs_col[TILE * DMAX];
+  const int li = blockIdx.x % a.nloc, tj = blockIdx.x / a.nloc;
+  const int gt = li * a.nranks + a.rank;
+  if (tj > gt) return;
+  const int tid = threadIdx.x, r = tid & (TILE - 1);
+  double* out = a.out + (long long)li * TILE + (long long)tj * TILE * a.ld;
+  if (gt == a.NB) {
+    for (int c = tid >> 7; c < TILE; c += 2) {
+      const int gj = tj * TILE + c;
+      const double v = (tj < a.NB && r < a.Pc) ? a.F[gj + (long long)r * a.ldF] : 0.0;
+      out[r + (long long)c * a.ld] = v;
+    }
+    return;
+  }
+  const int d = a.d;
+  for (int e = tid; e < TILE * d; e += 256) {
+    const int c = e / d, k = e - c * d;
+    xs_col[e] = a.xw[(long long)(tj * TILE + c) * d + k];
+  }
+  const int gi = gt * TILE + r;
+  double xi[DMAX];
+#pragma unroll
+  for (int k = 0; k < DMAX; ++k) xi[k] = (k < d) ? a.xw[(long long)gi * d + k] : 0.0;
+  __syncthreads();
+  const double pre = a.s2 * a.coff;
+  for (int c = tid >> 7; c < TILE; c += 2) {
+    const int gj = tj * TILE + c;
+    double v;
+    if (gi >= a.n_valid || gj >= a.n_valid) {
+      v = (gi == gj) ? 1.0 : 0.0;
+    } else if (gi == gj) {
+      v = a.s2 * a.cdiag + (a.r ? a.rscale * a.r[gi] : 0.0);
+    } else {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < DMAX; ++k) {
+        if (k < d) {
+          const double df = xi[k] - xs_col[c * d + k];
+          s = fma(df, df, s);
+        }
+      }
+      v = pre * exp(-s);
+    }
+    out[r + (long long)c * a.ld] = v;
+  }
+}
+
+// panel tiles (local rows li0 .. li0+cnt-1, column k) -> dst, 128x128 column-major each
+__global__ void __launch_bounds__(256) k_dist_pack(const double* Aloc, long long ld, int li0, int k,
+                                                   double* dst) {
+  const int t = blockIdx.x;
+  const double* src = Aloc + (long long)(li0 + t) * TILE + (long long)k * TILE * ld;
+  double* o = dst + (long long)t * TILE * TILE;
+  for (int e = threadIdx.x; e < TILE * TILE / 2; e += 256) {
+    const int i = (e & 63) * 2, c = e >> 6;
+    *reinterpret_cast<double2*>(o + i + c * TILE) =
+        *reinterpret_cast<const double2*>(src + i + (long long)c * ld);
+  }
+}
+
+// gathered segment of rank r (blockIdx.y), tile t -> panel rows of global tile (li0_r + t) P + r
+__global__ void __launch_bounds__(256) k_dist_unpermute(const double* recv, long long seg,
+                                                        const int* li0, const int* cnt, int P,
+                                                        double* panel, long long ldp) {
+  const int r = blockIdx.y, t = blockIdx.x;
+  if (t >= cnt[r]) return;
+  const int gt = (li0[r] + t) * P + r;
+  const double* src = recv + (long long)r * seg + (long long)t * TILE * TILE;
+  double* o = panel + (long long)gt * TILE;
+  for (int e = threadIdx.x; e < TILE * TILE / 2; e += 256) {
+    const int i = (e & 63) * 2, c = e >> 6;
+    *reinterpret_cast<double2*>(o + i + (long long)c * ldp) =
+        *reinterpret_cast<const double2*>(src + i + c * TILE);
+  }
+}
+
+// loopback: panel tiles of one logical rank straight into the panel column
+__global__ void __launch_bounds__(256) k_dist_to_panel(const double* Aloc, long long ld, int li0, int k,
+                                                       int P, int rank, double* panel, long long ldp) {
+  const int t = blockIdx.x;
+  const int gt = (li0 + t) * P + rank;
+  const double* src = Aloc + (long long)(li0 + t) * TILE + (long long)k * TILE * ld;
+  double* o = panel + (long long)gt * TILE;
+  for (int e = threadIdx.x; e < TILE * TILE / 2; e += 256) {
+    const int i = (e & 63) * 2, c = e >> 6;
+    *reinterpret_cast<double2*>(o + i + (long long)c * ldp) =
+        *reinterpret_cast<const double2*>(src + i + (long long)c * ld);
+  }
+}
+
+struct Rank {              // one rank's stored tile rows
+  int rank = 0, nloc = 0;
+  long long ld = 0;
+  double* A = nullptr;     // nloc*128 x (NB+1)*128, column-major
+  double* logdet = nullptr;
+};
+
+struct DLaunch {           // one grouped k_gemm launch
+  int first = 0, count = 0, tiles = 0;
+  long long list = -1;
+};
+
+constexpr int DIST_DESC_MAX = 1 << 20;
+
+int nloc_of(int NB, int P, int r) { return r <= NB ? (NB - r) / P + 1 : 0; }
+// first local row of rank r whose global tile row exceeds k
+int li0_of(int k, int P, int r) { return k < r ? 0 : (k - r) / P + 1; }
+
+}  // namespace
+
+struct gpe_dist {
+  int device = 0, P = 1, rank = 0;
+  bool loop = true;
+  ncclComm_t comm = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+
+  long long n = 0, n_pad = 0;
+  int d = 0, q = 0, NB = 0;
+  bool has_r = false;
+  double* dX = nullptr;    // n_pad x d raw
+  double* dXw = nullptr;   // scaled
+  double* dF = nullptr;    // n_pad x (q+1)
+  double* dr = nullptr;
+  double* dinvdelta = nullptr;
+  std::vector<Rank> ranks;   // local ranks (all P in loopback, one otherwise)
+
+  double* dinv = nullptr;    // 128 x 128
+  double* panel = nullptr;   // (NB+1)*128 x 128
+  double* recv = nullptr;    // RCCL all-gather buffer
+  double* gram = nullptr;    // Pc x Pc
+  int* dinfo = nullptr;
+  int* dli0 = nullptr;       // [NB][P] first local row with global row > k
+  int* dcnt = nullptr;       // [NB][P] panel tiles of rank r at step k
+  GemmProb* dprobs = nullptr;
+  unsigned* dtiles = nullptr;
+  std::vector<DLaunch> diag, panel_l, upd;   // per step
+  std::vector<int> maxT;                       // per step: max panel tiles over ranks
+  double* hpin = nullptr;
+  size_t hpin_cap = 0;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  std::vector<hipEvent_t> cev;
+  double total_ms = 0.0, comm_ms = 0.0;
+};
+
+namespace {
+
+#define DCHK_HIP(h, expr)                                                          \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) {                                                        \
+      (h)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                \
+      return GPE_ERR_HIP;                                                          \
+    }                                                                              \
+  } while (0)
+
+#define DCHK_NCCL(h, expr)                                                         \
+  do {                                                                             \
+    ncclResult_t e_ = (expr);                                                      \
+    if (e_ != ncclSuccess) {                                                       \
+      (h)->err = std::string(#expr) + ": " + ncclGetErrorString(e_);               \
+      return GPE_ERR_HIP;                                                          \
+    }                                                                              \
+  } while (0)
+
+#define DCHK(expr)                   \
+  do {                               \
+    int rc_ = (expr);                \
+    if (rc_ != GPE_OK) return rc_;   \
+  } while (0)
+
+int dfail(gpe_dist* h, int code, const std::string& m) {
+  h->err = m;
+  return code;
+}
+
+template <typename T>
+int dalloc(gpe_dist* h, T** p, size_t count) {
+  if (*p) {
+    (void)hipFree(*p);
+    *p = nullptr;
+  }
+  if (count == 0) return GPE_OK;
+  if (hipMalloc((void**)p, count * sizeof(T)) != hipSuccess) {
+    *p = nullptr;
+    return dfail(h, GPE_ERR_ALLOC, "hipMalloc failed (" + std::to_string(count * sizeof(T)) + " bytes)");
+  }
+  return GPE_OK;
+}
+
+int pinned(gpe_dist* h, size_t doubles) {
+  if (doubles <= h->hpin_cap) return GPE_OK;
+  if (h->hpin) (void)hipHostFree(h->hpin);
+  h->hpin = nullptr;
+  const size_t cap = std::max<size_t>(doubles, 1 << 14);
+  DCHK_HIP(h, hipHostMalloc((void**)&h->hpin, cap * sizeof(double), hipHostMallocDefault));
+  h->hpin_cap = cap;
+  return GPE_OK;
+}
+
+GemmProb dprob(const double* A, long long lda, const double* B, long long ldb, double* C, long long ldc,
+               int mt, int nt, int K, int flags, double alpha, double beta) {
+  GemmProb p;
+  std::memset(&p, 0, sizeof(p));
+  p.A = A; p.B = B; p.C = C;
+  p.lda = lda; p.ldb = ldb; p.ldc = ldc;
+  p.mt = mt; p.nt = nt; p.K = K; p.flags = flags;
+  p.alpha = alpha; p.beta = beta;
+  return p;
+}
+
+// every per-step GEMM descriptor and tile list, for the current n and partition
+int build_schedule(gpe_dist* h) {
+  const int NB = h->NB, P = h->P;
+  const long long ldp = (long long)(NB + 1) * TILE;
+  std::vector<GemmProb> probs;
+  std::vector<unsigned> tiles;
+  h->diag.assign(NB, DLaunch());
+  h->panel_l.assign(NB, DLaunch());
+  h->upd.assign(NB, DLaunch());
+  h->maxT.assign(NB, 0);
+  std::vector<int> li0((size_t)NB * P), cnt((size_t)NB * P);
+  for (int k = 0; k < NB; ++k) {
+    for (int r = 0; r < P; ++r) {
+      li0[(size_t)k * P + r] = li0_of(k, P, r);
+      cnt[(size_t)k * P + r] = std::max(0, nloc_of(NB, P, r) - li0_of(k, P, r));
+      h->maxT[k] = std::max(h->maxT[k], cnt[(size_t)k * P + r]);
+    }
+    // diagonal tile: owner's local row k / P, column k
+    const int owner = k % P;
+    for (Rank& R : h->ranks) {
+      if (R.rank != owner) continue;
+      double* Ckk = R.A + (long long)(k / P) * TILE + (long long)k * TILE * R.ld;
+      GemmProb p = dprob(nullptr, R.ld, nullptr, R.ld, Ckk, R.ld, 1, 1, 0, G_DIAG, 1.0, 1.0);
+      p.X = h->dinv;
+      p.ldx = TILE;
+      p.logdet = R.logdet + k;
+      p.diag_col0 = k * TILE;
+      p.ntiles = 1;
+      h->diag[k] = {(int)probs.size(), 1, 1, -1};
+      probs.push_back(p);
+    }
+    // panel: L(i,k) = A(i,k) Dinv^T over each local rank's rows i > k
+    DLaunch pl;
+    pl.first = (int)probs.size();
+    for (Rank& R : h->ranks) {
+      const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
+      if (c == 0) continue;
+      double* Aik = R.A + (long long)a * TILE + (long long)k * TILE * R.ld;
+      GemmProb p = dprob(Aik, R.ld, h->dinv, TILE, Aik, R.ld, c, 1, TILE, 0, 1.0, 0.0);
+      p.tile_begin = pl.tiles;
+      p.ntiles = c;
+      pl.tiles += c;
+      probs.push_back(p);
+      ++pl.count;
+    }
+    h->panel_l[k] = pl;
+    // trailing update of each local rank's rows i > k, columns k < j <= i
+    DLaunch ul;
+    ul.first = (int)probs.size();
+    ul.list = (long long)tiles.size();
+    int pi = 0;
+    for (Rank& R : h->ranks) {
+      const int a = li0_of(k, P, R.rank);
+      if (a >= R.nloc) continue;
+      GemmProb p = dprob(R.A + (long long)k * TILE * R.ld, R.ld, h->panel, ldp, R.A, R.ld,
+                         R.nloc, NB + 1, TILE, 0, -1.0, 1.0);
+      for (int li = a; li < R.nloc; ++li) {
+        const int gt = li * P + R.rank;
+        for (int j = k + 1; j <= gt; ++j) tiles.push_back(((unsigned)pi << 24) | ((unsigned)li << 12) | (unsigned)j);
+      }
+      probs.push_back(p);
+      ++pi;
+      ++ul.count;
+    }
+    ul.tiles = (int)(tiles.size() - ul.list);
+    if (ul.tiles == 0) ul.count = 0;
+    h->upd[k] = ul;
+  }
+  if ((int)probs.size() > DIST_DESC_MAX) return dfail(h, GPE_ERR_UNSUPPORTED, "distributed schedule too large");
+  DCHK(dalloc(h, &h->dprobs, probs.size()));
+  DCHK_HIP(h, hipMemcpy(h->dprobs, probs.data(), probs.size() * sizeof(GemmProb), hipMemcpyHostToDevice));
+  DCHK(dalloc(h, &h->dtiles, std::max<size_t>(tiles.size(), 1)));
+  if (!tiles.empty())
+    DCHK_HIP(h, hipMemcpy(h->dtiles, tiles.data(), tiles.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+  DCHK(dalloc(h, &h->dli0, li0.size()));
+  DCHK(dalloc(h, &h->dcnt, cnt.size()));
+  DCHK_HIP(h, hipMemcpy(h->dli0, li0.data(), li0.size() * sizeof(int), hipMemcpyHostToDevice));
+  DCHK_HIP(h, hipMemcpy(h->dcnt, cnt.data(), cnt.size() * sizeof(int), hipMemcpyHostToDevice));
+  return GPE_OK;
+}
+
+int launch(gpe_dist* h, const DLaunch& L) {
+  if (L.count == 0 || L.tiles == 0) return GPE_OK;
+  const size_t lds = G_LDS_LAUNCH_DOUBLES * sizeof(double);
+  const unsigned* tl = L.list >= 0 ? h->dtiles + L.list : nullptr;
+  hipLaunchKernelGGL((k_gemm<false, false>), dim3(L.tiles), dim3(256), lds, h->stream, h->dprobs + L.first,
+                     L.count, tl, h->dinfo);
+  DCHK_HIP(h, hipGetLastError());
+  return GPE_OK;
+}
+
+int kbuild(gpe_dist* h, int kernel, double nu, double s2, double rscale) {
+  double coff, cdiag;
+  if (kernel == GPE_KERNEL_ALT_NUG) {
+    coff = 1.0;
+    cdiag = 1.0 + nu * nu;
+  } else {
+    coff = 1.0 - nu;
+    cdiag = 1.0;
+  }
+  for (Rank& R : h->ranks) {
+    if (R.nloc == 0) continue;   // more ranks than tile rows
+    DistPairArgs a;
+    a.xw = h->dXw; a.F = h->dF; a.r = (h->has_r && rscale != 0.0) ? h->dr : nullptr; a.out = R.A;
+    a.ld = R.ld; a.ldF = h->n_pad; a.d = h->d; a.n_valid = (int)h->n; a.NB = h->NB; a.nranks = h->P;
+    a.rank = R.rank; a.nloc = R.nloc; a.Pc = h->q + 1;
+    a.s2 = s2; a.coff = coff; a.cdiag = cdiag; a.rscale = rscale;
+    const dim3 grid((unsigned)(R.nloc * (h->NB + 1)));
+    if (h->d <= 4) hipLaunchKernelGGL(k_dist_kbuild<4>, grid, dim3(256), 0, h->stream, a);
+    else if (h->d <= 8) hipLaunchKernelGGL(k_dist_kbuild<8>, grid, dim3(256), 0, h->stream, a);
+    else if (h->d <= 16) hipLaunchKernelGGL(k_dist_kbuild<16>, grid, dim3(256), 0, h->stream, a);
+    else hipLaunchKernelGGL(k_dist_kbuild<32>, grid, dim3(256), 0, h->stream, a);
+    DCHK_HIP(h, hipGetLastError());
+  }
+  return GPE_OK;
+}
+
+// one column step: diag, Dinv broadcast, panel, panel all-gather, trailing update
+int step(gpe_dist* h, int k, int& ev) {
+  const int P = h->P, owner = k % P;
+  DCHK(launch(h, h->diag[k]));
+  if (!h->loop) {
+    DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
+    DCHK_NCCL(h, ncclBroadcast(h->dinv, h->dinv, (size_t)TILE * TILE, ncclDouble, owner, h->comm, h->stream));
+    DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
+  }
+  DCHK(launch(h, h->panel_l[k]));
+  const long long ldp = (long long)(h->NB + 1) * TILE;
+  if (h->loop) {
+    if (h->cev.size() > (size_t)ev + 1) DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
+    for (Rank& R : h->ranks) {
+      const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
+      if (c == 0) continue;
+      hipLaunchKernelGGL(k_dist_to_panel, dim3(c), dim3(256), 0, h->stream, R.A, R.ld, a, k, P, R.rank,
+                         h->panel, ldp);
+      DCHK_HIP(h, hipGetLastError());
+    }
+    if (h->cev.size() > (size_t)ev) DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
+  } else {
+    const Rank& R = h->ranks[0];
+    const int T = h->maxT[k];
+    const long long seg = (long long)T * TILE * TILE;
+    if (T > 0) {
+      const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
+      if (c > 0) {
+        hipLaunchKernelGGL(k_dist_pack, dim3(c), dim3(256), 0, h->stream, R.A, R.ld, a, k,
+                           h->recv + (long long)h->rank * seg);
+        DCHK_HIP(h, hipGetLastError());
+      }
+      DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
+      DCHK_NCCL(h, ncclAllGather(h->recv + (long long)h->rank * seg, h->recv, (size_t)seg, ncclDouble, h->comm,
+                                 h->stream));
+      DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
+      hipLaunchKernelGGL(k_dist_unpermute, dim3(T, P), dim3(256), 0, h->stream, h->recv, seg,
+                         h->dli0 + (size_t)k * P, h->dcnt + (size_t)k * P, P, h->panel, ldp);
+      DCHK_HIP(h, hipGetLastError());
+    }
+  }
+  DCHK(launch(h, h->upd[k]));
+  return GPE_OK;
+}
+
+int ensure_events(gpe_dist* h, size_t n) {
+  while (h->cev.size() < n) {
+    hipEvent_t e;
+    DCHK_HIP(h, hipEventCreate(&e));
+    h->cev.push_back(e);
+  }
+  return GPE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gpe_dist_unique_id(uint8_t* out, int32_t len) {
+  if (!out || len < (int32_t)sizeof(ncclUniqueId)) return GPE_ERR_ARG;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return GPE_ERR_HIP;
+  std::memcpy(out, &id, sizeof(id));
+  return GPE_OK;
+}
+
+int32_t gpe_dist_owner(int32_t nranks, int32_t tile_row) {
+  if (nranks <= 0 || tile_row < 0) return -1;
+  return tile_row % nranks;
+}
+
+int32_t gpe_dist_local_rows(int64_t n, int32_t nranks, int32_t rank) {
+  if (n <= 0 || nranks <= 0 || rank < 0 || rank >= nranks) return -1;
+  const int NB = (int)((n + TILE - 1) / TILE);
+  return nloc_of(NB, nranks, rank);
+}
+
+gpe_dist* gpe_dist_create(int32_t device, int32_t nranks, int32_t rank, const uint8_t* unique_id) {
+  if (nranks <= 0 || nranks > 256 || (unique_id && (rank < 0 || rank >= nranks))) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  gpe_dist* h = new gpe_dist();
+  h->device = device;
+  h->P = nranks;
+  h->rank = unique_id ? rank : 0;
+  h->loop = unique_id == nullptr;
+  bool ok = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreate(&h->e0) == hipSuccess && hipEventCreate(&h->e1) == hipSuccess &&
+            hipMalloc((void**)&h->dinfo, sizeof(int)) == hipSuccess &&
+            hipMalloc((void**)&h->dinv, (size_t)TILE * TILE * sizeof(double)) == hipSuccess;
+  if (ok && !h->loop) {
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, sizeof(id));
+    ok = ncclCommInitRank(&h->comm, nranks, id, rank) == ncclSuccess;
+  }
+  if (!ok) {
+    gpe_dist_destroy(h);
+    return nullptr;
+  }
+  return h;
+}
+
+void gpe_dist_destroy(gpe_dist* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->comm) (void)ncclCommDestroy(h->comm);
+  for (Rank& R : h->ranks) {
+    if (R.A) (void)hipFree(R.A);
+    if (R.logdet) (void)hipFree(R.logdet);
+  }
+  double* bufs[] = {h->dX, h->dXw, h->dF, h->dr, h->dinvdelta, h->dinv, h->panel, h->recv, h->gram};
+  for (double* b : bufs)
+    if (b) (void)hipFree(b);
+  if (h->dinfo) (void)hipFree(h->dinfo);
+  if (h->dli0) (void)hipFree(h->dli0);
+  if (h->dcnt) (void)hipFree(h->dcnt);
+  if (h->dprobs) (void)hipFree(h->dprobs);
+  if (h->dtiles) (void)hipFree(h->dtiles);
+  if (h->hpin) (void)hipHostFree(h->hpin);
+  for (hipEvent_t e : h->cev) (void)hipEventDestroy(e);
+  if (h->e0) (void)hipEventDestroy(h->e0);
+  if (h->e1) (void)hipEventDestroy(h->e1);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+const char* gpe_dist_last_error(gpe_dist* h) { return h ? h->err.c_str() : "null handle"; }
+
+int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double* X, const double* f,
+                      const double* H, const double* r) {
+  if (!h) return GPE_ERR_ARG;
+  if (n <= 0 || d <= 0 || d > 32 || q < 0 || q + 1 > 128 || !X || !f || (q > 0 && !H))
+    return dfail(h, GPE_ERR_ARG, "bad shapes");
+  DCHK_HIP(h, hipSetDevice(h->device));
+  h->n = n;
+  h->d = d;
+  h->q = q;
+  h->NB = (int)((n + TILE - 1) / TILE);
+  h->n_pad = (long long)h->NB * TILE;
+  if (h->NB + 1 > 4095) return dfail(h, GPE_ERR_UNSUPPORTED, "n too large for the tile list");
+  const long long np = h->n_pad;
+  const int Pc = q + 1;
+  DCHK(pinned(h, (size_t)np * std::max(d, Pc) + 16));
+  // X (row-major, zero padded)
+  DCHK(dalloc(h, &h->dX, (size_t)np * d));
+  DCHK(dalloc(h, &h->dXw, (size_t)np * d));
+  std::memset(h->hpin, 0, (size_t)np * d * sizeof(double));
+  std::memcpy(h->hpin, X, (size_t)n * d * sizeof(double));
+  DCHK_HIP(h, hipMemcpy(h->dX, h->hpin, (size_t)np * d * sizeof(double), hipMemcpyHostToDevice));
+  // [f H] column-major, zero padded
+  DCHK(dalloc(h, &h->dF, (size_t)np * Pc));
+  std::memset(h->hpin, 0, (size_t)np * Pc * sizeof(double));
+  for (long long i = 0; i < n; ++i) {
+    h->hpin[i] = f[i];
+    for (int k = 0; k < q; ++k) h->hpin[i + (long long)(k + 1) * np] = H[i * q + k];
+  }
+  DCHK_HIP(h, hipMemcpy(h->dF, h->hpin, (size_t)np * Pc * sizeof(double), hipMemcpyHostToDevice));
+  h->has_r = r != nullptr;
+  if (r) {
+    DCHK(dalloc(h, &h->dr, (size_t)np));
+    std::memset(h->hpin, 0, (size_t)np * sizeof(double));
+    std::memcpy(h->hpin, r, (size_t)n * sizeof(double));
+    DCHK_HIP(h, hipMemcpy(h->dr, h->hpin, (size_t)np * sizeof(double), hipMemcpyHostToDevice));
+  }
+  DCHK(dalloc(h, &h->dinvdelta, 32));
+  // local tile rows
+  for (Rank& R : h->ranks) {
+    if (R.A) (void)hipFree(R.A);
+    if (R.logdet) (void)hipFree(R.logdet);
+  }
+  h->ranks.clear();
+  for (int rr = 0; rr < h->P; ++rr) {
+    if (!h->loop && rr != h->rank) continue;
+    Rank R;
+    R.rank = rr;
+    R.nloc = nloc_of(h->NB, h->P, rr);
+    R.ld = (long long)std::max(R.nloc, 1) * TILE;
+    h->ranks.push_back(R);
+    Rank& B = h->ranks.back();
+    DCHK(dalloc(h, &B.A, (size_t)B.ld * (size_t)(h->NB + 1) * TILE));
+    DCHK(dalloc(h, &B.logdet, (size_t)h->NB + 1));
+  }
+  DCHK(dalloc(h, &h->panel, (size_t)(h->NB + 1) * TILE * TILE));
+  if (!h->loop) {
+    const int T0 = nloc_of(h->NB, h->P, 0);   // the most tiles any rank contributes
+    DCHK(dalloc(h, &h->recv, (size_t)h->P * T0 * TILE * TILE));
+  }
+  DCHK(dalloc(h, &h->gram, (size_t)Pc * Pc));
+  DCHK(build_schedule(h));
+  DCHK(ensure_events(h, (size_t)4 * h->NB + 8));
+  return GPE_OK;
+}
+
+int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const double* hp, int32_t n_hp,
+                       double nu_fixed, double* llh_out, double* sigma2_out) {
+  if (!h) return GPE_ERR_ARG;
+  if (h->n <= 0) return dfail(h, GPE_ERR_STATE, "gpe_dist_set_data has not been called");
+  if (!hp || !llh_out) return dfail(h, GPE_ERR_ARG, "null argument");
+  if (variant != GPE_GP4ML && variant != GPE_MUCM) return dfail(h, GPE_ERR_ARG, "bad variant");
+  if (kernel != GPE_KERNEL_STD && kernel != GPE_KERNEL_ALT_NUG) return dfail(h, GPE_ERR_ARG, "bad kernel");
+  DCHK_HIP(h, hipSetDevice(h->device));
+  const int d = h->d, q = h->q, Pc = q + 1, P = h->P, NB = h->NB;
+  const bool gp4ml = variant == GPE_GP4ML;
+  const int base = gp4ml ? d + 1 : d;
+  if (n_hp != base && n_hp != base + 1) return dfail(h, GPE_ERR_ARG, "n_hp inconsistent with d");
+  const bool fitnug = n_hp == base + 1;
+  const double nu = fitnug ? hp[d] : nu_fixed;
+  const double sigma = gp4ml ? hp[n_hp - 1] : 1.0;
+  const double s2 = gp4ml ? sigma * sigma : 1.0;
+  const double rscale = (gp4ml && kernel == GPE_KERNEL_ALT_NUG) ? 1.0 : 0.0;
+
+  DCHK(pinned(h, (size_t)(NB + 1) * 2 + (size_t)Pc * Pc + 64));
+  for (int k = 0; k < d; ++k) {
+    if (!(hp[k] > 0.0) && !(hp[k] < 0.0)) return dfail(h, GPE_ERR_ARG, "delta must be non-zero");
+    h->hpin[k] = 1.0 / hp[k];
+  }
+  DCHK_HIP(h, hipEventRecord(h->e0, h->stream));
+  DCHK_HIP(h, hipMemcpyAsync(h->dinvdelta, h->hpin, d * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  DCHK_HIP(h, hipMemsetAsync(h->dinfo, 0, sizeof(int), h->stream));
+  const long long tot = h->n_pad * d;
+  hipLaunchKernelGGL(k_scale_points, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, h->dX,
+                     h->dinvdelta, d, (int)h->n, (int)h->n_pad, h->dXw);
+  DCHK_HIP(h, hipGetLastError());
+  for (Rank& R : h->ranks)
+    DCHK_HIP(h, hipMemsetAsync(R.logdet, 0, (size_t)(NB + 1) * sizeof(double), h->stream));
+  DCHK(kbuild(h, kernel, nu, s2, rscale));
+  int ev = 0;
+  for (int k = 0; k < NB; ++k) DCHK(step(h, k, ev));
+
+  // Gram of L^-1 [f H] = -(tile (NB, NB)), from the owner of tile row NB
+  const int ra = NB % P;
+  for (Rank& R : h->ranks) {
+    if (R.rank != ra) continue;
+    const double* t = R.A + (long long)(NB / P) * TILE + (long long)NB * TILE * R.ld;
+    DCHK_HIP(h, hipMemcpy2DAsync(h->gram, Pc * sizeof(double), t, R.ld * sizeof(double), Pc * sizeof(double),
+                                 Pc, hipMemcpyDeviceToDevice, h->stream));
+  }
+  std::vector<double> ld_sum((size_t)NB + 1, 0.0);
+  int info = 0;
+  if (h->loop) {
+    DCHK_HIP(h, hipEventRecord(h->e1, h->stream));
+    for (Rank& R : h->ranks) {
+      DCHK_HIP(h, hipMemcpyAsync(h->hpin, R.logdet, (NB + 1) * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+      DCHK_HIP(h, hipStreamSynchronize(h->stream));
+      for (int k = 0; k <= NB; ++k)
+        if (k % P == R.rank) ld_sum[k] = h->hpin[k];
+    }
+  } else {
+    const Rank& R = h->ranks[0];
+    DCHK_NCCL(h, ncclBroadcast(h->gram, h->gram, (size_t)Pc * Pc, ncclDouble, ra, h->comm, h->stream));
+    DCHK_NCCL(h, ncclAllReduce(R.logdet, R.logdet, (size_t)NB + 1, ncclDouble, ncclSum, h->comm, h->stream));
+    DCHK_NCCL(h, ncclAllReduce(h->dinfo, h->dinfo, 1, ncclInt32, ncclMax, h->comm, h->stream));
+    DCHK_HIP(h, hipEventRecord(h->e1, h->stream));
+    DCHK_HIP(h, hipMemcpyAsync(h->hpin, R.logdet, (NB + 1) * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    DCHK_HIP(h, hipStreamSynchronize(h->stream));
+    for (int k = 0; k <= NB; ++k) ld_sum[k] = h->hpin[k];
+  }
+  DCHK_HIP(h, hipMemcpyAsync(h->hpin, h->gram, (size_t)Pc * Pc * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  DCHK_HIP(h, hipMemcpyAsync(h->hpin + Pc * Pc, h->dinfo, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  DCHK_HIP(h, hipStreamSynchronize(h->stream));
+  std::memcpy(&info, h->hpin + Pc * Pc, sizeof(int));
+  {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, h->e0, h->e1);
+    h->total_ms = ms;
+    double c = 0.0;
+    for (int i = 0; i + 1 < ev; i += 2) {
+      ms = 0.f;
+      (void)hipEventElapsedTime(&ms, h->cev[i], h->cev[i + 1]);
+      c += ms;
+    }
+    h->comm_ms = c;
+  }
+  if (info == GEMM_WAIT_TIMEOUT) return dfail(h, GPE_ERR_HIP, "internal error: flag wait timed out");
+  if (info != 0) {
+    h->err = "matrix not positive definite (pivot " + std::to_string(info) + ")";
+    return GPE_NOT_PD;
+  }
+  std::vector<double> G((size_t)Pc * Pc);
+  for (int i = 0; i < Pc; ++i)
+    for (int j = 0; j < Pc; ++j) G[(size_t)i * Pc + j] = -h->hpin[i + (size_t)j * Pc];
+  double logdetA = 0.0;
+  for (int k = 0; k < NB; ++k) logdetA += ld_sum[k];
+  logdetA *= 2.0;
+  SmallAlgebra sa = small_from_gram(G, Pc);
+  if (!sa.ok) {
+    h->err = "H^T A^-1 H not positive definite";
+    return GPE_NOT_PD;
+  }
+  const double n = (double)h->n;
+  double llh, sig2;
+  if (gp4ml) {
+    llh = 0.5 * (sa.quad + logdetA + sa.logdetQ + (n - q) * std::log(2.0 * M_PI));
+    sig2 = s2;
+  } else {
+    sig2 = sa.quad / (n - q - 2.0);
+    llh = 0.5 * ((n - q) * std::log(sig2) + logdetA + sa.logdetQ);
+  }
+  *llh_out = llh;
+  if (sigma2_out) *sigma2_out = sig2;
+  return GPE_OK;
+}
+
+int gpe_dist_times(gpe_dist* h, double* total_ms, double* comm_ms) {
+  if (!h) return GPE_ERR_ARG;
+  if (total_ms) *total_ms = h->total_ms;
+  if (comm_ms) *comm_ms = h->comm_ms;
+  return GPE_OK;
+}
+
+}  // extern "C"

@@ -54,7 +54,7 @@ __device__ inline void tri_decode(int e, int& ti, int& tj) {
 }
 
 template <int DMAX>
-__global__ void __launch_bounds__(256) k_pairs(PairArgs a) {
+static __global__ void __launch_bounds__(256) k_pairs(PairArgs a) {
   __shared__ double xs_col[TILE * DMAX];
   int ti, tj;
   if (a.mode & 1) tri_decode(blockIdx.x, ti, tj);
@@ -291,7 +291,7 @@ __device__ void dg_node(double* S, double* xd, int* fail, int tid) {
   }
 }
 
-__global__ void __launch_bounds__(DIAG_THREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_potrf_diag(double* A, long long lda, int kt,
+static __global__ void __launch_bounds__(DIAG_THREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_potrf_diag(double* A, long long lda, int kt,
                                                              double* Dinv, long long ldd,
                                                              double* logdet, int* info) {
   __shared__ double S[TILE * SP];
@@ -359,7 +359,7 @@ __global__ void __launch_bounds__(DIAG_THREADS, 1) __attribute__((amdgpu_waves_p
 // ---------------------------------------------------------------------------
 constexpr int DIAG_ROWS_THREADS = 1024;
 
-__global__ void __launch_bounds__(DIAG_ROWS_THREADS) k_potrf_diag_rows(double* A, long long lda, int kt,
+static __global__ void __launch_bounds__(DIAG_ROWS_THREADS) k_potrf_diag_rows(double* A, long long lda, int kt,
                                                              double* Dinv, long long ldd,
                                                              double* logdet, int* info) {
   __shared__ double colbuf[TILE];
@@ -739,7 +739,7 @@ __device__ __forceinline__ int gemm_wait_flag(const int* flag) {
 constexpr int GEMM_WAIT_TIMEOUT = 0x7fffffff;   // info value after a flag wait timed out
 
 template <bool AK, bool BK>
-__global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restrict__ probs, int nprob,
+static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restrict__ probs, int nprob,
                                                   const unsigned* __restrict__ tiles,
                                                   int* __restrict__ abort_flag) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -872,7 +872,7 @@ struct SkinnyArgs {
 
 // grid: blockIdx.x = it + nit * ch
 template <int PM>
-__global__ void __launch_bounds__(256) k_trmm_skinny_n(SkinnyArgs a) {
+static __global__ void __launch_bounds__(256) k_trmm_skinny_n(SkinnyArgs a) {
   __shared__ double Rs[TILE * PM];
   __shared__ double red[TILE * PM];
   if (a.abort_flag && *a.abort_flag) return;
@@ -917,7 +917,7 @@ __global__ void __launch_bounds__(256) k_trmm_skinny_n(SkinnyArgs a) {
 
 // grid: blockIdx.x = it + nit * ch ; k tiles: lower ? [it + ch*CH, ...) : [ch*CH, ...)
 template <int PM>
-__global__ void __launch_bounds__(256) k_trmm_skinny_t(SkinnyArgs a) {
+static __global__ void __launch_bounds__(256) k_trmm_skinny_t(SkinnyArgs a) {
   constexpr int KS = 64;            // k rows staged per pass
   __shared__ double Ms[TILE * (KS + 1)];   // [col i][k]
   __shared__ double Rs[KS * PM];
@@ -1025,7 +1025,7 @@ __device__ __forceinline__ void skm_sstore(double* Ms, double* Rs, int tid, cons
 }
 
 template <int PM, bool TR>
-__global__ void __launch_bounds__(256) k_skinny_mfma(SkinnyArgs a) {
+static __global__ void __launch_bounds__(256) k_skinny_mfma(SkinnyArgs a) {
   constexpr int MIMG = TR ? TILE * SKM_PT : SKM_GK * SKM_PN;
   __shared__ __attribute__((aligned(16))) double Ms[MIMG];
   __shared__ __attribute__((aligned(16))) double Rs[PM * SKM_PT];
@@ -1091,7 +1091,7 @@ __global__ void __launch_bounds__(256) k_skinny_mfma(SkinnyArgs a) {
 
 // out[i + p*ldp] = sum_{ch < nch(i)} part[ch][i + p*ldp], fixed order
 // nch(i) for the n-kernel (lower): ceil((it+1)/CH); t-kernel lower: ceil((ntr-it)/CH)
-__global__ void k_reduce_chunks(const double* part, long long pstride, double* out,
+static __global__ void k_reduce_chunks(const double* part, long long pstride, double* out,
                                 long long ldp, int P, int nrows, int ntr, int mode,
                                 const int* abort_flag) {
   if (abort_flag && *abort_flag) return;
@@ -1111,7 +1111,7 @@ __global__ void k_reduce_chunks(const double* part, long long pstride, double* o
 // ---------------------------------------------------------------------------
 // Gram: part[blk][a*P+b] = sum_{rows in blk} Z(row,a) Z(row,b); rows 256 per block
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_gram(const double* Z, long long ldz, int P, int nrows,
+static __global__ void __launch_bounds__(256) k_gram(const double* Z, long long ldz, int P, int nrows,
                                               double* part, const int* abort_flag) {
   __shared__ double zs[256 * (SK_PMAX + 1)];
   if (abort_flag && *abort_flag) return;
@@ -1132,7 +1132,7 @@ __global__ void __launch_bounds__(256) k_gram(const double* Z, long long ldz, in
 }
 
 // out[j] = sum_w part[w*len + j]; one block per j, fixed tree -> reproducible
-__global__ void __launch_bounds__(256) k_reduce_rows(const double* part, int nw, int len,
+static __global__ void __launch_bounds__(256) k_reduce_rows(const double* part, int nw, int len,
                                                      double* out) {
   __shared__ double red[256];
   const int j = blockIdx.x, tid = threadIdx.x;
@@ -1148,7 +1148,7 @@ __global__ void __launch_bounds__(256) k_reduce_rows(const double* part, int nw,
 }
 
 // Y(i, :) = Z(i, :) x T   (T P x Pout column-major, Z/Y column-major)
-__global__ void k_apply_small(const double* Z, long long ldz, int P, const double* T,
+static __global__ void k_apply_small(const double* Z, long long ldz, int P, const double* T,
                               int Pout, double* Y, long long ldy, int nrows,
                               const int* abort_flag) {
   if (abort_flag && *abort_flag) return;
@@ -1167,7 +1167,7 @@ __global__ void k_apply_small(const double* Z, long long ldz, int P, const doubl
 }
 
 // colsum2[j] = sum_i V(i, j)^2  (one wave per column)
-__global__ void __launch_bounds__(256) k_colnorm2(const double* V, long long ldv, int nrows,
+static __global__ void __launch_bounds__(256) k_colnorm2(const double* V, long long ldv, int nrows,
                                                   int ncols, double* out) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int j = blockIdx.x * 4 + wave;
@@ -1189,7 +1189,7 @@ __global__ void __launch_bounds__(256) k_colnorm2(const double* V, long long ldv
 // part[blk][0:d] = acc_k, [d] = accE, [d+1] = accT
 // ---------------------------------------------------------------------------
 template <int DMAX, int QMAX>
-__global__ void __launch_bounds__(256) k_contract(const double* Ainv, long long lda,
+static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, long long lda,
                                                   const double* xw, int d,
                                                   const double* Wa, long long ldw, int q1,
                                                   int n_valid, double* part,
@@ -1287,7 +1287,7 @@ __global__ void __launch_bounds__(256) k_contract(const double* Ainv, long long 
 }
 
 // xw(i,k) = X(i,k) / delta_k  for i < n, 0 for padded rows
-__global__ void k_scale_points(const double* X, const double* inv_delta, int d, int n,
+static __global__ void k_scale_points(const double* X, const double* inv_delta, int d, int n,
                                int n_pad, double* xw) {
   long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (long long)n_pad * d) return;
@@ -1296,7 +1296,7 @@ __global__ void k_scale_points(const double* X, const double* inv_delta, int d, 
 }
 
 // set tile (t,t) of M to the identity for t >= t0 (padding blocks of the inverse)
-__global__ void k_identity_tiles(double* M, long long ld, int t0) {
+static __global__ void k_identity_tiles(double* M, long long ld, int t0) {
   const int t = t0 + blockIdx.x;
   double* base = M + (long long)t * TILE * (ld + 1);
   for (int e = threadIdx.x; e < TILE * TILE; e += blockDim.x) {

@@ -52,7 +52,20 @@ SIGNATURES = {
     "gpe_set_profiling": (_ct.c_int, [_VP, _ct.c_int32]),
     "gpe_phase_times": (_ct.c_int, [_VP, _D, _ct.c_int32]),
     "gpe_gemm_stats": (_ct.c_int, [_VP, _D, _D, _D]),
+    # include/gpemu_dist.h: row-block distributed value objective (RCCL / loopback)
+    "gpe_dist_unique_id": (_ct.c_int, [_ct.c_char_p, _ct.c_int32]),
+    "gpe_dist_create": (_VP, [_ct.c_int32, _ct.c_int32, _ct.c_int32, _ct.c_char_p]),
+    "gpe_dist_destroy": (None, [_VP]),
+    "gpe_dist_last_error": (_ct.c_char_p, [_VP]),
+    "gpe_dist_set_data": (_ct.c_int, [_VP, _ct.c_int64, _ct.c_int32, _ct.c_int32, _D, _D, _D, _D]),
+    "gpe_dist_objective": (_ct.c_int, [_VP, _ct.c_int32, _ct.c_int32, _D, _ct.c_int32, _ct.c_double,
+                                       _D, _D]),
+    "gpe_dist_owner": (_ct.c_int32, [_ct.c_int32, _ct.c_int32]),
+    "gpe_dist_local_rows": (_ct.c_int32, [_ct.c_int64, _ct.c_int32, _ct.c_int32]),
+    "gpe_dist_times": (_ct.c_int, [_VP, _D, _D]),
 }
+
+UNIQUE_ID_BYTES = 128
 
 
 class NativeUnavailable(RuntimeError):
@@ -308,3 +321,93 @@ def default_context() -> Context:
             dev = int(_os.environ.get("GPEMU_DEVICE", _os.environ.get("LOCAL_RANK", "0")))
             _default_ctx = Context(dev)
         return _default_ctx
+
+
+class DistContext:
+    """Row-block distributed value objective over P GPUs (include/gpemu_dist.h).
+
+    unique_id=None selects the in-process loopback transport: all `nranks`
+    logical ranks run in this process on `device` (same partition and schedule,
+    device copies instead of RCCL).  With a unique id (bytes from
+    ``dist_unique_id()`` on rank 0, shared by the host, see distributed.py) this
+    process is rank `rank` of an RCCL communicator of `nranks` GPUs.
+    """
+
+    def __init__(self, device: int, nranks: int, rank: int = 0, unique_id: bytes | None = None):
+        self.lib = load_library()
+        if self.lib.gpe_device_count() <= 0:
+            raise NativeUnavailable("no HIP device visible to libgpemu.so")
+        if unique_id is not None and len(unique_id) != UNIQUE_ID_BYTES:
+            raise ValueError("unique_id must be 128 bytes")
+        h = self.lib.gpe_dist_create(int(device), int(nranks), int(rank), unique_id)
+        if not h:
+            raise NativeUnavailable("gpe_dist_create failed")
+        self._h = h
+        self.nranks, self.rank, self.loopback = nranks, rank, unique_id is None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.gpe_dist_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc == GPE_OK:
+            return
+        msg = self.lib.gpe_dist_last_error(self._h).decode()
+        if rc == GPE_NOT_PD:
+            raise NotPositiveDefinite(f"{what}: {msg}")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+    def set_data(self, X, f, H, r=None):
+        X = _f64(X)
+        if X.ndim == 1:
+            X = X.reshape(-1, 1)
+        n, d = X.shape
+        f = _f64(f, (n,))
+        H = _f64(H)
+        if H.ndim == 1:
+            H = H.reshape(n, -1)
+        rr = None if r is None or _np.isscalar(r) else _f64(r, (n,))
+        self._keep = (X, f, H, rr)
+        self._check(self.lib.gpe_dist_set_data(self._h, n, d, H.shape[1], _ptr(X), _ptr(f), _ptr(H),
+                                               _ptr(rr)), "gpe_dist_set_data")
+
+    def objective(self, variant, kernel, hp, nu_fixed=0.0):
+        """Value-only objective (collective over all ranks): (llh, sigma2)."""
+        hp = _f64(hp).ravel()
+        llh, s2 = _ct.c_double(0.0), _ct.c_double(0.0)
+        self._check(self.lib.gpe_dist_objective(self._h, int(variant), int(kernel), _ptr(hp), hp.size,
+                                                float(nu_fixed), _ct.byref(llh), _ct.byref(s2)),
+                    "gpe_dist_objective")
+        return llh.value, s2.value
+
+    def times(self):
+        tot, comm = _ct.c_double(0.0), _ct.c_double(0.0)
+        self._check(self.lib.gpe_dist_times(self._h, _ct.byref(tot), _ct.byref(comm)), "gpe_dist_times")
+        return {"total_ms": tot.value, "comm_ms": comm.value}
+
+
+def dist_unique_id() -> bytes:
+    """A fresh RCCL communicator id (rank 0 only)."""
+    lib = load_library()
+    buf = _ct.create_string_buffer(UNIQUE_ID_BYTES)
+    rc = lib.gpe_dist_unique_id(buf, UNIQUE_ID_BYTES)
+    if rc != GPE_OK:
+        raise RuntimeError(f"gpe_dist_unique_id failed ({rc})")
+    return buf.raw
+
+
+def dist_owner(nranks: int, tile_row: int) -> int:
+    """Rank that stores 128-row tile row `tile_row` (pure; no GPU)."""
+    return int(load_library().gpe_dist_owner(int(nranks), int(tile_row)))
+
+
+def dist_local_rows(n: int, nranks: int, rank: int) -> int:
+    """Tile rows (incl. the augmented [f H] row) rank `rank` stores (pure; no GPU)."""
+    return int(load_library().gpe_dist_local_rows(int(n), int(nranks), int(rank)))

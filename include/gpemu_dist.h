@@ -1,0 +1,68 @@
+/*
+ * gpemu_dist.h -- C-ABI of the row-block distributed objective in libgpemu.so
+ * (BASELINE configs[3]: n = 65536, d = 20 on 8 x MI355X).
+ *
+ * Replaces, for one evaluation spread over P GPUs, the value part of
+ * Optimize.loglikelihood_gp4ml / _mucm (_emulatoroptimise.py:412-493, :305-378):
+ * K-build + blocked right-looking Cholesky + log|A| + L^-1 [f H].  The n x n
+ * covariance is partitioned by 128-row tile rows, dealt cyclically (tile row i on
+ * rank i mod P); each rank stores only its tile rows of the lower triangle.  Per
+ * column step the owner factors the diagonal tile in-kernel, RCCL broadcasts its
+ * inverse (128 KB), every rank forms its panel tiles, RCCL all-gathers the panel
+ * column, and every rank applies the trailing update to its own rows.  [f H] is
+ * carried as one extra tile row under the matrix, so L^-1 [f H] and its Gram
+ * matrix fall out of the same sweep (no triangular inverse for the value).
+ *
+ * Processes: one per GPU.  Rank 0 calls gpe_dist_unique_id, the host shares the
+ * 128 bytes (torch.distributed / gloo in gp_emu_uqsa_amd/distributed.py), every
+ * rank calls gpe_dist_create with it.  unique_id == NULL selects the in-process
+ * loopback transport: all P logical ranks live in this process on one GPU, with
+ * the same partition and schedule and device copies in place of RCCL (used to
+ * test P = 2..8 on one GPU).
+ *
+ * Same conventions and status codes as gpemu.h.  The gradient stays on the
+ * single-GPU path (the distributed TRTRI/LAUUM is SURVEY.md 8f item 2).
+ */
+#ifndef GPEMU_DIST_H
+#define GPEMU_DIST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gpe_dist gpe_dist;
+
+/* RCCL unique id for a new communicator (len >= 128); rank 0 only. */
+int gpe_dist_unique_id(uint8_t* out, int32_t len);
+
+/* device: GPU of this process; nranks: P; rank: this process's rank (ignored in
+ * loopback); unique_id: 128 bytes from gpe_dist_unique_id, or NULL = loopback. */
+gpe_dist* gpe_dist_create(int32_t device, int32_t nranks, int32_t rank, const uint8_t* unique_id);
+void gpe_dist_destroy(gpe_dist* h);
+const char* gpe_dist_last_error(gpe_dist* h);
+
+/* Replicated inputs, as gpe_set_data (every rank passes the same arrays). */
+int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double* X,
+                      const double* f, const double* H, const double* r);
+
+/* Value-only objective, arguments as gpe_objective (want_grad = 0).  All ranks
+ * call it collectively and all receive the same llh / sigma2. */
+int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const double* hp,
+                       int32_t n_hp, double nu_fixed, double* llh_out, double* sigma2_out);
+
+/* Partition map (pure functions, no GPU): owner rank of tile row t and the number
+ * of tile rows (including the augmented [f H] row) rank `rank` stores. */
+int32_t gpe_dist_owner(int32_t nranks, int32_t tile_row);
+int32_t gpe_dist_local_rows(int64_t n, int32_t nranks, int32_t rank);
+
+/* Time of the last gpe_dist_objective: total and the part spent in collectives
+ * (RCCL or loopback copies), ms, measured with HIP events on this rank. */
+int gpe_dist_times(gpe_dist* h, double* total_ms, double* comm_ms);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GPEMU_DIST_H */

@@ -1,0 +1,140 @@
+"""Row-block distributed objective on CPU: the partition map the
+library exports, the RCCL-id hand-off over gloo, and a NumPy model of the exact
+per-step schedule of gpemu_dist.hip (cyclic tile rows + augmented [f H] row,
+broadcast of the diagonal inverse, all-gather of the panel column, own-row trailing
+update) run on 2 and 3 gloo ranks against a dense factorisation.  NumPy is only the
+test's stand-in for the HIP tile kernels."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from gp_emu_uqsa_amd import distributed, native
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("n,P", [(1, 1), (128, 2), (1000, 4), (16384, 8), (65536, 8), (700, 3)])
+def test_partition_map(n, P):
+    nb = (n + 127) // 128
+    rows = distributed.partition(n, P)
+    assert sorted(t for r in rows.values() for t in r) == list(range(nb + 1))
+    for r in range(P):
+        assert rows[r] == list(range(r, nb + 1, P))
+        assert native.dist_local_rows(n, P, r) == len(rows[r])
+    assert native.dist_owner(P, nb) == nb % P
+
+
+def _uid_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        calls = []
+
+        def make():
+            calls.append(1)
+            return bytes(range(128))
+        out[rank] = (distributed.share_unique_id(make_id=make), len(calls))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_unique_id_shared_from_rank0():
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_uid_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    assert res[0][0] == res[1][0] == bytes(range(128))
+    assert res[0][1] == 1 and res[1][1] == 0          # only rank 0 creates the id
+
+
+B = 8   # model tile size (the library uses 128; the schedule does not depend on it)
+
+
+def _problem(n, q, seed=3):
+    rng = np.random.RandomState(seed)
+    X = rng.uniform(size=(n, 2))
+    d2 = ((X[:, None, :] - X[None, :, :]) ** 2).sum(-1)
+    A = np.exp(-d2 / 0.3) + 0.05 * np.eye(n)
+    F = rng.normal(size=(n, q + 1))
+    return A, F
+
+
+def _sched_worker(rank, world, port, n, q, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        A, F = _problem(n, q)
+        nb = n // B
+        Pc = q + 1
+        # augmented matrix: tile row nb holds F^T (zero padded to B rows), (nb, nb) = 0
+        full = np.zeros(((nb + 1) * B, (nb + 1) * B))
+        full[:n, :n] = A
+        full[n:n + Pc, :n] = F.T
+        mine = [t for t in range(nb + 1) if t % world == rank]
+        loc = {t: full[t * B:(t + 1) * B, :].copy() for t in mine}     # own tile rows
+        logdet = np.zeros(nb + 1)
+        for k in range(nb):
+            owner = k % world
+            dinv = torch.zeros(B, B, dtype=torch.float64)
+            if owner == rank:
+                L = np.linalg.cholesky(loc[k][:, k * B:(k + 1) * B])
+                loc[k][:, k * B:(k + 1) * B] = L
+                logdet[k] = np.log(np.diag(L)).sum()
+                dinv = torch.from_numpy(np.linalg.inv(L))
+            dist.broadcast(dinv, src=owner)
+            Dinv = dinv.numpy()
+            rows = [t for t in mine if t > k]
+            for t in rows:                                            # panel
+                loc[t][:, k * B:(k + 1) * B] = loc[t][:, k * B:(k + 1) * B] @ Dinv.T
+            maxT = max(len([t for t in range(nb + 1) if t % world == r and t > k]) for r in range(world))
+            send = torch.zeros(maxT, B, B, dtype=torch.float64)
+            for i, t in enumerate(rows):
+                send[i] = torch.from_numpy(loc[t][:, k * B:(k + 1) * B])
+            recv = [torch.zeros_like(send) for _ in range(world)]
+            dist.all_gather(recv, send)
+            panel = {}
+            for r in range(world):                                   # unpermute
+                rt = [t for t in range(nb + 1) if t % world == r and t > k]
+                for i, t in enumerate(rt):
+                    panel[t] = recv[r][i].numpy()
+            for t in rows:                                            # own-row update
+                for j in range(k + 1, t + 1):
+                    loc[t][:, j * B:(j + 1) * B] -= loc[t][:, k * B:(k + 1) * B] @ panel[j].T
+        ld = torch.from_numpy(logdet)
+        dist.all_reduce(ld)
+        g = torch.zeros(Pc, Pc, dtype=torch.float64)
+        if nb % world == rank:
+            g = torch.from_numpy(-loc[nb][:Pc, nb * B:nb * B + Pc].copy())
+        dist.broadcast(g, src=nb % world)
+        out[rank] = (2.0 * float(ld.sum()), g.numpy().tolist())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_schedule_model_matches_dense(world):
+    n, q = 7 * B, 3
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_sched_worker, args=(world, port, n, q, out), nprocs=world, join=True)
+        res = dict(out)
+    A, F = _problem(n, q)
+    L = np.linalg.cholesky(A)
+    Z = np.linalg.solve(L, F)
+    for r in range(world):
+        logdet, G = res[r]
+        assert abs(logdet - np.linalg.slogdet(A)[1]) < 1e-10 * abs(logdet)
+        assert np.max(np.abs(np.array(G) - Z.T @ Z)) < 1e-10 * np.max(np.abs(Z.T @ Z))

@@ -1,0 +1,75 @@
+"""Row-block distributed value objective (include/gpemu_dist.h) on the GPU:
+the loopback transport (P logical ranks in one process, same partition and
+schedule as RCCL) for P = 1..8, and a 1-rank RCCL communicator, against the
+oracle (reference op order) and the single-GPU path."""
+import numpy as np
+import pytest
+
+from gp_emu_uqsa_amd import native
+from oracle import gp_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _hp(d, fit_nug=True, gp4ml=True):
+    hp = [0.6 + 0.1 * k for k in range(d)]
+    if fit_nug:
+        hp.append(1e-2)
+    if gp4ml:
+        hp.append(0.9)
+    return np.array(hp)
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("n", [300, 1000])
+def test_loopback_matches_oracle(P, n):
+    X, f, H = orc.synthetic_problem(n, 3, seed=1)
+    hp = _hp(3)
+    ctx = native.DistContext(0, P)
+    ctx.set_data(X, f, H)
+    llh, s2 = ctx.objective(native.GP4ML, native.KERNEL_STD, hp)
+    ref = orc.objective_ref(X, f, H, hp, orc.GP4ML, orc.STD, True, want_grad=False)[0]
+    assert abs(llh - ref) <= 1e-9 * abs(ref), (llh, ref)
+    assert abs(s2 - hp[-1] ** 2) < 1e-15
+    ctx.close()
+
+
+@pytest.mark.parametrize("variant,kernel,use_r", [(native.MUCM, native.KERNEL_STD, False),
+                                                  (native.GP4ML, native.KERNEL_ALT_NUG, True)])
+def test_loopback_variants_match_single_gpu(ctx, variant, kernel, use_r):
+    n, d = 777, 4
+    X, f, H = orc.synthetic_problem(n, d, seed=2)
+    r = np.random.RandomState(5).uniform(1e-4, 1e-3, size=n) if use_r else None
+    hp = _hp(d, gp4ml=variant == native.GP4ML)
+    ctx.set_data(X, f, H, r)
+    ref, _, s2ref = ctx.objective(variant, kernel, hp, want_grad=False)
+    dc = native.DistContext(0, 3)
+    dc.set_data(X, f, H, r)
+    llh, s2 = dc.objective(variant, kernel, hp)
+    assert abs(llh - ref) <= 1e-10 * abs(ref), (llh, ref)
+    assert abs(s2 - s2ref) <= 1e-10 * abs(s2ref)
+    dc.close()
+
+
+def test_loopback_not_pd():
+    X, f, H = orc.synthetic_problem(400, 2, seed=3)
+    X[1] = X[0]                                   # duplicate point, no nugget
+    dc = native.DistContext(0, 2)
+    dc.set_data(X, f, H)
+    with pytest.raises(native.NotPositiveDefinite):
+        dc.objective(native.GP4ML, native.KERNEL_STD, np.array([0.5, 0.5, 1.0]), nu_fixed=0.0)
+    dc.close()
+
+
+def test_rccl_single_rank():
+    n, d = 2000, 10
+    X, f, H = orc.synthetic_problem(n, d, seed=4)
+    hp = _hp(d)
+    dc = native.DistContext(0, 1, 0, native.dist_unique_id())
+    dc.set_data(X, f, H)
+    llh, _ = dc.objective(native.GP4ML, native.KERNEL_STD, hp)
+    ref = orc.objective_ref(X, f, H, hp, orc.GP4ML, orc.STD, True, want_grad=False)[0]
+    assert abs(llh - ref) <= 1e-9 * abs(ref), (llh, ref)
+    t = dc.times()
+    assert t["total_ms"] > 0.0
+    dc.close()

@@ -1,0 +1,77 @@
+"""Distributed value objective (BASELINE configs[3]) -- runner.
+
+  one GPU, P logical ranks (loopback):   python tools/dist_objective.py --loopback P --points N --dims D
+  P GPUs over RCCL (one process each):    python -m torch.distributed.run --nproc-per-node P \\
+                                              --master-addr 127.0.0.1 tools/dist_objective.py --points N --dims D
+Prints one JSON line (rank 0): llh, ms per eval (max over ranks), comm ms, and
+with --check the single-GPU value for the same inputs.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--points", type=int, default=4096)
+    ap.add_argument("--dims", type=int, default=10)
+    ap.add_argument("--loopback", type=int, default=0)
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--check", action="store_true")
+    args = ap.parse_args()
+    from gp_emu_uqsa_amd import native
+    from oracle import gp_oracle as orc   # synthetic input generator
+    X, f, H = orc.synthetic_problem(args.points, args.dims, seed=0)
+    hp = np.concatenate([np.ones(args.dims), [1e-3, 1.0]])
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dist = None
+    if args.loopback:
+        ctx = native.DistContext(int(os.environ.get("LOCAL_RANK", "0")), args.loopback)
+        nranks = args.loopback
+    else:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from gp_emu_uqsa_amd import distributed
+        ctx = distributed.dist_context()
+        nranks = world
+    ctx.set_data(X, f, H)
+    llh, _ = ctx.objective(native.GP4ML, native.KERNEL_STD, hp)   # warm-up
+    ts = []
+    for _ in range(args.reps):
+        if dist is not None:
+            dist.barrier()
+        t = time.perf_counter()
+        llh, _ = ctx.objective(native.GP4ML, native.KERNEL_STD, hp)
+        ts.append(time.perf_counter() - t)
+    el = min(ts)
+    if dist is not None:
+        import torch
+        v = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        el = float(v.item())
+    out = {"n": args.points, "d": args.dims, "ranks": nranks, "transport": "loopback" if args.loopback else "rccl",
+           "llh": llh, "ms_per_eval": 1e3 * el, **ctx.times()}
+    if args.check and rank == 0:
+        c1 = native.Context(int(os.environ.get("LOCAL_RANK", "0")))
+        c1.set_data(X, f, H)
+        ref, _, _ = c1.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=False)
+        out["single_gpu_llh"] = ref
+        out["rel_diff"] = abs(llh - ref) / abs(ref)
+        c1.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
