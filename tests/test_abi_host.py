@@ -12,9 +12,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _declared_symbols():
-    text = open(os.path.join(ROOT, "include", "gpemu.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|gpe_ctx\*|const char\*)\s+\*?(gpe_\w+)\s*\(",
-                                 text, flags=re.M)))
+    names = set()
+    for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
+        if not h.endswith(".h"):
+            continue
+        text = open(os.path.join(ROOT, "include", h)).read()
+        names |= set(re.findall(r"^\s*(?:int|int32_t|void|gpe_ctx\*|gpe_dist\*|const char\*)\s+\*?(gpe_\w+)\s*\(",
+                                text, flags=re.M))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():
