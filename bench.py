@@ -111,10 +111,10 @@ def main():
         torch.cuda.set_device(local)
 
     from gp_emu_uqsa_amd import native
-    from oracle import gp_oracle as orc   # synthetic input generator only
+    from gp_emu_uqsa_amd import synthetic
 
     ctx = native.Context(local)
-    X, f, H = orc.synthetic_problem(args.n, args.d, seed=0)
+    X, f, H = synthetic.problem(args.n, args.d, seed=0)
     ctx.set_data(X, f, H)
     hp = eval_point(args.d, rank)
     prof = not args.no_profile

@@ -92,3 +92,14 @@ def test_posterior_ref(tag):
     np.testing.assert_allclose(m, z["mean"], rtol=0, atol=1e-12)
     np.testing.assert_allclose(v, z["var"], rtol=0, atol=1e-12)
     np.testing.assert_allclose(orc.optimal_beta_ref(A, z["HT"], z["fT"]), z["beta_opt"], atol=1e-10)
+
+
+def test_product_generator_equals_oracle_generator():
+    """bench.py/tools draw their inputs from gp_emu_uqsa_amd.synthetic; the oracle
+    keeps its own copy for the checks -- both must give the same data."""
+    from gp_emu_uqsa_amd import synthetic
+    for n, d, seed in [(50, 1, 0), (300, 3, 1), (1000, 10, 2)]:
+        a = synthetic.problem(n, d, seed)
+        b = orc.synthetic_problem(n, d, seed)
+        for u, v in zip(a, b):
+            assert np.array_equal(u, v)

@@ -27,8 +27,8 @@ def main():
     ap.add_argument("--check", action="store_true")
     args = ap.parse_args()
     from gp_emu_uqsa_amd import native
-    from oracle import gp_oracle as orc   # synthetic input generator
-    X, f, H = orc.synthetic_problem(args.points, args.dims, seed=0)
+    from gp_emu_uqsa_amd import synthetic
+    X, f, H = synthetic.problem(args.points, args.dims, seed=0)
     hp = np.concatenate([np.ones(args.dims), [1e-3, 1.0]])
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

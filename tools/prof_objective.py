@@ -3,10 +3,10 @@ import sys
 import numpy as np
 sys.path.insert(0, '.')
 from gp_emu_uqsa_amd import native
-from oracle import gp_oracle as orc
+from gp_emu_uqsa_amd import synthetic
 n = int(sys.argv[1]); d = int(sys.argv[2]); reps = int(sys.argv[3])
 ctx = native.Context(0)
-X, f, H = orc.synthetic_problem(n, d, seed=0)
+X, f, H = synthetic.problem(n, d, seed=0)
 ctx.set_data(X, f, H)
 hp = np.concatenate([np.ones(d), [1e-3, 1.0]])
 for _ in range(reps):

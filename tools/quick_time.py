@@ -3,11 +3,11 @@ import sys, time
 import numpy as np
 sys.path.insert(0, '.')
 from gp_emu_uqsa_amd import native
-from oracle import gp_oracle as orc
+from gp_emu_uqsa_amd import synthetic
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
 d = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 ctx = native.Context(0)
-X, f, H = orc.synthetic_problem(n, d, seed=0)
+X, f, H = synthetic.problem(n, d, seed=0)
 ctx.set_data(X, f, H)
 hp = np.concatenate([np.ones(d), [1e-3, 1.0]])
 ctx.objective(0, 0, hp)

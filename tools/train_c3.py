@@ -1,0 +1,84 @@
+"""BASELINE configs[2]: the full g.setup()/g.train() loop at
+n=16384, d=10 through the reference's API and file surface, scipy L-BFGS-B
+driving the GPU objective (LLH + gradient) -- dev/measurement tool.
+
+Writes config/beliefs/inputs/outputs for synthetic oLHC data into a scratch
+directory (tv_config 10 0 0: every point in training; gp4ml, nugget fitted,
+linear mean in all inputs, tries 1, constraints bounds), then times setup and
+train and prints one JSON line: wall seconds, objective evaluations, seconds per
+evaluation, trained delta / nugget / sigma, final LLH.
+usage: python tools/train_c3.py [--points 16384] [--dims 10] [--tries 1]
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def write_files(root, n, d, tries):
+    from gp_emu_uqsa_amd import synthetic
+    X, f, _ = synthetic.problem(n, d, seed=0)
+    np.savetxt(os.path.join(root, "c3_input"), X, fmt="%.10f")
+    np.savetxt(os.path.join(root, "c3_output"), f.reshape(-1, 1), fmt="%.10f")
+    with open(os.path.join(root, "c3_config"), "w") as fh:
+        fh.write("beliefs c3_beliefs\ninputs c3_input\noutputs c3_output\ntv_config 10 0 0\n"
+                 "delta_bounds [ ]\nnugget_bounds [ ]\nsigma_bounds [ ]\n"
+                 f"tries {tries}\nconstraints bounds\n")
+    with open(os.path.join(root, "c3_beliefs"), "w") as fh:
+        fh.write("active all\noutput 0\n"
+                 "basis_str 1.0" + " x" * d + "\n"
+                 "basis_inf NA" + "".join(f" {k}" for k in range(d)) + "\n"
+                 "beta" + " 1.0" * (d + 1) + "\n"
+                 "delta" + " 1.0" * d + "\n"
+                 "sigma 1.0\nnugget 0.001\nfix_nugget F\nmucm F\n")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--points", type=int, default=16384)
+    ap.add_argument("--dims", type=int, default=10)
+    ap.add_argument("--tries", type=int, default=1)
+    args = ap.parse_args()
+    import gp_emu_uqsa_amd as g
+    from gp_emu_uqsa_amd import native
+    calls = {"n": 0, "s": 0.0}
+    orig = native.Context.objective
+
+    def counted(self, *a, **k):
+        t = time.perf_counter()
+        try:
+            return orig(self, *a, **k)
+        finally:
+            calls["n"] += 1
+            calls["s"] += time.perf_counter() - t
+    native.Context.objective = counted
+    with tempfile.TemporaryDirectory() as tmp:
+        write_files(tmp, args.points, args.dims, args.tries)
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            np.random.seed(0)
+            t0 = time.perf_counter()
+            E = g.setup("c3_config", datashuffle=True)
+            t1 = time.perf_counter()
+            g.train(E, auto=True)
+            t2 = time.perf_counter()
+        finally:
+            os.chdir(cwd)
+    out = {"config": f"C3 g.train(): n={args.points} d={args.dims} gp4ml nugget fitted, tries {args.tries}",
+           "setup_s": t1 - t0, "train_s": t2 - t1, "objective_evals": calls["n"],
+           "objective_s": calls["s"], "s_per_eval": calls["s"] / max(calls["n"], 1),
+           "delta": np.asarray(E.par.delta).tolist(), "nugget": float(E.par.nugget),
+           "sigma": float(E.par.sigma)}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
