@@ -120,6 +120,13 @@ struct gpe_ctx {
   double* hpin = nullptr;
   size_t hpin_cap = 0;
 
+  // fp32 posterior (precision 32): copy of L^-1 and per-chunk K*, V
+  float* dX32 = nullptr;
+  size_t x32_cap = 0;
+  bool x32_valid = false;
+  float* dK32 = nullptr;
+  size_t k32_cap = 0;
+
   // resident factor (gpe_factor)
   bool factor_valid = false;
   int f_kernel = 0;
@@ -858,6 +865,8 @@ void gpe_destroy(gpe_ctx* c) {
   for (double* b : bufs)
     if (b) hipFree(b);
   if (c->dinfo) hipFree(c->dinfo);
+  if (c->dX32) hipFree(c->dX32);
+  if (c->dK32) hipFree(c->dK32);
   if (c->tr.flags) hipFree(c->tr.flags);
   if (c->aux.flags) hipFree(c->aux.flags);
   if (c->dprobs) hipFree(c->dprobs);
@@ -896,6 +905,7 @@ int gpe_set_data(gpe_ctx* c, int64_t n, int32_t d, int32_t q, const double* X, c
   const bool resize = (n_pad != c->n_pad) || (d != c->d) || (q != c->q);
   c->n = n; c->d = d; c->q = q; c->n_pad = n_pad; c->NB = (int)(n_pad / TILE);
   c->factor_valid = false;
+  c->x32_valid = false;
   if (resize) {
     CHK(ensure_fact(c, c->tr, n_pad));
     CHK(dalloc(c, &c->dX, (size_t)n_pad * d));
@@ -966,6 +976,7 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
   const double s2 = gp4ml ? sigma * sigma : 1.0;
   const double rscale = (gp4ml && kernel == GPE_KERNEL_ALT_NUG) ? 1.0 : 0.0;
   c->factor_valid = false;
+  c->x32_valid = false;
   if (c->prof) {
     c->gev_used = 0;
     c->gemm_launches = c->gemm_flops = c->gemm_ms = 0.0;
@@ -1091,6 +1102,7 @@ int gpe_factor(gpe_ctx* c, int32_t kernel, const double* delta, double nu, doubl
   if (!delta) return fail(c, GPE_ERR_ARG, "null delta");
   if (kernel != GPE_KERNEL_STD && kernel != GPE_KERNEL_ALT_NUG) return fail(c, GPE_ERR_ARG, "bad kernel");
   c->factor_valid = false;
+  c->x32_valid = false;
   CHK(factor_and_invert(c, kernel, delta, nu, s2, r_scale));
   int info = 0;
   double logdet = 0.0;
@@ -1100,6 +1112,7 @@ int gpe_factor(gpe_ctx* c, int32_t kernel, const double* delta, double nu, doubl
     return GPE_NOT_PD;
   }
   c->factor_valid = true;
+  c->x32_valid = false;
   c->f_kernel = kernel;
   c->f_delta.assign(delta, delta + c->d);
   c->f_nu = nu;
@@ -1121,13 +1134,31 @@ int gpe_beta(gpe_ctx* c, double* beta_out) {
 }
 
 int gpe_posterior(gpe_ctx* c, int64_t m, const double* Xs, const double* Hs, const double* beta,
-                  double sigma, int32_t full_var, double* mean_out, double* var_out) {
+                  double sigma, int32_t full_var, int32_t precision, double* mean_out, double* var_out) {
   CHK(check_ready(c));
   if (!c->factor_valid) return fail(c, GPE_ERR_STATE, "no resident factor (call gpe_factor)");
   if (m <= 0 || !Xs || !Hs || !beta || !mean_out || !var_out) return fail(c, GPE_ERR_ARG, "bad posterior args");
+  if (precision != 64 && precision != 32) return fail(c, GPE_ERR_ARG, "precision must be 64 or 32");
+  if (precision == 32 && full_var) return fail(c, GPE_ERR_UNSUPPORTED, "precision 32 is for the diagonal variance");
+  const bool f32 = precision == 32;
   const int d = c->d, q = c->q, P = q + 1;
   const long long np = c->n_pad;
-  const long long CHUNK = full_var ? 16384 : 4096;
+  const long long CHUNK = full_var ? 16384 : 8192;
+  if (f32 && !c->x32_valid) {
+    // fp32 copy of L^-1 (the full square: the GEMM reads only k <= its row tile)
+    const size_t need = (size_t)np * np;
+    if (need > c->x32_cap) {
+      if (c->dX32) (void)hipFree(c->dX32);
+      c->dX32 = nullptr;
+      HIPCHK(c, hipMalloc((void**)&c->dX32, need * sizeof(float)));
+      c->x32_cap = need;
+    }
+    const long long tot = np * np;
+    hipLaunchKernelGGL(k_to_f32, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, c->tr.B, np,
+                       c->dX32, np, np, (int)np);
+    HIPCHK(c, hipGetLastError());
+    c->x32_valid = true;
+  }
   if (full_var && m > CHUNK) return fail(c, GPE_ERR_UNSUPPORTED, "full posterior variance limited to m <= 16384");
   // [gamma, G] = A^-1 [f - H beta, H]
   CHK(ensure_pinned(c, (size_t)P * P + 64));
@@ -1227,7 +1258,24 @@ int gpe_posterior(gpe_ctx* c, int64_t m, const double* Xs, const double* Hs, con
       HIPCHK(c, hipGetLastError());
     }
     // V = L^-1 K*   (np x mp), X lower-triangular -> kend = (ti+1)*128
-    {
+    if (f32) {
+      const size_t need32 = 2 * (size_t)np * mp;
+      if (need32 > c->k32_cap) {
+        if (c->dK32) (void)hipFree(c->dK32);
+        c->dK32 = nullptr;
+        HIPCHK(c, hipMalloc((void**)&c->dK32, need32 * sizeof(float)));
+        c->k32_cap = need32;
+      }
+      float* K32 = c->dK32;
+      float* V32 = c->dK32 + (size_t)np * mp;
+      const long long tot = np * mp;
+      hipLaunchKernelGGL(k_to_f32, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, c->dW1, np,
+                         K32, np, np, (int)mp);
+      HIPCHK(c, hipGetLastError());
+      hipLaunchKernelGGL(k_gemm_f32, dim3((unsigned)(c->NB * mt)), dim3(256), 2 * F32_STAGE * sizeof(float),
+                         c->stream, c->dX32, np, K32, np, V32, np, c->NB, (int)np, 1);
+      HIPCHK(c, hipGetLastError());
+    } else {
       std::vector<GemmProb> pv = {mkprob(c->tr.B, np, c->dW1, np, c->dW2, np, c->NB, mt, (int)np,
                                          G_KEND_TI, 1.0, 0.0)};
       pv[0].tile_begin = 0;
@@ -1256,8 +1304,12 @@ int gpe_posterior(gpe_ctx* c, int64_t m, const double* Xs, const double* Hs, con
     if (!full_var) {
       CHK(ensure_small(c, (size_t)mp * P + mp + 64));
       double* dn = c->dsmall + (size_t)mp * P;
-      hipLaunchKernelGGL(k_colnorm2, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, c->stream, c->dW2, np,
-                         (int)np, (int)mp, dn);
+      if (f32)
+        hipLaunchKernelGGL(k_colnorm2_f32, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, c->stream,
+                           c->dK32 + (size_t)np * mp, np, (int)np, (int)mp, dn);
+      else
+        hipLaunchKernelGGL(k_colnorm2, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, c->stream, c->dW2, np,
+                           (int)np, (int)mp, dn);
       HIPCHK(c, hipGetLastError());
       HIPCHK(c, hipMemcpyAsync(c->hpin, dn, (size_t)mp * sizeof(double), hipMemcpyDeviceToHost, c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));

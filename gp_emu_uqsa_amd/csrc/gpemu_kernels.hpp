@@ -846,6 +846,134 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
 }
 
 // ---------------------------------------------------------------------------
+// fp32 GEMM for the posterior's V = L^-1 K* at precision 32 (BASELINE C5):
+// C(m,n) = sum_k A(m,k) B(k,n), A M-contiguous (the triangle, G_KEND_TI), B
+// K-contiguous (K*), fp32 in and out, v_mfma_f32_16x16x4_f32.  Same tiling as
+// k_gemm: 128x128 tile, 4 waves of 64x64, K staged 32 deep in double-buffered
+// LDS: [k][m] pitch 144 floats and [n][k] pitch 36 floats, both conflict-free for
+// ds_read_b32 (lane -> bank is a permutation).  Operands swapped as in k_gemm so
+// the stores are M-contiguous; f32 C/D map: row = 4 (lane >> 4) + reg.
+// ---------------------------------------------------------------------------
+constexpr int F32_GK = 32;
+constexpr int F32_PA = 144;   // [k][m]
+constexpr int F32_PB = 36;    // [n][k]
+constexpr int F32_STAGE = F32_GK * F32_PA + TILE * F32_PB;   // floats per stage (9216)
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float4 gld4f(const float* p) {
+  const f4v v = *(__attribute__((address_space(1))) const f4v*)(p);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ void g32_gload(const float* Ab, const float* Bb, long long lda, long long ldb, int k0,
+                                          int tid, float (&ra)[16], float (&rb)[16]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int c = tid + 256 * u;
+    const int kk = c >> 5, mm = (c & 31) * 4;
+    const float4 a = gld4f(Ab + mm + (long long)(k0 + kk) * lda);
+    const int nn = c >> 3, k2 = (c & 7) * 4;
+    const float4 b = gld4f(Bb + (long long)nn * ldb + k0 + k2);
+    ra[4 * u] = a.x; ra[4 * u + 1] = a.y; ra[4 * u + 2] = a.z; ra[4 * u + 3] = a.w;
+    rb[4 * u] = b.x; rb[4 * u + 1] = b.y; rb[4 * u + 2] = b.z; rb[4 * u + 3] = b.w;
+  }
+}
+
+__device__ __forceinline__ void g32_sstore(float* st, int tid, const float (&ra)[16], const float (&rb)[16]) {
+  float* As = st;
+  float* Bs = st + F32_GK * F32_PA;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int c = tid + 256 * u;
+    const int kk = c >> 5, mm = (c & 31) * 4;
+    *reinterpret_cast<float4*>(As + kk * F32_PA + mm) = make_float4(ra[4 * u], ra[4 * u + 1], ra[4 * u + 2], ra[4 * u + 3]);
+    const int nn = c >> 3, k2 = (c & 7) * 4;
+    *reinterpret_cast<float4*>(Bs + nn * F32_PB + k2) = make_float4(rb[4 * u], rb[4 * u + 1], rb[4 * u + 2], rb[4 * u + 3]);
+  }
+}
+
+static __global__ void __launch_bounds__(256, 2) k_gemm_f32(const float* A, long long lda, const float* B,
+                                                             long long ldb, float* C, long long ldc, int mt,
+                                                             int K, int kend_ti) {
+  extern __shared__ __attribute__((aligned(16))) float lds32[];
+  const int ti = blockIdx.x % mt, tj = blockIdx.x / mt;
+  const int kend = kend_ti ? min(K, (ti + 1) * TILE) : K;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const float* Ab = A + (long long)ti * TILE;
+  const float* Bb = B + (long long)tj * TILE * ldb;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  const int nk = kend / F32_GK;
+  float ra[16], rb[16];
+  if (nk > 0) {
+    g32_gload(Ab, Bb, lda, ldb, 0, tid, ra, rb);
+    g32_sstore(lds32, tid, ra, rb);
+    __syncthreads();
+  }
+  for (int s = 0; s < nk; ++s) {
+    if (s + 1 < nk) g32_gload(Ab, Bb, lda, ldb, (s + 1) * F32_GK, tid, ra, rb);
+    const float* As = lds32 + (s & 1) * F32_STAGE;
+    const float* Bs = As + F32_GK * F32_PA;
+#pragma unroll
+    for (int ks = 0; ks < F32_GK / 4; ++ks) {
+      const int krow = 4 * ks + (lane >> 4);
+      float af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = As[krow * F32_PA + wm + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = Bs[(wn + j * 16 + (lane & 15)) * F32_PB + krow];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bf[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (s + 1 < nk) g32_sstore(lds32 + ((s + 1) & 1) * F32_STAGE, tid, ra, rb);
+    __syncthreads();
+  }
+  float* Cb = C + (long long)ti * TILE + (long long)tj * TILE * ldc;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = wm + i * 16 + (lane & 15);
+        const int n = wn + j * 16 + 4 * (lane >> 4) + r;
+        Cb[m + (long long)n * ldc] = acc[i][j][r];
+      }
+}
+
+// out (fp32, ld_out) = in (fp64, ld_in) over rows x cols
+static __global__ void __launch_bounds__(256) k_to_f32(const double* in, long long ld_in, float* out,
+                                                        long long ld_out, long long rows, int cols) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= rows * cols) return;
+  const long long i = e % rows, j = e / rows;
+  out[i + j * ld_out] = (float)in[i + j * ld_in];
+}
+
+// out[j] = sum_i V(i, j)^2 over fp32 V, fp64 accumulation (4 columns per block)
+static __global__ void __launch_bounds__(256) k_colnorm2_f32(const float* V, long long ldv, int nrows,
+                                                              int ncols, double* out) {
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (j >= ncols) return;
+  const float* col = V + (long long)j * ldv;
+  double s = 0.0;
+  for (int i = lane; i < nrows; i += 64) {
+    const double v = col[i];
+    s = fma(v, v, s);
+  }
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+  if (lane == 0) out[j] = s;
+}
+
+// ---------------------------------------------------------------------------
 // skinny products with a lower-triangular (or full) tiled matrix M (ld = ldm):
 //   k_trmm_skinny_n : part[ch] = M[rows it, cols k in chunk] x R[k, 0:P]
 //   k_trmm_skinny_t : part[ch] = M[rows k in chunk, cols it]^T x R[k, 0:P]

@@ -39,7 +39,8 @@ SIGNATURES = {
                                   _ct.c_int32, _D, _D, _D]),
     "gpe_factor": (_ct.c_int, [_VP, _ct.c_int32, _D, _ct.c_double, _ct.c_double, _ct.c_double]),
     "gpe_beta": (_ct.c_int, [_VP, _D]),
-    "gpe_posterior": (_ct.c_int, [_VP, _ct.c_int64, _D, _D, _D, _ct.c_double, _ct.c_int32, _D, _D]),
+    "gpe_posterior": (_ct.c_int, [_VP, _ct.c_int64, _D, _D, _D, _ct.c_double, _ct.c_int32, _ct.c_int32,
+                                  _D, _D]),
     "gpe_kernel_var": (_ct.c_int, [_VP, _ct.c_int32, _D, _ct.c_int32, _ct.c_double, _ct.c_int32,
                                    _ct.c_int64, _D, _D, _ct.c_double, _D]),
     "gpe_kernel_covar": (_ct.c_int, [_VP, _ct.c_int32, _D, _ct.c_int32, _ct.c_double, _ct.c_int64,
@@ -221,7 +222,11 @@ class Context:
         self._check(self.lib.gpe_beta(self._h, _ptr(out)), "gpe_beta")
         return out
 
-    def posterior(self, Xs, Hs, beta, sigma, full_var=True):
+    def posterior(self, Xs, Hs, beta, sigma, full_var=True, precision=64):
+        """(mean, var): var is m x m when full_var, else its diagonal.  precision=32
+        runs the L^-1 K* product on fp32 MFMA (diagonal variance only)."""
+        if precision not in (32, 64):
+            raise ValueError("precision must be 32 or 64")
         Xs = _f64(Xs)
         if Xs.ndim == 1:
             Xs = Xs.reshape(-1, 1)
@@ -231,7 +236,7 @@ class Context:
         mean = _np.zeros(m)
         var = _np.zeros((m, m)) if full_var else _np.zeros(m)
         self._check(self.lib.gpe_posterior(self._h, m, _ptr(Xs), _ptr(Hs), _ptr(beta), float(sigma),
-                                           1 if full_var else 0, _ptr(mean), _ptr(var)),
+                                           1 if full_var else 0, int(precision), _ptr(mean), _ptr(var)),
                     "gpe_posterior")
         return mean, var
 

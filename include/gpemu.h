@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GPE_ABI_VERSION 1
+#define GPE_ABI_VERSION 2
 
 enum gpe_status {
     GPE_OK = 0,
@@ -90,9 +90,12 @@ int gpe_beta(gpe_ctx* ctx, double* beta_out);
 /* Posterior at m points: replaces Posterior.make_covar/make_mean/make_var
  * (_emulatorclasses.py:607-631) with the resident factor.  Xs m x d, Hs m x q.
  * mean_out m; var_out m x m when full_var != 0 (m <= 16384), else its diagonal
- * (m values).  sigma is par.sigma. */
+ * (m values), streamed in chunks for any m.  sigma is par.sigma.
+ * precision 64: everything in fp64.  precision 32 (diagonal only; SURVEY 8b/8d,
+ * BASELINE config C5): the dominant product L^-1 K* (n^2 m flops) runs on fp32
+ * MFMA from fp32 copies of L^-1 and K*; the mean and the q x q terms stay fp64. */
 int gpe_posterior(gpe_ctx* ctx, int64_t m, const double* Xs, const double* Hs,
-                  const double* beta, double sigma, int32_t full_var,
+                  const double* beta, double sigma, int32_t full_var, int32_t precision,
                   double* mean_out, double* var_out);
 
 /* K.var(X, predict) materialised (m x m, symmetric): _emulatorkernels.py:39-50 /

@@ -58,3 +58,23 @@ def test_posterior_large_m_chunked(ctx):
     m_ref, v_ref = orc.posterior_ref(X, f, H, A, xs[sel], hs[sel], beta, 0.8, delta, nu, orc.STD)
     assert np.max(np.abs(mean[sel] - m_ref)) < 1e-8
     assert np.max(np.abs(var[sel] - np.diag(v_ref))) < 1e-8
+
+
+def test_posterior_precision32_diagonal(ctx):
+    """precision 32 (config C5): L^-1 K* on fp32 MFMA.  The mean is fp64 and must
+    equal the fp64 path; the diagonal variance sigma^2 (1 - |L^-1 k*|^2 + ...)
+    loses ~fp32 eps * |L^-1 k*|^2 to cancellation, tolerance 2e-5 * sigma^2."""
+    from gp_emu_uqsa_amd import native, synthetic
+    X, f, H = synthetic.problem(2000, 6, seed=3)
+    ctx.set_data(X, f, H)
+    delta = np.full(6, 0.8)
+    ctx.factor(native.KERNEL_STD, delta, 1e-3, 1.0, 0.0)
+    beta = ctx.beta()
+    xs = synthetic.design(10000, 6, seed=9)
+    hs = synthetic.linear_basis(xs)
+    m64, v64 = ctx.posterior(xs, hs, beta, 0.9, full_var=False, precision=64)
+    m32, v32 = ctx.posterior(xs, hs, beta, 0.9, full_var=False, precision=32)
+    assert np.array_equal(m32, m64)
+    assert np.max(np.abs(v32 - v64)) < 2e-5 * 0.81, np.max(np.abs(v32 - v64))
+    with pytest.raises(RuntimeError):
+        ctx.posterior(xs[:10], hs[:10], beta, 0.9, full_var=True, precision=32)
