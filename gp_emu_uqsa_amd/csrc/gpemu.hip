@@ -396,6 +396,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
     p.X = tile(B, t, t);
     p.ldx = ld;
     p.flag = F.flags + t;
+    p.diag_col0 = t * TILE;   // step index for the GEMM_TRACE dev build
     return p;
   };
   // bulk problems: tiles (i, j), i >= j, j in [a, b), updated by columns [g0, g0 + K/128)
@@ -779,6 +780,14 @@ bool create_priority_stream(hipStream_t* st) {
 
 // =====================================================================  C-ABI
 extern "C" {
+
+#ifdef GEMM_TRACE
+// dev build only: copy the fused-Cholesky timeline out (8 slots per column step)
+int gpe_debug_trace(uint64_t* out, int32_t n) {
+  if (n > 8 * 4096) n = 8 * 4096;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gemm_trace), (size_t)n * 8) == hipSuccess ? 0 : -2;
+}
+#endif
 
 int gpe_abi_version(void) { return GPE_ABI_VERSION; }
 

@@ -738,6 +738,17 @@ __device__ __forceinline__ int gemm_wait_flag(const int* flag) {
 
 constexpr int GEMM_WAIT_TIMEOUT = 0x7fffffff;   // info value after a flag wait timed out
 
+// dev-tool timeline of the fused Cholesky (-DGEMM_TRACE build only): per column
+// step t, slots [t*8 + 0..3] = diagonal workgroup start / update done / factor
+// done / flag published, [t*8 + 4..7] = first panel workgroup start / update done /
+// flag seen / multiply done (wall_clock64, 100 MHz).
+#ifdef GEMM_TRACE
+__device__ unsigned long long gemm_trace[8 * 4096];
+#define GTRACE(P, slot) do { if (threadIdx.x == 0 && (P).flag) gemm_trace[(P).diag_col0 / TILE * 8 + (slot)] = wall_clock64(); } while (0)
+#else
+#define GTRACE(P, slot) do {} while (0)
+#endif
+
 template <bool AK, bool BK>
 static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restrict__ probs, int nprob,
                                                   const unsigned* __restrict__ tiles,
@@ -764,6 +775,8 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  if (P.flags & G_DIAG) GTRACE(P, 0);
+  if ((P.flags & G_PANEL) && ti == 0) GTRACE(P, 4);
 
   const double* Ab = AK ? P.A + (long long)ti * TILE * P.lda : P.A + (long long)ti * TILE;
   const double* Bb = BK ? P.B + (long long)tj * TILE * P.ldb : P.B + (long long)tj * TILE;
@@ -797,6 +810,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
 
   if constexpr (!AK && !BK) {
     if (P.flags & G_DIAG) {
+      GTRACE(P, 1);
       // updated diagonal tile -> block-packed LDS (lower half), then factor + invert;
       // then release the panel workgroups of this launch waiting on *P.flag
 #pragma unroll
@@ -811,17 +825,20 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
           }
       __syncthreads();
       const int bad = db_factor_invert(lds, Cb, P.ldc, P.X, P.ldx, P.logdet);
+      GTRACE(P, 2);
       if (bad && tid == 0 && abort_flag) atomicCAS(abort_flag, 0, P.diag_col0 + bad);
       if (P.flag) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's L / X stores done
         __syncthreads();
         if (tid == 0) gemm_publish_flag(P.flag, bad ? 2 : 1);
       }
+      GTRACE(P, 3);
       return;
     }
     if (P.flags & G_PANEL) {
       // updated panel tile -> C; wait for the diagonal inverse X of this launch;
       // then L = C X^T over the same tile
+      if (ti == 0) GTRACE(P, 5);
       gemm_store(Cb, P.ldc, P.alpha, acc);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       int* ready = reinterpret_cast<int*>(lds + G_LDS_LAUNCH_DOUBLES - 1);   // staging is idle here
@@ -829,6 +846,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
       __syncthreads();
       const int st = *ready;
       __syncthreads();
+      if (ti == 0) GTRACE(P, 6);
       if (st != 1) {
         if (st == 0 && tid == 0 && abort_flag) atomicCAS(abort_flag, 0, GEMM_WAIT_TIMEOUT);
         return;
@@ -839,6 +857,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
         for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
       gemm_kloop<false, false>(Cb, P.X, P.ldc, P.ldx, 0, TILE / GK, lds, acc);
       gemm_store(Cb, P.ldc, 1.0, acc);
+      if (ti == 0) GTRACE(P, 7);
       return;
     }
   }
