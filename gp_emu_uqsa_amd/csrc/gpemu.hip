@@ -146,6 +146,7 @@ struct gpe_ctx {
   // look-ahead stream and events
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_host = nullptr;   // host-visible results of the value part are in hpin
   std::vector<hipEvent_t> ev_panel, ev_rest;
 
   // profiling
@@ -728,6 +729,21 @@ int gram(gpe_ctx* c, const double* Z, long long ldz, int P, int nrows, double* h
   return GPE_OK;
 }
 
+// Gram of Z (P x P) into hpin[0, P*P) without waiting; the caller syncs on an event
+int gram_async(gpe_ctx* c, const double* Z, long long ldz, int P, int nrows) {
+  const int nblk = (nrows + 255) / 256;
+  const size_t need = (size_t)nblk * P * P;
+  CHK(ensure_small(c, need + P * P));
+  hipLaunchKernelGGL(k_gram, dim3(nblk), dim3(256), 0, c->stream, Z, ldz, P, nrows, c->dsmall, c->dinfo);
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(k_reduce_rows, dim3(P * P), dim3(256), 0, c->stream, c->dsmall, nblk, P * P,
+                     c->dgram);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->hpin, c->dgram, (size_t)P * P * sizeof(double), hipMemcpyDeviceToHost,
+                           c->stream));
+  return GPE_OK;
+}
+
 int read_info_logdet(gpe_ctx* c, const Fact& F, int* info, double* logdetA) {
   CHK(ensure_pinned(c, (size_t)F.NB + 8));
   HIPCHK(c, hipMemcpyAsync(c->hpin, F.logdet, F.NB * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -837,7 +853,8 @@ gpe_ctx* gpe_create(int32_t device) {
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       !create_priority_stream(&c->stream2) ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_host, hipEventDisableTiming) != hipSuccess) {
     g_create_error = "failed to initialise device/stream";
     delete c;
     return nullptr;
@@ -888,6 +905,7 @@ void gpe_destroy(gpe_ctx* c) {
   for (auto& e : c->ev_rest) (void)hipEventDestroy(e);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->ev_host) (void)hipEventDestroy(c->ev_host);
   if (c->stream2) {
     (void)hipStreamSynchronize(c->stream2);
     (void)hipStreamDestroy(c->stream2);
@@ -995,12 +1013,27 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
   // z, w = L^-1 [f H]
   const int P = q + 1;
   const long long np = c->n_pad;
+  const int NBt = c->tr.NB;
   CHK(skinny(c, false, c->tr.B, np, c->NB, c->NB, true, c->dF, np, P, c->dZ, np));
-  std::vector<double> G((size_t)P * P);
-  CHK(gram(c, c->dZ, np, P, (int)np, G.data()));
+  // Gram, log-determinant parts and the failure flag go to the host behind an event;
+  // A^-1 = L^-T L^-1 (22 ms at n=16384, independent of the host algebra) is queued
+  // before the host waits, so the GPU does not idle over the round trip
+  CHK(ensure_pinned(c, (size_t)P * P + NBt + 64));
+  CHK(gram_async(c, c->dZ, np, P, (int)np));
+  HIPCHK(c, hipMemcpyAsync(c->hpin + P * P, c->tr.logdet, NBt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->hpin + P * P + NBt, c->dinfo, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev_host, c->stream));
+  ev_rec(c, 4);
+  if (want_grad) CHK(launch_gemm_range(c, c->tr.plan.launches[c->tr.plan.lauum]));
+  ev_rec(c, 5);
+  HIPCHK(c, hipEventSynchronize(c->ev_host));
+  std::vector<double> G(c->hpin, c->hpin + (size_t)P * P);
   int info = 0;
+  std::memcpy(&info, c->hpin + P * P + NBt, sizeof(int));
+  if (info == GEMM_WAIT_TIMEOUT) return fail(c, GPE_ERR_HIP, "internal error: Cholesky panel wait timed out");
   double logdetA = 0.0;
-  CHK(read_info_logdet(c, c->tr, &info, &logdetA));
+  for (int k = 0; k < NBt; ++k) logdetA += c->hpin[P * P + k];
+  logdetA *= 2.0;
   if (info != 0) {
     c->err = "matrix not positive definite (pivot " + std::to_string(info) + ")";
     return GPE_NOT_PD;
@@ -1026,17 +1059,11 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
   *llh_out = llh;
   if (sigma2_out) *sigma2_out = sig2;
   if (!want_grad) {
-    ev_rec(c, 4);
-    ev_rec(c, 5);
     ev_rec(c, 6);
     ev_rec(c, 7);
     goto done;
   }
   {
-    ev_rec(c, 4);
-    // A^-1 = L^-T L^-1 over L in dA
-    CHK(launch_gemm_range(c, c->tr.plan.launches[c->tr.plan.lauum]));
-    ev_rec(c, 5);
     // R2 = [sqrt(c)(z - w B), w Kq^-T] ; [sqrt(c) alpha, W] = L^-T R2
     std::vector<double> Kinv = small_trinv(sa.Kq, q);  // row-major
     CHK(ensure_pinned(c, (size_t)P * P + 8));
