@@ -10,6 +10,7 @@ Fixtures:
   G4 train_*.npz       seeded toy-sim g.train() trajectory (objective x's, result)
   G5 scale_4096.npz    n=4096 d=10 gp4ml LLH+grad (X regenerated from the seed)
   G6 host_*.npz        host-side setup() state: shuffle, T/V split, H, bounds, RNG
+  G7 history_match.npz imp_plot IMP/ODP grids + oLHC designs, nonimp_data, new_wave_design
 Versions of numpy/scipy used are stored in every file ("meta").
 """
 from __future__ import annotations
@@ -282,9 +283,63 @@ def make_g5():
          grad=res[1], seconds=np.array(dt))
 
 
+# ---------------------------------------------------------------- G7
+def make_g7():
+    """History matching on the reconstructed toysim3D emulators:
+    imp_plot (grid 4, olhcmult 20, maxno 2), nonimp_data and new_wave_design with
+    fixed seeds.  design_inputs.py:55 uses np.int, removed in NumPy 1.24: the alias
+    is restored for this run (the reference's algorithm is unchanged)."""
+    np.int = int
+    with contextlib.redirect_stdout(io.StringIO()):
+        import gp_emu_uqsa.history_match as hm
+    tmp = tempfile.mkdtemp()
+    shutil.copytree(os.path.join(REF, "examples/sensitivity_multi_outputs/sensitivity_recon"),
+                    os.path.join(tmp, "w"))
+    cwd = os.getcwd()
+    os.chdir(os.path.join(tmp, "w"))
+    try:
+        # the example's final beliefs predate the 'active_index' line that the reference's
+        # final_beliefs writes (_emulatorclasses.py:233) and that emulsetup needs
+        for i in range(2):
+            with open(f"toysim3D_beliefs{i}-1f", "a") as fh:
+                fh.write("active_index 0 1 2\n")
+        emuls = [quiet(g.setup, f"toysim3D_config{i}_recon", datashuffle=False, scaleinputs=True)
+                 for i in range(2)]
+        ys = [np.loadtxt(f"toysim3D_output-o{i}-1f") for i in range(2)]
+        zs = [float(np.median(y)) for y in ys]
+        ve = [float(0.05 * np.var(y)) for y in ys]
+        out = {"zs": np.array(zs), "var_extra": np.array(ve), "cm": np.array(3.0)}
+        np.random.seed(21)
+        quiet(hm.imp_plot, emuls, zs, 3.0, ve, maxno=2, olhcmult=20, grid=4, plot=False)
+        for s in ([0, 1], [0, 2], [1, 2]):
+            tag = f"{s[0]}_{s[1]}"
+            out["design_" + tag] = np.loadtxt("imp_input_" + tag)
+            for m in (1, 2):
+                out[f"IMP{m}_" + tag] = np.loadtxt(f"{m}_IMP_" + tag)
+                out[f"ODP{m}_" + tag] = np.loadtxt(f"{m}_ODP_" + tag)
+        # the example's simulator data (original units, two output columns)
+        for f in ("toysim3D_input", "toysim3D_output"):
+            shutil.copy(os.path.join(REF, "examples/sensitivity_multi_outputs", f), f)
+        din, dout = "toysim3D_input", "toysim3D_output"
+        out["data_in"] = np.loadtxt(din)
+        out["data_out"] = np.loadtxt(dout)
+        out["nonimp_count"] = np.array(quiet(hm.nonimp_data, emuls, zs, 3.0, ve, [din, dout], maxno=1))
+        out["nonimp_in"] = np.loadtxt("nonimp_" + din)
+        out["nonimp_out"] = np.loadtxt("noninp_" + dout)
+        np.random.seed(22)
+        out["wave_count"] = np.array(quiet(hm.new_wave_design, emuls, zs, 3.0, ve,
+                                           ["nonimp_" + din, "noninp_" + dout], maxno=1, olhcmult=10))
+        out["wave_design"] = np.loadtxt("nonimp_" + din)
+        out["wave_olhc"] = np.loadtxt("olhc_des")
+        save("history_match.npz", **out)
+    finally:
+        os.chdir(cwd)
+        shutil.rmtree(tmp)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["G1", "G2", "G3", "G4", "G5", "G6"]
+    which = sys.argv[1:] or ["G1", "G2", "G3", "G4", "G5", "G6", "G7"]
     for w in which:
         print("==", w)
         {"G1": make_g1, "G2": make_g2, "G3": make_g3, "G4": make_g4, "G5": make_g5,
-         "G6": make_g6}[w]()
+         "G6": make_g6, "G7": make_g7}[w]()
