@@ -1065,14 +1065,8 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
   }
   {
     // R2 = [sqrt(c)(z - w B), w Kq^-T] ; [sqrt(c) alpha, W] = L^-T R2
-    std::vector<double> Kinv = small_trinv(sa.Kq, q);  // row-major
     CHK(ensure_pinned(c, (size_t)P * P + 8));
-    std::vector<double> T2((size_t)P * P, 0.0);    // column-major P x P
-    const double sc = std::sqrt(cfac);
-    T2[0] = sc;
-    for (int i = 0; i < q; ++i) T2[(i + 1) + 0 * P] = -sc * sa.beta[i];
-    for (int o = 0; o < q; ++o)
-      for (int i = 0; i < q; ++i) T2[(i + 1) + (o + 1) * P] = Kinv[o * q + i];  // (Kq^-T)(i,o) = Kinv(o,i)
+    const std::vector<double> T2 = small_t2(sa, q, cfac);
     std::memcpy(c->hpin, T2.data(), T2.size() * sizeof(double));
     HIPCHK(c, hipMemcpyAsync(c->dT2, c->hpin, T2.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
     hipLaunchKernelGGL(k_apply_small, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, c->stream,
@@ -1101,14 +1095,8 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
     const double* red = c->hpin;
     double coff, cdiag;
     kernel_consts(kernel, nu, true, &coff, &cdiag);
-    const double pref = (kernel == GPE_KERNEL_ALT_NUG) ? 1.0 : (1.0 - nu);
-    const double SE = 2.0 * red[d], Tr = red[d + 1];
-    for (int k = 0; k < d; ++k) grad_out[k] = 0.5 * gscale * pref * 2.0 * red[k];
-    if (fitnug) {
-      grad_out[d] = (kernel == GPE_KERNEL_ALT_NUG) ? 0.5 * gscale * nu * nu * Tr
-                                                   : 0.5 * gscale * (-0.5 * nu) * SE;
-    }
-    if (gp4ml) grad_out[n_hp - 1] = 0.5 * s2 * (coff * SE + cdiag * Tr);
+    small_grad(red, d, kernel == GPE_KERNEL_ALT_NUG, nu, fitnug, gp4ml, gscale, s2, coff, cdiag, n_hp,
+               grad_out);
   }
 done:
   if (c->prof) {

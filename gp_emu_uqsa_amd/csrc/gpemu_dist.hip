@@ -1,4 +1,4 @@
-// gpemu_dist.hip -- row-block distributed value objective over RCCL (include/gpemu_dist.h).
+// gpemu_dist.hip -- row-block distributed objective over RCCL (include/gpemu_dist.h).
 //
 // Partition: 128-row tile rows dealt cyclically, tile row t on rank t mod P (the
 // trailing matrix shrinks evenly on every rank); rank r stores its tile rows of
@@ -12,6 +12,16 @@
 //   panel:   L(i,k) = A(i,k) Dinv^T for its rows i > k      (k_gemm)
 //   pack its panel tiles, RCCL all-gather, unpermute into the panel column
 //   update:  A(i,j) -= L(i,k) L(j,k)^T, its rows i > k, k < j <= i (k_gemm, tile list)
+//
+// Gradient (want_grad), same partition, no n x n collective:
+//   X = L^-1 by rows, right-looking: step k, owner(k) finishes its row
+//     X(k, 0:k) = Dinv_k R(k, 0:k)  (X(k,k) = Dinv_k kept from the sweep),
+//     RCCL broadcasts X(k, 0:k+1), every rank updates its rows i > k:
+//     R(i, 0:k+1) -= L(i,k) X(k, 0:k+1)                      (k_gemm)
+//   A^-1 = X^T X = sum_r X_r^T X_r over each rank's rows: rank r forms its partial
+//   P_r (lower tiles, K = its rows) and W_r = X_r^T R2_r; W is all-reduced (n x (q+1))
+//   the contraction <M, dA/dtheta> is linear in A^-1, so each rank contracts its own
+//   P_r (rank 0 also carries the -W W^T term) and only d+2 sums are all-reduced.
 // Loopback transport: all P ranks in this process on one GPU (separate local
 // buffers, one shared Dinv and panel column), copies instead of RCCL.
 #include <hip/hip_runtime.h>
@@ -137,16 +147,38 @@ __global__ void __launch_bounds__(256) k_dist_to_panel(const double* Aloc, long 
   }
 }
 
+// Z = L^-1 [f H] (n_pad x Pc, column-major) out of the augmented tile row (local row li)
+__global__ void __launch_bounds__(256) k_dist_take_z(const double* Aloc, long long ld, int li, long long np,
+                                                     int Pc, double* Z) {
+  const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (j >= np) return;
+  const double* src = Aloc + (long long)li * TILE + j * ld;
+  for (int p = 0; p < Pc; ++p) Z[j + p * np] = src[p];
+}
+
+// rows of R2 (n_pad x Pc) at rank `rank`'s tile rows -> out (local rows, ld ldo)
+__global__ void __launch_bounds__(256) k_dist_rows(const double* R2, long long ldr, int Pc, int P, int rank,
+                                                   int nlx, double* out, long long ldo) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long long)nlx * TILE) return;
+  const int li = (int)(e / TILE), rr = (int)(e % TILE);
+  const long long g = (long long)(li * P + rank) * TILE + rr;
+  for (int p = 0; p < Pc; ++p) out[e + p * ldo] = R2[g + p * ldr];
+}
+
 struct Rank {              // one rank's stored tile rows
   int rank = 0, nloc = 0;
   long long ld = 0;
   double* A = nullptr;     // nloc*128 x (NB+1)*128, column-major
   double* logdet = nullptr;
+  int nlx = 0;             // tile rows of the matrix proper (without the [f H] row)
+  double* X = nullptr;     // L^-1 rows, ld as A, NB*128 columns (gradient only)
 };
 
 struct DLaunch {           // one grouped k_gemm launch
   int first = 0, count = 0, tiles = 0;
   long long list = -1;
+  int kind = 0;            // 0 <false,false>, 1 <false,true>, 2 <true,true>
 };
 
 constexpr int DIST_DESC_MAX = 1 << 20;
@@ -190,6 +222,21 @@ struct gpe_dist {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   std::vector<hipEvent_t> cev;
   double total_ms = 0.0, comm_ms = 0.0;
+
+  // gradient (allocated on the first want_grad call after gpe_dist_set_data)
+  bool grad_ready = false, grad_now = false;
+  double* xrow = nullptr;    // 128 x n_pad: X(k, 0:k+1), broadcast per step
+  double* dZ = nullptr;      // n_pad x Pc: L^-1 [f H]
+  double* dR2 = nullptr;     // n_pad x Pc
+  double* r2loc = nullptr;   // local rows of R2, 128 columns (zero beyond Pc)
+  double* wpart = nullptr;   // n_pad x 128: [sqrt(c) alpha, W] (sum over ranks)
+  double* pbuf = nullptr;    // n_pad x n_pad: this rank's partial of A^-1 (lower tiles)
+  double* dT2 = nullptr;
+  double* cpart = nullptr;   // contraction partials
+  double* csum = nullptr;    // d+2 per local rank
+  GemmProb* gprobs = nullptr;
+  std::vector<DLaunch> tri_x, tri_u, wa_l, lau_l;
+  double grad_ms = 0.0;
 };
 
 namespace {
@@ -339,13 +386,140 @@ int build_schedule(gpe_dist* h) {
   return GPE_OK;
 }
 
-int launch(gpe_dist* h, const DLaunch& L) {
+int launch(gpe_dist* h, const DLaunch& L, const GemmProb* base = nullptr) {
   if (L.count == 0 || L.tiles == 0) return GPE_OK;
   const size_t lds = G_LDS_LAUNCH_DOUBLES * sizeof(double);
   const unsigned* tl = L.list >= 0 ? h->dtiles + L.list : nullptr;
-  hipLaunchKernelGGL((k_gemm<false, false>), dim3(L.tiles), dim3(256), lds, h->stream, h->dprobs + L.first,
-                     L.count, tl, h->dinfo);
+  const GemmProb* pr = (base ? base : h->dprobs) + L.first;
+  const dim3 g(L.tiles);
+  switch (L.kind) {
+    case 1: hipLaunchKernelGGL((k_gemm<false, true>), g, dim3(256), lds, h->stream, pr, L.count, tl, h->dinfo); break;
+    case 2: hipLaunchKernelGGL((k_gemm<true, true>), g, dim3(256), lds, h->stream, pr, L.count, tl, h->dinfo); break;
+    default: hipLaunchKernelGGL((k_gemm<false, false>), g, dim3(256), lds, h->stream, pr, L.count, tl, h->dinfo); break;
+  }
   DCHK_HIP(h, hipGetLastError());
+  return GPE_OK;
+}
+
+// first local tile row of rank r whose global row is >= a
+int lstart_of(int a, int P, int r) { return a <= r ? 0 : (a - r + P - 1) / P; }
+
+// gradient buffers and GEMM descriptors (TRTRI steps, W partial, A^-1 partial)
+int ensure_grad(gpe_dist* h) {
+  if (h->grad_ready) return GPE_OK;
+  const int NB = h->NB, P = h->P, Pc = h->q + 1, d = h->d;
+  const long long np = h->n_pad;
+  long long maxld = TILE;
+  for (Rank& R : h->ranks) {
+    R.nlx = R.rank <= NB - 1 ? (NB - 1 - R.rank) / P + 1 : 0;
+    DCHK(dalloc(h, &R.X, (size_t)R.ld * NB * TILE));
+    maxld = std::max(maxld, R.ld);
+  }
+  DCHK(dalloc(h, &h->xrow, (size_t)TILE * np));
+  DCHK(dalloc(h, &h->dZ, (size_t)np * Pc));
+  DCHK(dalloc(h, &h->dR2, (size_t)np * Pc));
+  DCHK(dalloc(h, &h->r2loc, (size_t)maxld * TILE));
+  DCHK_HIP(h, hipMemset(h->r2loc, 0, (size_t)maxld * TILE * sizeof(double)));
+  DCHK(dalloc(h, &h->wpart, (size_t)np * TILE));
+  DCHK(dalloc(h, &h->pbuf, (size_t)np * np));
+  DCHK(dalloc(h, &h->dT2, (size_t)Pc * Pc));
+  DCHK(dalloc(h, &h->cpart, (size_t)NB * (NB + 1) / 2 * (d + 2)));
+  DCHK(dalloc(h, &h->csum, h->ranks.size() * (size_t)(d + 2)));
+
+  std::vector<GemmProb> probs;
+  h->tri_x.assign(NB, DLaunch());
+  h->tri_u.assign(NB, DLaunch());
+  for (int k = 0; k < NB; ++k) {
+    const int owner = k % P, lk = k / P;
+    for (Rank& R : h->ranks) {
+      if (R.rank != owner || k == 0) continue;
+      // X(k, 0:k) = Dinv_k R(k, 0:k) with R(k, c) = -sum_{j<k} L(k,j) X(j,c), in place
+      // (each output tile reads only itself)
+      double* row = R.X + (long long)lk * TILE;
+      GemmProb p = dprob(row + (long long)k * TILE * R.ld, R.ld, row, R.ld, row, R.ld, 1, k, TILE, 0, 1.0, 0.0);
+      p.ntiles = k;
+      DLaunch L;
+      L.first = (int)probs.size(); L.count = 1; L.tiles = k; L.kind = 1;
+      h->tri_x[k] = L;
+      probs.push_back(p);
+    }
+    DLaunch ul;
+    ul.first = (int)probs.size();
+    ul.kind = 1;
+    for (Rank& R : h->ranks) {
+      const int a = li0_of(k, P, R.rank), c = R.nlx - a;
+      if (c <= 0) continue;
+      // R(i, 0:k+1) -= L(i,k) X(k, 0:k+1) over its rows i > k
+      GemmProb p = dprob(R.A + (long long)a * TILE + (long long)k * TILE * R.ld, R.ld, h->xrow, TILE,
+                         R.X + (long long)a * TILE, R.ld, c, k + 1, TILE, 0, -1.0, 1.0);
+      p.tile_begin = ul.tiles;
+      p.ntiles = c * (k + 1);
+      ul.tiles += p.ntiles;
+      probs.push_back(p);
+      ++ul.count;
+    }
+    h->tri_u[k] = ul;
+  }
+  h->wa_l.assign(h->ranks.size(), DLaunch());
+  h->lau_l.assign(h->ranks.size(), DLaunch());
+  for (size_t s = 0; s < h->ranks.size(); ++s) {
+    Rank& R = h->ranks[s];
+    DLaunch wl, ll;
+    wl.kind = ll.kind = 2;
+    wl.first = (int)probs.size();
+    for (int a = 0; a < NB; ++a) {
+      const int ls = lstart_of(a, P, R.rank), K = (R.nlx - ls) * TILE;
+      if (K <= 0) continue;
+      // W(a) += X_r(:, a)^T R2_r over its rows >= a
+      GemmProb p = dprob(R.X + (long long)ls * TILE + (long long)a * TILE * R.ld, R.ld,
+                         h->r2loc + (long long)ls * TILE, R.ld, h->wpart + (long long)a * TILE, np,
+                         1, 1, K, 0, 1.0, 1.0);
+      p.tile_begin = wl.tiles;
+      p.ntiles = 1;
+      ++wl.tiles;
+      ++wl.count;
+      probs.push_back(p);
+    }
+    ll.first = (int)probs.size();
+    for (int a = 0; a < NB; ++a) {
+      const int ls = lstart_of(a, P, R.rank), K = std::max(0, (R.nlx - ls) * TILE);
+      // P_r(a, 0:a+1) = X_r(:, a)^T X_r(:, 0:a+1) over its rows >= a (K = 0 writes zeros)
+      GemmProb p = dprob(R.X + (long long)ls * TILE + (long long)a * TILE * R.ld, R.ld,
+                         R.X + (long long)ls * TILE, R.ld, h->pbuf + (long long)a * TILE, np,
+                         1, a + 1, K, 0, 1.0, 0.0);
+      p.tile_begin = ll.tiles;
+      p.ntiles = a + 1;
+      ll.tiles += a + 1;
+      ++ll.count;
+      probs.push_back(p);
+    }
+    h->wa_l[s] = wl;
+    h->lau_l[s] = ll;
+  }
+  if ((int)probs.size() > DIST_DESC_MAX) return dfail(h, GPE_ERR_UNSUPPORTED, "distributed gradient schedule too large");
+  DCHK(dalloc(h, &h->gprobs, probs.size()));
+  DCHK_HIP(h, hipMemcpy(h->gprobs, probs.data(), probs.size() * sizeof(GemmProb), hipMemcpyHostToDevice));
+  h->grad_ready = true;
+  return GPE_OK;
+}
+
+// TRTRI step k: owner finishes X(k, :), broadcast, every rank updates its rows > k
+int trtri_step(gpe_dist* h, int k, int& ev) {
+  const int P = h->P, owner = k % P, lk = k / P;
+  DCHK(launch(h, h->tri_x[k], h->gprobs));
+  if (k == h->NB - 1) return GPE_OK;   // no rows below
+  for (Rank& R : h->ranks) {
+    if (R.rank != owner) continue;
+    DCHK_HIP(h, hipMemcpy2DAsync(h->xrow, TILE * sizeof(double), R.X + (long long)lk * TILE, R.ld * sizeof(double),
+                                 TILE * sizeof(double), (size_t)(k + 1) * TILE, hipMemcpyDeviceToDevice, h->stream));
+  }
+  if (!h->loop) {
+    DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
+    DCHK_NCCL(h, ncclBroadcast(h->xrow, h->xrow, (size_t)(k + 1) * TILE * TILE, ncclDouble, owner, h->comm,
+                               h->stream));
+    DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
+  }
+  DCHK(launch(h, h->tri_u[k], h->gprobs));
   return GPE_OK;
 }
 
@@ -383,6 +557,14 @@ int step(gpe_dist* h, int k, int& ev) {
     DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
     DCHK_NCCL(h, ncclBroadcast(h->dinv, h->dinv, (size_t)TILE * TILE, ncclDouble, owner, h->comm, h->stream));
     DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
+  }
+  if (h->grad_now) {
+    for (Rank& R : h->ranks) {
+      if (R.rank != owner) continue;
+      DCHK_HIP(h, hipMemcpy2DAsync(R.X + (long long)(k / P) * TILE + (long long)k * TILE * R.ld,
+                                   R.ld * sizeof(double), h->dinv, TILE * sizeof(double), TILE * sizeof(double),
+                                   TILE, hipMemcpyDeviceToDevice, h->stream));
+    }
   }
   DCHK(launch(h, h->panel_l[k]));
   const long long ldp = (long long)(h->NB + 1) * TILE;
@@ -484,8 +666,11 @@ void gpe_dist_destroy(gpe_dist* h) {
   for (Rank& R : h->ranks) {
     if (R.A) (void)hipFree(R.A);
     if (R.logdet) (void)hipFree(R.logdet);
+    if (R.X) (void)hipFree(R.X);
   }
-  double* bufs[] = {h->dX, h->dXw, h->dF, h->dr, h->dinvdelta, h->dinv, h->panel, h->recv, h->gram};
+  double* bufs[] = {h->dX,    h->dXw,   h->dF,   h->dr,    h->dinvdelta, h->dinv, h->panel,
+                    h->recv,  h->gram,  h->xrow, h->dZ,    h->dR2,       h->r2loc, h->wpart,
+                    h->pbuf,  h->dT2,   h->cpart, h->csum};
   for (double* b : bufs)
     if (b) (void)hipFree(b);
   if (h->dinfo) (void)hipFree(h->dinfo);
@@ -493,6 +678,7 @@ void gpe_dist_destroy(gpe_dist* h) {
   if (h->dcnt) (void)hipFree(h->dcnt);
   if (h->dprobs) (void)hipFree(h->dprobs);
   if (h->dtiles) (void)hipFree(h->dtiles);
+  if (h->gprobs) (void)hipFree(h->gprobs);
   if (h->hpin) (void)hipHostFree(h->hpin);
   for (hipEvent_t e : h->cev) (void)hipEventDestroy(e);
   if (h->e0) (void)hipEventDestroy(h->e0);
@@ -544,8 +730,10 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
   for (Rank& R : h->ranks) {
     if (R.A) (void)hipFree(R.A);
     if (R.logdet) (void)hipFree(R.logdet);
+    if (R.X) (void)hipFree(R.X);
   }
   h->ranks.clear();
+  h->grad_ready = false;
   for (int rr = 0; rr < h->P; ++rr) {
     if (!h->loop && rr != h->rank) continue;
     Rank R;
@@ -564,19 +752,22 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
   }
   DCHK(dalloc(h, &h->gram, (size_t)Pc * Pc));
   DCHK(build_schedule(h));
-  DCHK(ensure_events(h, (size_t)4 * h->NB + 8));
+  DCHK(ensure_events(h, (size_t)6 * h->NB + 16));
   return GPE_OK;
 }
 
 int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const double* hp, int32_t n_hp,
-                       double nu_fixed, double* llh_out, double* sigma2_out) {
+                       double nu_fixed, int32_t want_grad, double* llh_out, double* grad_out,
+                       double* sigma2_out) {
   if (!h) return GPE_ERR_ARG;
   if (h->n <= 0) return dfail(h, GPE_ERR_STATE, "gpe_dist_set_data has not been called");
   if (!hp || !llh_out) return dfail(h, GPE_ERR_ARG, "null argument");
+  if (want_grad && !grad_out) return dfail(h, GPE_ERR_ARG, "grad_out is NULL");
   if (variant != GPE_GP4ML && variant != GPE_MUCM) return dfail(h, GPE_ERR_ARG, "bad variant");
   if (kernel != GPE_KERNEL_STD && kernel != GPE_KERNEL_ALT_NUG) return dfail(h, GPE_ERR_ARG, "bad kernel");
   DCHK_HIP(h, hipSetDevice(h->device));
   const int d = h->d, q = h->q, Pc = q + 1, P = h->P, NB = h->NB;
+  const long long np = h->n_pad;
   const bool gp4ml = variant == GPE_GP4ML;
   const int base = gp4ml ? d + 1 : d;
   if (n_hp != base && n_hp != base + 1) return dfail(h, GPE_ERR_ARG, "n_hp inconsistent with d");
@@ -585,8 +776,11 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
   const double sigma = gp4ml ? hp[n_hp - 1] : 1.0;
   const double s2 = gp4ml ? sigma * sigma : 1.0;
   const double rscale = (gp4ml && kernel == GPE_KERNEL_ALT_NUG) ? 1.0 : 0.0;
+  if (want_grad) DCHK(ensure_grad(h));
+  h->grad_now = want_grad != 0;
+  const size_t nslot = h->ranks.size();
 
-  DCHK(pinned(h, (size_t)(NB + 1) * 2 + (size_t)Pc * Pc + 64));
+  DCHK(pinned(h, nslot * (NB + 1) + (size_t)Pc * Pc + nslot * (d + 2) + 64));
   for (int k = 0; k < d; ++k) {
     if (!(hp[k] > 0.0) && !(hp[k] < 0.0)) return dfail(h, GPE_ERR_ARG, "delta must be non-zero");
     h->hpin[k] = 1.0 / hp[k];
@@ -594,48 +788,161 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
   DCHK_HIP(h, hipEventRecord(h->e0, h->stream));
   DCHK_HIP(h, hipMemcpyAsync(h->dinvdelta, h->hpin, d * sizeof(double), hipMemcpyHostToDevice, h->stream));
   DCHK_HIP(h, hipMemsetAsync(h->dinfo, 0, sizeof(int), h->stream));
-  const long long tot = h->n_pad * d;
+  const long long tot = np * d;
   hipLaunchKernelGGL(k_scale_points, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, h->dX,
-                     h->dinvdelta, d, (int)h->n, (int)h->n_pad, h->dXw);
+                     h->dinvdelta, d, (int)h->n, (int)np, h->dXw);
   DCHK_HIP(h, hipGetLastError());
-  for (Rank& R : h->ranks)
+  for (Rank& R : h->ranks) {
     DCHK_HIP(h, hipMemsetAsync(R.logdet, 0, (size_t)(NB + 1) * sizeof(double), h->stream));
+    if (h->grad_now && R.nlx > 0)
+      DCHK_HIP(h, hipMemsetAsync(R.X, 0, (size_t)R.ld * NB * TILE * sizeof(double), h->stream));
+  }
   DCHK(kbuild(h, kernel, nu, s2, rscale));
   int ev = 0;
   for (int k = 0; k < NB; ++k) DCHK(step(h, k, ev));
 
-  // Gram of L^-1 [f H] = -(tile (NB, NB)), from the owner of tile row NB
+  // Gram of L^-1 [f H] = -(tile (NB, NB)), and Z = L^-1 [f H], from the owner of tile row NB
   const int ra = NB % P;
   for (Rank& R : h->ranks) {
     if (R.rank != ra) continue;
     const double* t = R.A + (long long)(NB / P) * TILE + (long long)NB * TILE * R.ld;
     DCHK_HIP(h, hipMemcpy2DAsync(h->gram, Pc * sizeof(double), t, R.ld * sizeof(double), Pc * sizeof(double),
                                  Pc, hipMemcpyDeviceToDevice, h->stream));
-  }
-  std::vector<double> ld_sum((size_t)NB + 1, 0.0);
-  int info = 0;
-  if (h->loop) {
-    DCHK_HIP(h, hipEventRecord(h->e1, h->stream));
-    for (Rank& R : h->ranks) {
-      DCHK_HIP(h, hipMemcpyAsync(h->hpin, R.logdet, (NB + 1) * sizeof(double), hipMemcpyDeviceToHost, h->stream));
-      DCHK_HIP(h, hipStreamSynchronize(h->stream));
-      for (int k = 0; k <= NB; ++k)
-        if (k % P == R.rank) ld_sum[k] = h->hpin[k];
+    if (h->grad_now) {
+      hipLaunchKernelGGL(k_dist_take_z, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, h->stream, R.A, R.ld,
+                         NB / P, np, Pc, h->dZ);
+      DCHK_HIP(h, hipGetLastError());
     }
-  } else {
+  }
+  if (!h->loop) {
     const Rank& R = h->ranks[0];
     DCHK_NCCL(h, ncclBroadcast(h->gram, h->gram, (size_t)Pc * Pc, ncclDouble, ra, h->comm, h->stream));
     DCHK_NCCL(h, ncclAllReduce(R.logdet, R.logdet, (size_t)NB + 1, ncclDouble, ncclSum, h->comm, h->stream));
     DCHK_NCCL(h, ncclAllReduce(h->dinfo, h->dinfo, 1, ncclInt32, ncclMax, h->comm, h->stream));
-    DCHK_HIP(h, hipEventRecord(h->e1, h->stream));
-    DCHK_HIP(h, hipMemcpyAsync(h->hpin, R.logdet, (NB + 1) * sizeof(double), hipMemcpyDeviceToHost, h->stream));
-    DCHK_HIP(h, hipStreamSynchronize(h->stream));
-    for (int k = 0; k <= NB; ++k) ld_sum[k] = h->hpin[k];
+    if (h->grad_now) DCHK_NCCL(h, ncclBroadcast(h->dZ, h->dZ, (size_t)np * Pc, ncclDouble, ra, h->comm, h->stream));
   }
-  DCHK_HIP(h, hipMemcpyAsync(h->hpin, h->gram, (size_t)Pc * Pc * sizeof(double), hipMemcpyDeviceToHost, h->stream));
-  DCHK_HIP(h, hipMemcpyAsync(h->hpin + Pc * Pc, h->dinfo, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  // host reads behind an event; the triangular inverse (independent of the host
+  // algebra) is queued first so the GPU does not idle over the round trip
+  double* hld = h->hpin;
+  double* hgram = h->hpin + nslot * (NB + 1);
+  for (size_t s = 0; s < nslot; ++s)
+    DCHK_HIP(h, hipMemcpyAsync(hld + s * (NB + 1), h->ranks[s].logdet, (NB + 1) * sizeof(double),
+                               hipMemcpyDeviceToHost, h->stream));
+  DCHK_HIP(h, hipMemcpyAsync(hgram, h->gram, (size_t)Pc * Pc * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  DCHK_HIP(h, hipMemcpyAsync(hgram + Pc * Pc, h->dinfo, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  DCHK_HIP(h, hipEventRecord(h->e1, h->stream));
+  if (h->grad_now)
+    for (int k = 0; k < NB; ++k) DCHK(trtri_step(h, k, ev));
+  DCHK_HIP(h, hipEventSynchronize(h->e1));
+  int info = 0;
+  std::memcpy(&info, hgram + Pc * Pc, sizeof(int));
+  if (info == GEMM_WAIT_TIMEOUT) return dfail(h, GPE_ERR_HIP, "internal error: flag wait timed out");
+  if (info != 0) {
+    h->err = "matrix not positive definite (pivot " + std::to_string(info) + ")";
+    return GPE_NOT_PD;
+  }
+  double logdetA = 0.0;
+  for (int k = 0; k < NB; ++k) {
+    // loopback: step k's log-determinant part sits in its owner's slot; RCCL: summed
+    logdetA += h->loop ? hld[(size_t)(k % P) * (NB + 1) + k] : hld[k];
+  }
+  logdetA *= 2.0;
+  std::vector<double> G((size_t)Pc * Pc);
+  for (int i = 0; i < Pc; ++i)
+    for (int j = 0; j < Pc; ++j) G[(size_t)i * Pc + j] = -hgram[i + (size_t)j * Pc];
+  SmallAlgebra sa = small_from_gram(G, Pc);
+  if (!sa.ok) {
+    h->err = "H^T A^-1 H not positive definite";
+    return GPE_NOT_PD;
+  }
+  const double n = (double)h->n;
+  double llh, sig2, cfac, gscale;
+  if (gp4ml) {
+    llh = 0.5 * (sa.quad + logdetA + sa.logdetQ + (n - q) * std::log(2.0 * M_PI));
+    sig2 = s2;
+    cfac = 1.0;
+    gscale = s2;
+  } else {
+    sig2 = sa.quad / (n - q - 2.0);
+    llh = 0.5 * ((n - q) * std::log(sig2) + logdetA + sa.logdetQ);
+    cfac = (n - q) / (sig2 * (n - q - 2.0));
+    gscale = sig2;
+  }
+  *llh_out = llh;
+  if (sigma2_out) *sigma2_out = sig2;
+
+  if (h->grad_now) {
+    // R2 = Z T2; [sqrt(c) alpha, W] = X^T R2 = sum over ranks of X_r^T R2_r
+    const std::vector<double> T2 = small_t2(sa, q, cfac);
+    std::memcpy(h->hpin, T2.data(), T2.size() * sizeof(double));
+    DCHK_HIP(h, hipMemcpyAsync(h->dT2, h->hpin, T2.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    hipLaunchKernelGGL(k_apply_small, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, h->stream, h->dZ, np, Pc,
+                       h->dT2, Pc, h->dR2, np, (int)np, h->dinfo);
+    DCHK_HIP(h, hipGetLastError());
+    DCHK_HIP(h, hipMemsetAsync(h->wpart, 0, (size_t)np * TILE * sizeof(double), h->stream));
+    for (size_t s = 0; s < nslot; ++s) {
+      const Rank& R = h->ranks[s];
+      if (R.nlx == 0) continue;
+      const long long e = (long long)R.nlx * TILE;
+      hipLaunchKernelGGL(k_dist_rows, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, h->stream, h->dR2, np, Pc,
+                         P, R.rank, R.nlx, h->r2loc, R.ld);
+      DCHK_HIP(h, hipGetLastError());
+      DCHK(launch(h, h->wa_l[s], h->gprobs));
+    }
+    if (!h->loop) {
+      DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
+      DCHK_NCCL(h, ncclAllReduce(h->wpart, h->wpart, (size_t)np * Pc, ncclDouble, ncclSum, h->comm, h->stream));
+      DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
+    }
+    // each rank: partial A^-1 over its rows, then its share of the contraction
+    DCHK_HIP(h, hipMemsetAsync(h->csum, 0, nslot * (d + 2) * sizeof(double), h->stream));
+    const int nblk = NB * (NB + 1) / 2;
+    const int bucket = std::max(d, Pc);
+    for (size_t s = 0; s < nslot; ++s) {
+      const Rank& R = h->ranks[s];
+      if (R.nlx == 0) continue;
+      DCHK(launch(h, h->lau_l[s], h->gprobs));
+      const int q1 = R.rank == 0 ? Pc : 0;   // the -W W^T term once
+      const dim3 g(nblk);
+      if (d == 10 && Pc <= 13)
+        hipLaunchKernelGGL((k_contract<10, 13>), g, dim3(256), 0, h->stream, h->pbuf, np, h->dXw, d, h->wpart, np, q1, (int)h->n, h->cpart, h->dinfo);
+      else if (d == 20 && Pc <= 21)   // BASELINE configs[3]
+        hipLaunchKernelGGL((k_contract<20, 21>), g, dim3(256), 0, h->stream, h->pbuf, np, h->dXw, d, h->wpart, np, q1, (int)h->n, h->cpart, h->dinfo);
+      else if (bucket <= 8)
+        hipLaunchKernelGGL((k_contract<8, 9>), g, dim3(256), 0, h->stream, h->pbuf, np, h->dXw, d, h->wpart, np, q1, (int)h->n, h->cpart, h->dinfo);
+      else if (bucket <= 16)
+        hipLaunchKernelGGL((k_contract<16, 17>), g, dim3(256), 0, h->stream, h->pbuf, np, h->dXw, d, h->wpart, np, q1, (int)h->n, h->cpart, h->dinfo);
+      else
+        hipLaunchKernelGGL((k_contract<32, 33>), g, dim3(256), 0, h->stream, h->pbuf, np, h->dXw, d, h->wpart, np, q1, (int)h->n, h->cpart, h->dinfo);
+      DCHK_HIP(h, hipGetLastError());
+      hipLaunchKernelGGL(k_reduce_rows, dim3(d + 2), dim3(256), 0, h->stream, h->cpart, nblk, d + 2,
+                         h->csum + s * (d + 2));
+      DCHK_HIP(h, hipGetLastError());
+    }
+    if (!h->loop) {
+      DCHK_NCCL(h, ncclAllReduce(h->csum, h->csum, (size_t)d + 2, ncclDouble, ncclSum, h->comm, h->stream));
+    }
+  }
+  DCHK_HIP(h, hipEventRecord(h->e1, h->stream));
+  if (h->grad_now)
+    DCHK_HIP(h, hipMemcpyAsync(h->hpin, h->csum, nslot * (d + 2) * sizeof(double), hipMemcpyDeviceToHost,
+                               h->stream));
   DCHK_HIP(h, hipStreamSynchronize(h->stream));
-  std::memcpy(&info, h->hpin + Pc * Pc, sizeof(int));
+  if (h->grad_now) {
+    std::vector<double> red((size_t)d + 2, 0.0);
+    for (size_t s = 0; s < nslot; ++s)
+      for (int k = 0; k < d + 2; ++k) red[k] += h->hpin[s * (d + 2) + k];
+    double coff, cdiag;
+    if (kernel == GPE_KERNEL_ALT_NUG) {
+      coff = 1.0;
+      cdiag = 1.0 + nu * nu;
+    } else {
+      coff = 1.0 - nu;
+      cdiag = 1.0;
+    }
+    small_grad(red.data(), d, kernel == GPE_KERNEL_ALT_NUG, nu, fitnug, gp4ml, gscale, s2, coff, cdiag, n_hp,
+               grad_out);
+  }
   {
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, h->e0, h->e1);
@@ -648,33 +955,6 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
     }
     h->comm_ms = c;
   }
-  if (info == GEMM_WAIT_TIMEOUT) return dfail(h, GPE_ERR_HIP, "internal error: flag wait timed out");
-  if (info != 0) {
-    h->err = "matrix not positive definite (pivot " + std::to_string(info) + ")";
-    return GPE_NOT_PD;
-  }
-  std::vector<double> G((size_t)Pc * Pc);
-  for (int i = 0; i < Pc; ++i)
-    for (int j = 0; j < Pc; ++j) G[(size_t)i * Pc + j] = -h->hpin[i + (size_t)j * Pc];
-  double logdetA = 0.0;
-  for (int k = 0; k < NB; ++k) logdetA += ld_sum[k];
-  logdetA *= 2.0;
-  SmallAlgebra sa = small_from_gram(G, Pc);
-  if (!sa.ok) {
-    h->err = "H^T A^-1 H not positive definite";
-    return GPE_NOT_PD;
-  }
-  const double n = (double)h->n;
-  double llh, sig2;
-  if (gp4ml) {
-    llh = 0.5 * (sa.quad + logdetA + sa.logdetQ + (n - q) * std::log(2.0 * M_PI));
-    sig2 = s2;
-  } else {
-    sig2 = sa.quad / (n - q - 2.0);
-    llh = 0.5 * ((n - q) * std::log(sig2) + logdetA + sa.logdetQ);
-  }
-  *llh_out = llh;
-  if (sigma2_out) *sigma2_out = sig2;
   return GPE_OK;
 }
 

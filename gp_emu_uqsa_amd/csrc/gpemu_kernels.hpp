@@ -759,8 +759,14 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
   if (tiles) {
     tile_unpack(tiles[blockIdx.x], p, ti, tj);
   } else {
-    for (int i = 1; i < nprob; ++i)
-      if ((int)blockIdx.x >= probs[i].tile_begin) p = i;
+    // last problem whose tile_begin <= blockIdx.x (tile_begin is non-decreasing)
+    int lo = 0, hi = nprob - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if ((int)blockIdx.x >= probs[mid].tile_begin) lo = mid;
+      else hi = mid - 1;
+    }
+    p = lo;
   }
   const GemmProb P = probs[p];
   if (!tiles) {

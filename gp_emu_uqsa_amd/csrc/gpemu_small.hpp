@@ -81,4 +81,29 @@ inline SmallAlgebra small_from_gram(const std::vector<double>& G, int P) {
   return s;
 }
 
+// T2 (P x P, column-major) with R2 = [z w] T2 = [sqrt(c)(z - w beta), w Kq^-T]:
+// L^-T R2 = [sqrt(c) alpha, W], the two low-rank terms of the gradient's M
+inline std::vector<double> small_t2(const SmallAlgebra& sa, int q, double cfac) {
+  const int P = q + 1;
+  std::vector<double> Kinv = small_trinv(sa.Kq, q);   // row-major
+  std::vector<double> T2((size_t)P * P, 0.0);
+  const double sc = std::sqrt(cfac);
+  T2[0] = sc;
+  for (int i = 0; i < q; ++i) T2[(i + 1) + 0 * P] = -sc * sa.beta[i];
+  for (int o = 0; o < q; ++o)
+    for (int i = 0; i < q; ++i) T2[(i + 1) + (o + 1) * P] = Kinv[o * q + i];   // (Kq^-T)(i,o)
+  return T2;
+}
+
+// gradient from the contraction sums red[0:d] = sum M E dx_k^2, red[d] = sum_{i>j} M E,
+// red[d+1] = tr M (the d+2 outputs of k_contract); coff/cdiag as the K-build's
+inline void small_grad(const double* red, int d, bool alt_nug, double nu, bool fitnug, bool gp4ml,
+                       double gscale, double s2, double coff, double cdiag, int n_hp, double* grad) {
+  const double pref = alt_nug ? 1.0 : (1.0 - nu);
+  const double SE = 2.0 * red[d], Tr = red[d + 1];
+  for (int k = 0; k < d; ++k) grad[k] = 0.5 * gscale * pref * 2.0 * red[k];
+  if (fitnug) grad[d] = alt_nug ? 0.5 * gscale * nu * nu * Tr : 0.5 * gscale * (-0.5 * nu) * SE;
+  if (gp4ml) grad[n_hp - 1] = 0.5 * s2 * (coff * SE + cdiag * Tr);
+}
+
 }  // namespace gpe

@@ -60,7 +60,7 @@ SIGNATURES = {
     "gpe_dist_last_error": (_ct.c_char_p, [_VP]),
     "gpe_dist_set_data": (_ct.c_int, [_VP, _ct.c_int64, _ct.c_int32, _ct.c_int32, _D, _D, _D, _D]),
     "gpe_dist_objective": (_ct.c_int, [_VP, _ct.c_int32, _ct.c_int32, _D, _ct.c_int32, _ct.c_double,
-                                       _D, _D]),
+                                       _ct.c_int32, _D, _D, _D]),
     "gpe_dist_owner": (_ct.c_int32, [_ct.c_int32, _ct.c_int32]),
     "gpe_dist_local_rows": (_ct.c_int32, [_ct.c_int64, _ct.c_int32, _ct.c_int32]),
     "gpe_dist_times": (_ct.c_int, [_VP, _D, _D]),
@@ -329,7 +329,7 @@ def default_context() -> Context:
 
 
 class DistContext:
-    """Row-block distributed value objective over P GPUs (include/gpemu_dist.h).
+    """Row-block distributed objective and gradient over P GPUs (include/gpemu_dist.h).
 
     unique_id=None selects the in-process loopback transport: all `nranks`
     logical ranks run in this process on `device` (same partition and schedule,
@@ -383,13 +383,18 @@ class DistContext:
         self._check(self.lib.gpe_dist_set_data(self._h, n, d, H.shape[1], _ptr(X), _ptr(f), _ptr(H),
                                                _ptr(rr)), "gpe_dist_set_data")
 
-    def objective(self, variant, kernel, hp, nu_fixed=0.0):
-        """Value-only objective (collective over all ranks): (llh, sigma2)."""
+    def objective(self, variant, kernel, hp, nu_fixed=0.0, want_grad=False):
+        """Objective (collective over all ranks): (llh, sigma2), or (llh, grad, sigma2)
+        with want_grad."""
         hp = _f64(hp).ravel()
         llh, s2 = _ct.c_double(0.0), _ct.c_double(0.0)
+        grad = _np.zeros(hp.size) if want_grad else None
         self._check(self.lib.gpe_dist_objective(self._h, int(variant), int(kernel), _ptr(hp), hp.size,
-                                                float(nu_fixed), _ct.byref(llh), _ct.byref(s2)),
+                                                float(nu_fixed), int(bool(want_grad)), _ct.byref(llh),
+                                                _ptr(grad), _ct.byref(s2)),
                     "gpe_dist_objective")
+        if want_grad:
+            return llh.value, grad, s2.value
         return llh.value, s2.value
 
     def times(self):

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GPE_ABI_VERSION 2
+#define GPE_ABI_VERSION 3   /* 3: gpe_dist_objective gained want_grad / grad_out */
 
 enum gpe_status {
     GPE_OK = 0,

@@ -2,16 +2,23 @@
  * gpemu_dist.h -- C-ABI of the row-block distributed objective in libgpemu.so
  * (BASELINE configs[3]: n = 65536, d = 20 on 8 x MI355X).
  *
- * Replaces, for one evaluation spread over P GPUs, the value part of
- * Optimize.loglikelihood_gp4ml / _mucm (_emulatoroptimise.py:412-493, :305-378):
- * K-build + blocked right-looking Cholesky + log|A| + L^-1 [f H].  The n x n
- * covariance is partitioned by 128-row tile rows, dealt cyclically (tile row i on
- * rank i mod P); each rank stores only its tile rows of the lower triangle.  Per
- * column step the owner factors the diagonal tile in-kernel, RCCL broadcasts its
- * inverse (128 KB), every rank forms its panel tiles, RCCL all-gathers the panel
- * column, and every rank applies the trailing update to its own rows.  [f H] is
- * carried as one extra tile row under the matrix, so L^-1 [f H] and its Gram
- * matrix fall out of the same sweep (no triangular inverse for the value).
+ * Replaces, for one evaluation spread over P GPUs, Optimize.loglikelihood_gp4ml /
+ * _mucm and their gradients (_emulatoroptimise.py:412-493, :305-378, the same
+ * functions gpe_objective replaces on one GPU): K-build + blocked right-looking
+ * Cholesky + log|A| + L^-1 [f H], and for the gradient L^-1, A^-1 and the
+ * contraction <M, dA/dtheta>.  The n x n covariance is partitioned by 128-row
+ * tile rows, dealt cyclically (tile row i on rank i mod P); each rank stores only
+ * its tile rows of the lower triangle.  Per column step the owner factors the
+ * diagonal tile in-kernel, RCCL broadcasts its inverse (128 KB), every rank forms
+ * its panel tiles, RCCL all-gathers the panel column, and every rank applies the
+ * trailing update to its own rows.  [f H] is carried as one extra tile row under
+ * the matrix, so L^-1 [f H] and its Gram matrix fall out of the same sweep.
+ *
+ * Gradient: X = L^-1 is formed by rows with the same partition (per step the
+ * owner finishes X(k, :) and RCCL broadcasts it; every rank updates its own rows);
+ * each rank then forms its partial X_r^T X_r of A^-1 and contracts it locally, so
+ * the only other collectives are an all-reduce of the n x (q+1) matrix
+ * [sqrt(c) alpha, W] and of the d+2 contraction sums.
  *
  * Processes: one per GPU.  Rank 0 calls gpe_dist_unique_id, the host shares the
  * 128 bytes (torch.distributed / gloo in gp_emu_uqsa_amd/distributed.py), every
@@ -20,8 +27,7 @@
  * the same partition and schedule and device copies in place of RCCL (used to
  * test P = 2..8 on one GPU).
  *
- * Same conventions and status codes as gpemu.h.  The gradient stays on the
- * single-GPU path (the distributed TRTRI/LAUUM is SURVEY.md 8f item 2).
+ * Same conventions and status codes as gpemu.h.
  */
 #ifndef GPEMU_DIST_H
 #define GPEMU_DIST_H
@@ -47,10 +53,13 @@ const char* gpe_dist_last_error(gpe_dist* h);
 int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double* X,
                       const double* f, const double* H, const double* r);
 
-/* Value-only objective, arguments as gpe_objective (want_grad = 0).  All ranks
- * call it collectively and all receive the same llh / sigma2. */
+/* Objective (and gradient when want_grad != 0), arguments and outputs as
+ * gpe_objective.  All ranks call it collectively and all receive the same llh,
+ * gradient and sigma2.  The gradient buffers (this rank's rows of L^-1 and an
+ * n_pad x n_pad partial of A^-1) are allocated on the first want_grad call. */
 int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const double* hp,
-                       int32_t n_hp, double nu_fixed, double* llh_out, double* sigma2_out);
+                       int32_t n_hp, double nu_fixed, int32_t want_grad, double* llh_out,
+                       double* grad_out, double* sigma2_out);
 
 /* Partition map (pure functions, no GPU): owner rank of tile row t and the number
  * of tile rows (including the augmented [f H] row) rank `rank` stores. */

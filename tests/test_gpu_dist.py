@@ -1,7 +1,10 @@
-"""Row-block distributed value objective (include/gpemu_dist.h) on the GPU:
+"""Row-block distributed objective and gradient (include/gpemu_dist.h) on the GPU:
 the loopback transport (P logical ranks in one process, same partition and
 schedule as RCCL) for P = 1..8, and a 1-rank RCCL communicator, against the
-oracle (reference op order) and the single-GPU path."""
+oracle (reference op order) and the single-GPU path.
+
+Gradient tolerance as tests/test_gpu_objective.py:
+|g - g_ref| <= 1e-7 (|g_ref| + max|g_ref|)."""
 import numpy as np
 import pytest
 
@@ -51,6 +54,52 @@ def test_loopback_variants_match_single_gpu(ctx, variant, kernel, use_r):
     dc.close()
 
 
+def _grad_ok(g, gref, tol=1e-7):
+    g, gref = np.asarray(g), np.asarray(gref)
+    err = np.abs(g - gref)
+    return bool(np.all(err <= tol * (np.abs(gref) + np.abs(gref).max()))), err.max()
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("n", [300, 1000])
+def test_loopback_gradient_matches_oracle(P, n):
+    d = 3
+    X, f, H = orc.synthetic_problem(n, d, seed=1)
+    hp = _hp(d)
+    ctx = native.DistContext(0, P)
+    ctx.set_data(X, f, H)
+    llh, g, s2 = ctx.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=True)
+    ref, gref = orc.objective_ref(X, f, H, hp, orc.GP4ML, orc.STD, True)[:2]
+    assert abs(llh - ref) <= 1e-9 * abs(ref), (llh, ref)
+    ok, err = _grad_ok(g, gref)
+    assert ok, (g, gref, err)
+    # value-only call after a gradient call reuses the same buffers
+    llh2, _ = ctx.objective(native.GP4ML, native.KERNEL_STD, hp)
+    assert llh2 == llh
+    ctx.close()
+
+
+@pytest.mark.parametrize("variant,kernel,use_r,d,P", [(native.MUCM, native.KERNEL_STD, False, 4, 3),
+                                                       (native.GP4ML, native.KERNEL_ALT_NUG, True, 4, 2),
+                                                       (native.GP4ML, native.KERNEL_STD, False, 10, 4),
+                                                       (native.GP4ML, native.KERNEL_STD, False, 20, 3)])
+def test_loopback_gradient_matches_single_gpu(ctx, variant, kernel, use_r, d, P):
+    n = 1100
+    X, f, H = orc.synthetic_problem(n, d, seed=6)
+    r = np.random.RandomState(5).uniform(1e-4, 1e-3, size=n) if use_r else None
+    hp = _hp(d, gp4ml=variant == native.GP4ML)
+    ctx.set_data(X, f, H, r)
+    ref, gref, s2ref = ctx.objective(variant, kernel, hp, want_grad=True)
+    dc = native.DistContext(0, P)
+    dc.set_data(X, f, H, r)
+    llh, g, s2 = dc.objective(variant, kernel, hp, want_grad=True)
+    assert abs(llh - ref) <= 1e-10 * abs(ref), (llh, ref)
+    assert abs(s2 - s2ref) <= 1e-10 * abs(s2ref)
+    ok, err = _grad_ok(g, gref)
+    assert ok, (g, gref, err)
+    dc.close()
+
+
 def test_loopback_not_pd():
     X, f, H = orc.synthetic_problem(400, 2, seed=3)
     X[1] = X[0]                                   # duplicate point, no nugget
@@ -58,6 +107,8 @@ def test_loopback_not_pd():
     dc.set_data(X, f, H)
     with pytest.raises(native.NotPositiveDefinite):
         dc.objective(native.GP4ML, native.KERNEL_STD, np.array([0.5, 0.5, 1.0]), nu_fixed=0.0)
+    with pytest.raises(native.NotPositiveDefinite):
+        dc.objective(native.GP4ML, native.KERNEL_STD, np.array([0.5, 0.5, 1.0]), nu_fixed=0.0, want_grad=True)
     dc.close()
 
 
@@ -68,8 +119,12 @@ def test_rccl_single_rank():
     dc = native.DistContext(0, 1, 0, native.dist_unique_id())
     dc.set_data(X, f, H)
     llh, _ = dc.objective(native.GP4ML, native.KERNEL_STD, hp)
-    ref = orc.objective_ref(X, f, H, hp, orc.GP4ML, orc.STD, True, want_grad=False)[0]
+    ref, gref = orc.objective_ref(X, f, H, hp, orc.GP4ML, orc.STD, True)[:2]
     assert abs(llh - ref) <= 1e-9 * abs(ref), (llh, ref)
+    llh_g, g, _ = dc.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=True)
+    assert llh_g == llh
+    ok, err = _grad_ok(g, gref)
+    assert ok, (g, gref, err)
     t = dc.times()
     assert t["total_ms"] > 0.0
     dc.close()

@@ -1,10 +1,10 @@
-"""Distributed value objective (BASELINE configs[3]) -- runner.
+"""Distributed objective / gradient (BASELINE configs[3]) -- runner.
 
   one GPU, P logical ranks (loopback):   python tools/dist_objective.py --loopback P --points N --dims D
   P GPUs over RCCL (one process each):    python -m torch.distributed.run --nproc-per-node P \\
                                               --master-addr 127.0.0.1 tools/dist_objective.py --points N --dims D
 Prints one JSON line (rank 0): llh, ms per eval (max over ranks), comm ms, and
-with --check the single-GPU value for the same inputs.
+with --check the single-GPU value (and gradient with --grad) for the same inputs.
 """
 import argparse
 import json
@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--loopback", type=int, default=0)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--grad", action="store_true", help="LLH + gradient instead of the value only")
     args = ap.parse_args()
     from gp_emu_uqsa_amd import native
     from gp_emu_uqsa_amd import synthetic
@@ -43,13 +44,16 @@ def main():
         ctx = distributed.dist_context()
         nranks = world
     ctx.set_data(X, f, H)
-    llh, _ = ctx.objective(native.GP4ML, native.KERNEL_STD, hp)   # warm-up
+    def ev():
+        r = ctx.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=args.grad)
+        return r[0], (r[1] if args.grad else None)
+    llh, g = ev()   # warm-up (allocates the gradient buffers)
     ts = []
     for _ in range(args.reps):
         if dist is not None:
             dist.barrier()
         t = time.perf_counter()
-        llh, _ = ctx.objective(native.GP4ML, native.KERNEL_STD, hp)
+        llh, g = ev()
         ts.append(time.perf_counter() - t)
     el = min(ts)
     if dist is not None:
@@ -58,13 +62,15 @@ def main():
         dist.all_reduce(v, op=dist.ReduceOp.MAX)
         el = float(v.item())
     out = {"n": args.points, "d": args.dims, "ranks": nranks, "transport": "loopback" if args.loopback else "rccl",
-           "llh": llh, "ms_per_eval": 1e3 * el, **ctx.times()}
+           "grad": args.grad, "llh": llh, "ms_per_eval": 1e3 * el, **ctx.times()}
     if args.check and rank == 0:
         c1 = native.Context(int(os.environ.get("LOCAL_RANK", "0")))
         c1.set_data(X, f, H)
-        ref, _, _ = c1.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=False)
+        ref, gref, _ = c1.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=args.grad)
         out["single_gpu_llh"] = ref
         out["rel_diff"] = abs(llh - ref) / abs(ref)
+        if args.grad:
+            out["grad_max_rel_diff"] = float(np.max(np.abs(g - gref)) / np.max(np.abs(gref)))
         c1.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
