@@ -5,12 +5,15 @@ LOCAL_RANK).  torch.distributed (gloo is enough: only 128 bytes travel) carries
 the RCCL unique id from rank 0 to the others; every data-path collective after
 that is RCCL on the GPU, issued by libgpemu.so itself (include/gpemu_dist.h):
 a 128 KB broadcast of the diagonal-block inverse and an all-gather of the panel
-column per 128-column step, plus three tiny reductions at the end.
+column per 128-column step; for the gradient a broadcast of one row of L^-1 per
+step, an all-reduce of [sqrt(c) alpha, W] (n x (q+1)) and of d+2 sums.
 
-This replaces, for one evaluation spread over P GPUs, the value part of
-Optimize.loglikelihood_gp4ml / _mucm (_emulatoroptimise.py:412-493, :305-378).
-The gradient stays on the single-GPU path (distributed TRTRI/LAUUM is SURVEY.md
-8f item 2); multistart tries are spread as replicas by replicas.py.
+This replaces, for one evaluation spread over P GPUs, Optimize.loglikelihood_gp4ml
+/ _mucm and their gradients (_emulatoroptimise.py:412-493, :305-378).
+``enable_objective()`` routes train()'s objective calls through it: every rank
+then runs the same L-BFGS-B chains in lockstep (the objective is collective and
+returns identical values on every rank), so multistart tries are not sharded
+over ranks in that mode (replicas.py does that when the objective is local).
 """
 from __future__ import annotations
 
@@ -53,3 +56,57 @@ def partition(n: int, nranks: int):
     for t in range(nb + 1):
         rows[native.dist_owner(nranks, t)].append(t)
     return rows
+
+
+class RowBlockObjective:
+    """Collective objective for Optimize: the DistContext plus resident-data tracking."""
+
+    def __init__(self, ctx: native.DistContext):
+        self.ctx = ctx
+        self._key = None
+
+    def ensure_data(self, X, f, H, r=None):
+        key = native.Context._digest(X, f, H, r)
+        if key != self._key:
+            self.ctx.set_data(X, f, H, r)
+            self._key = key
+
+    def objective(self, variant, kernel, hp, nu_fixed=0.0, want_grad=True):
+        """(llh, grad or None, sigma2), as native.Context.objective."""
+        if want_grad:
+            return self.ctx.objective(variant, kernel, hp, nu_fixed, want_grad=True)
+        llh, s2 = self.ctx.objective(variant, kernel, hp, nu_fixed)
+        return llh, None, s2
+
+    def close(self):
+        self.ctx.close()
+
+
+_OBJECTIVE: RowBlockObjective | None = None
+
+
+def enable_objective(device: int | None = None, group=None, loopback: int = 0) -> RowBlockObjective:
+    """Route Optimize's objective through the row-block distributed path.
+
+    With an initialised process group this is collective (every rank calls it);
+    ``loopback=P`` instead runs P logical ranks in this process on one GPU."""
+    global _OBJECTIVE
+    disable_objective()
+    if loopback:
+        dev = int(os.environ.get("LOCAL_RANK", "0")) if device is None else device
+        ctx = native.DistContext(dev, int(loopback))
+    else:
+        ctx = dist_context(device, group)
+    _OBJECTIVE = RowBlockObjective(ctx)
+    return _OBJECTIVE
+
+
+def disable_objective():
+    global _OBJECTIVE
+    if _OBJECTIVE is not None:
+        _OBJECTIVE.close()
+        _OBJECTIVE = None
+
+
+def active_objective() -> RowBlockObjective | None:
+    return _OBJECTIVE

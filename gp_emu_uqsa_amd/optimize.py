@@ -10,12 +10,15 @@ Multistart tries are independent units: when torch.distributed is initialised
 with world_size > 1 the tries are sharded over ranks (one GPU per rank, no data
 exchange) and only the (fun, x) results are gathered -- the guess grid is drawn
 identically on every rank, so the chosen optimum equals the sequential one.
+With distributed.enable_objective() each evaluation is instead spread over all
+ranks (row-block partition) and every rank runs every try in lockstep.
 """
 from __future__ import annotations
 
 import numpy as np
 from scipy.optimize import minimize
 
+from . import distributed
 from . import native
 from .model import upload_training
 from . import replicas
@@ -137,7 +140,8 @@ class Optimize:
         else:
             print("Using L-BFGS-G method (no constraints)...")
 
-        upload_training(self.data)
+        if distributed.active_objective() is None:
+            upload_training(self.data)
         results = {}
         for C in replicas.my_items(numguesses):
             try:
@@ -189,7 +193,13 @@ class Optimize:
 
     # -- objectives: one gpe_objective call each
     def _call(self, variant, x, want_grad=True):
-        ctx = native.default_context()
+        obj = distributed.active_objective()
+        if obj is not None:   # collective row-block objective (distributed.enable_objective)
+            r = None if np.isscalar(self.data.r) else self.data.r
+            obj.ensure_data(self.data.inputs, self.data.outputs, self.data.H, r)
+            ctx = obj
+        else:
+            ctx = native.default_context()
         return ctx.objective(variant, self.data.K.kind, x, nu_fixed=float(self.data.K.n),
                              want_grad=want_grad)
 

@@ -4,13 +4,18 @@ The reference has no parallelism; its multistart loop (_emulatoroptimise.py:227-
 runs `tries` independent L-BFGS-B chains and keeps the best.  Here the chains are
 dealt round-robin over the ranks of an initialised torch.distributed group (any
 backend; gloo is enough since only a few floats per chain are exchanged) and the
-(fun, x) results are gathered on every rank.  Without a process group, or with
-world_size 1, everything runs locally in order.
+(fun, x) results are gathered on every rank.  Without a process group, with
+world_size 1, or while the row-block distributed objective is enabled
+(distributed.enable_objective: each evaluation is itself collective), everything
+runs locally in order.
 """
 from __future__ import annotations
 
 
 def _group():
+    from . import distributed
+    if distributed.active_objective() is not None:
+        return None   # collective objective: every rank runs every unit in lockstep
     try:
         import torch.distributed as dist
     except Exception:  # torch absent: single process

@@ -2,8 +2,10 @@
 library exports, the RCCL-id hand-off over gloo, and a NumPy model of the exact
 per-step schedule of gpemu_dist.hip (cyclic tile rows + augmented [f H] row,
 broadcast of the diagonal inverse, all-gather of the panel column, own-row trailing
-update) run on 2 and 3 gloo ranks against a dense factorisation.  NumPy is only the
-test's stand-in for the HIP tile kernels."""
+update) run on 2 and 3 gloo ranks against a dense factorisation, extended by the
+gradient schedule (rows of L^-1 finished by their owner and broadcast, own-row
+updates, per-rank partials X_r^T X_r whose sum is A^-1).  NumPy is only the test's
+stand-in for the HIP tile kernels."""
 import os
 import socket
 
@@ -118,7 +120,26 @@ def _sched_worker(rank, world, port, n, q, out):
         if nb % world == rank:
             g = torch.from_numpy(-loc[nb][:Pc, nb * B:nb * B + Pc].copy())
         dist.broadcast(g, src=nb % world)
-        out[rank] = (2.0 * float(ld.sum()), g.numpy().tolist())
+        # gradient schedule: X = L^-1 by rows; R(t, :) accumulates -sum L(t,j) X(j, :)
+        Xl = {t: np.zeros((B, nb * B)) for t in mine if t < nb}
+        for k in range(nb):
+            owner = k % world
+            xrow = torch.zeros(B, (k + 1) * B, dtype=torch.float64)
+            if owner == rank:
+                Dinv = np.linalg.inv(loc[k][:, k * B:(k + 1) * B])
+                Xl[k][:, :k * B] = Dinv @ Xl[k][:, :k * B]
+                Xl[k][:, k * B:(k + 1) * B] = Dinv
+                xrow = torch.from_numpy(Xl[k][:, :(k + 1) * B].copy())
+            dist.broadcast(xrow, src=owner)
+            for t in Xl:
+                if t > k:
+                    Xl[t][:, :(k + 1) * B] -= loc[t][:, k * B:(k + 1) * B] @ xrow.numpy()
+        part = np.zeros((nb * B, nb * B))
+        for xr in Xl.values():
+            part += xr.T @ xr
+        ainv = torch.from_numpy(part)
+        dist.all_reduce(ainv)     # the library contracts each partial instead; the sum is A^-1
+        out[rank] = (2.0 * float(ld.sum()), g.numpy().tolist(), ainv.numpy().tolist())
     finally:
         dist.destroy_process_group()
 
@@ -134,7 +155,39 @@ def test_schedule_model_matches_dense(world):
     A, F = _problem(n, q)
     L = np.linalg.cholesky(A)
     Z = np.linalg.solve(L, F)
+    Ainv = np.linalg.inv(A)
     for r in range(world):
-        logdet, G = res[r]
+        logdet, G, ainv = res[r]
         assert abs(logdet - np.linalg.slogdet(A)[1]) < 1e-10 * abs(logdet)
         assert np.max(np.abs(np.array(G) - Z.T @ Z)) < 1e-10 * np.max(np.abs(Z.T @ Z))
+        assert np.max(np.abs(np.array(ainv) - Ainv)) < 1e-9 * np.max(np.abs(Ainv))
+
+
+def _lockstep_worker(rank, world, port, out):
+    from gp_emu_uqsa_amd import replicas
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sharded = replicas.my_items(5)
+        distributed._OBJECTIVE = object()      # stand-in for an enabled collective objective
+        try:
+            lockstep = replicas.my_items(5)
+            merged = replicas.gather_results({i: (float(i), np.zeros(1), None) for i in lockstep}, 5)
+        finally:
+            distributed._OBJECTIVE = None
+        out[rank] = (sharded, lockstep, sorted(merged))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_collective_objective_runs_every_try_on_every_rank():
+    """With distributed.enable_objective() each evaluation is collective, so every
+    rank must step every multistart chain (no replica sharding)."""
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_lockstep_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    assert res[0][0] == [0, 2, 4] and res[1][0] == [1, 3]
+    for r in range(2):
+        assert res[r][1] == [0, 1, 2, 3, 4] and res[r][2] == [0, 1, 2, 3, 4]

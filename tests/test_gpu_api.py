@@ -3,6 +3,8 @@
 * g.train() on examples/toy-sim with np.random.seed(s) must follow the
   reference's L-BFGS-B trajectory (G4): same objective call sequence (1e-6) and
   the same trained hyperparameters, sigma and beta (1e-6 relative).
+  The same again with the objective routed through the row-block distributed
+  path (distributed.enable_objective, loopback transport, 3 logical ranks).
 * g.posterior() on the reconstructed emulators (G3) within 1e-8.
 """
 import json
@@ -30,8 +32,17 @@ def workdir(tmp_path, monkeypatch):
     return make
 
 
+@pytest.fixture(params=["single", "rowblock3"])
+def objective_path(request):
+    from gp_emu_uqsa_amd import distributed
+    if request.param == "rowblock3":
+        distributed.enable_objective(loopback=3)
+    yield request.param
+    distributed.disable_objective()
+
+
 @pytest.mark.parametrize("seed", [0, 1])
-def test_train_toysim_trajectory(workdir, seed, monkeypatch):
+def test_train_toysim_trajectory(workdir, seed, monkeypatch, objective_path):
     z = np.load(os.path.join(GOLD, f"train_toysim_seed{seed}.npz"))
     workdir("toy-sim")
     np.random.seed(seed)

@@ -2,12 +2,19 @@
 n=16384, d=10 through the reference's API and file surface, scipy L-BFGS-B
 driving the GPU objective (LLH + gradient) -- dev/measurement tool.
 
+configs[3] (C4, n=65536, d=20 on 8 GPUs): run under torchrun, one process per
+GPU; the objective is then the row-block distributed one (distributed.
+enable_objective over RCCL) and every rank steps the same L-BFGS-B chain.
+--loopback P runs that path with P logical ranks on one GPU.
+
 Writes config/beliefs/inputs/outputs for synthetic oLHC data into a scratch
 directory (tv_config 10 0 0: every point in training; gp4ml, nugget fitted,
 linear mean in all inputs, tries 1, constraints bounds), then times setup and
 train and prints one JSON line: wall seconds, objective evaluations, seconds per
 evaluation, trained delta / nugget / sigma, final LLH.
-usage: python tools/train_c3.py [--points 16384] [--dims 10] [--tries 1]
+usage: python tools/train_c3.py [--points 16384] [--dims 10] [--tries 1] [--loopback P]
+       python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+           tools/train_c3.py --points 65536 --dims 20
 """
 import argparse
 import json
@@ -45,11 +52,24 @@ def main():
     ap.add_argument("--points", type=int, default=16384)
     ap.add_argument("--dims", type=int, default=10)
     ap.add_argument("--tries", type=int, default=1)
+    ap.add_argument("--loopback", type=int, default=0, help="row-block objective, P logical ranks on one GPU")
     args = ap.parse_args()
     import gp_emu_uqsa_amd as g
-    from gp_emu_uqsa_amd import native
+    from gp_emu_uqsa_amd import distributed, native
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    mode = "single"
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo", rank=rank, world_size=world)
+        distributed.enable_objective()
+        mode = f"rowblock-rccl-{world}"
+    elif args.loopback:
+        distributed.enable_objective(loopback=args.loopback)
+        mode = f"rowblock-loopback-{args.loopback}"
     calls = {"n": 0, "s": 0.0}
-    orig = native.Context.objective
+    cls = native.Context if mode == "single" else distributed.RowBlockObjective
+    orig = cls.objective
 
     def counted(self, *a, **k):
         t = time.perf_counter()
@@ -58,7 +78,7 @@ def main():
         finally:
             calls["n"] += 1
             calls["s"] += time.perf_counter() - t
-    native.Context.objective = counted
+    cls.objective = counted
     with tempfile.TemporaryDirectory() as tmp:
         write_files(tmp, args.points, args.dims, args.tries)
         cwd = os.getcwd()
@@ -72,12 +92,17 @@ def main():
             t2 = time.perf_counter()
         finally:
             os.chdir(cwd)
-    out = {"config": f"C3 g.train(): n={args.points} d={args.dims} gp4ml nugget fitted, tries {args.tries}",
+    out = {"config": f"g.train(): n={args.points} d={args.dims} gp4ml nugget fitted, tries {args.tries}",
+           "objective": mode,
            "setup_s": t1 - t0, "train_s": t2 - t1, "objective_evals": calls["n"],
            "objective_s": calls["s"], "s_per_eval": calls["s"] / max(calls["n"], 1),
            "delta": np.asarray(E.par.delta).tolist(), "nugget": float(E.par.nugget),
            "sigma": float(E.par.sigma)}
-    print(json.dumps(out), flush=True)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    distributed.disable_objective()
+    if world > 1:
+        tdist.destroy_process_group()
 
 
 if __name__ == "__main__":
