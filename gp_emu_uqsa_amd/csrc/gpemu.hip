@@ -127,8 +127,17 @@ struct gpe_ctx {
   float* dK32 = nullptr;
   size_t k32_cap = 0;
 
+  // sensitivity workspace (gpe_sense_pairs / gpe_gauss_transform)
+  double* dSU = nullptr;     // J x n_pad per-point factors
+  double* dSZ = nullptr;     // n_pad x p
+  double* dSW = nullptr;     // J x d weights
+  double* dSpart = nullptr;  // per-wave partials
+  double* dSout = nullptr;
+  size_t su_cap = 0, sz_cap = 0, sw_cap = 0, spart_cap = 0, sout_cap = 0;
+
   // resident factor (gpe_factor)
   bool factor_valid = false;
+  bool ainv_valid = false;   // tr.A holds A^-1 (LAUUM of the resident L^-1)
   int f_kernel = 0;
   std::vector<double> f_delta;
   double f_nu = 0.0;
@@ -884,7 +893,8 @@ void gpe_destroy(gpe_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
-  double* bufs[] = {c->dX, c->dXw, c->dF, c->dr, c->tr.A, c->tr.B, c->tr.logdet, c->aux.A, c->aux.B,
+  double* bufs[] = {c->dSU, c->dSZ, c->dSW, c->dSpart, c->dSout,
+                    c->dX, c->dXw, c->dF, c->dr, c->tr.A, c->tr.B, c->tr.logdet, c->aux.A, c->aux.B,
                     c->aux.logdet, c->dinvdelta, c->dZ,
                     c->dR2, c->dWa, c->dskp, c->dgpart, c->dgram, c->dT2, c->dcpart, c->dcsum,
                     c->dW1, c->dW2, c->dW3, c->dXs, c->dXsw, c->dsmall};
@@ -932,6 +942,7 @@ int gpe_set_data(gpe_ctx* c, int64_t n, int32_t d, int32_t q, const double* X, c
   const bool resize = (n_pad != c->n_pad) || (d != c->d) || (q != c->q);
   c->n = n; c->d = d; c->q = q; c->n_pad = n_pad; c->NB = (int)(n_pad / TILE);
   c->factor_valid = false;
+  c->ainv_valid = false;
   c->x32_valid = false;
   if (resize) {
     CHK(ensure_fact(c, c->tr, n_pad));
@@ -1003,6 +1014,7 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
   const double s2 = gp4ml ? sigma * sigma : 1.0;
   const double rscale = (gp4ml && kernel == GPE_KERNEL_ALT_NUG) ? 1.0 : 0.0;
   c->factor_valid = false;
+  c->ainv_valid = false;
   c->x32_valid = false;
   if (c->prof) {
     c->gev_used = 0;
@@ -1126,6 +1138,7 @@ int gpe_factor(gpe_ctx* c, int32_t kernel, const double* delta, double nu, doubl
   if (!delta) return fail(c, GPE_ERR_ARG, "null delta");
   if (kernel != GPE_KERNEL_STD && kernel != GPE_KERNEL_ALT_NUG) return fail(c, GPE_ERR_ARG, "bad kernel");
   c->factor_valid = false;
+  c->ainv_valid = false;
   c->x32_valid = false;
   CHK(factor_and_invert(c, kernel, delta, nu, s2, r_scale));
   int info = 0;
@@ -1140,6 +1153,129 @@ int gpe_factor(gpe_ctx* c, int32_t kernel, const double* delta, double nu, doubl
   c->f_kernel = kernel;
   c->f_delta.assign(delta, delta + c->d);
   c->f_nu = nu;
+  return GPE_OK;
+}
+
+// ---------------------------------------------------------------- sensitivity
+// grow a device buffer to at least `need` doubles
+static int grow(gpe_ctx* c, double** p, size_t* cap, size_t need) {
+  if (need <= *cap) return GPE_OK;
+  CHK(dalloc(c, p, need));
+  *cap = need;
+  return GPE_OK;
+}
+
+// A^-1 = L^-T L^-1 of the resident factor into tr.A (the LAUUM launch of the plan)
+static int ensure_ainv(gpe_ctx* c) {
+  if (c->ainv_valid) return GPE_OK;
+  CHK(launch_gemm_range(c, c->tr.plan.launches[c->tr.plan.lauum]));
+  c->ainv_valid = true;
+  return GPE_OK;
+}
+
+int gpe_solve(gpe_ctx* c, int32_t ncols, const double* B, double* X) {
+  CHK(check_ready(c));
+  if (!c->factor_valid) return fail(c, GPE_ERR_STATE, "no resident factor (call gpe_factor)");
+  if (ncols <= 0 || !B || !X) return fail(c, GPE_ERR_ARG, "bad solve args");
+  const long long np = c->n_pad, n = c->n;
+  for (int c0 = 0; c0 < ncols; c0 += SK_PMAX) {
+    const int cc = std::min(SK_PMAX, ncols - c0);
+    CHK(ensure_pinned(c, (size_t)np * cc + 64));
+    std::memset(c->hpin, 0, (size_t)np * cc * sizeof(double));
+    for (long long i = 0; i < n; ++i)
+      for (int k = 0; k < cc; ++k) c->hpin[i + k * np] = B[i * ncols + c0 + k];
+    HIPCHK(c, hipMemcpyAsync(c->dR2, c->hpin, (size_t)np * cc * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    CHK(skinny(c, false, c->tr.B, np, c->NB, c->NB, true, c->dR2, np, cc, c->dZ, np));   // L^-1 B
+    CHK(skinny(c, true, c->tr.B, np, c->NB, c->NB, true, c->dZ, np, cc, c->dWa, np));    // L^-T L^-1 B
+    HIPCHK(c, hipMemcpyAsync(c->hpin, c->dWa, (size_t)np * cc * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (long long i = 0; i < n; ++i)
+      for (int k = 0; k < cc; ++k) X[i * ncols + c0 + k] = c->hpin[i + k * np];
+  }
+  return GPE_OK;
+}
+
+int gpe_sense_pairs(gpe_ctx* c, int32_t J, const double* w, const double* u, int32_t p, const double* Z,
+                    double* trace_out, double* quad_out) {
+  CHK(check_ready(c));
+  if (!c->factor_valid) return fail(c, GPE_ERR_STATE, "no resident factor (call gpe_factor)");
+  if (J <= 0 || J > 65535 || p <= 0 || !w || !u || !Z || !trace_out || !quad_out)
+    return fail(c, GPE_ERR_ARG, "bad sense_pairs args");
+  const int d = c->d;
+  const int need_d = std::max(d, p - 2);
+  if (d > 32 || p > 34) return fail(c, GPE_ERR_UNSUPPORTED, "sense_pairs supports d <= 32, p <= 34");
+  const long long np = c->n_pad, n = c->n;
+  const int NB = c->NB;
+  CHK(ensure_ainv(c));
+  const long long ldp = (long long)J * (1 + p * p);
+  CHK(grow(c, &c->dSU, &c->su_cap, (size_t)J * np));
+  CHK(grow(c, &c->dSZ, &c->sz_cap, (size_t)np * p));
+  CHK(grow(c, &c->dSW, &c->sw_cap, (size_t)J * d));
+  CHK(grow(c, &c->dSpart, &c->spart_cap, (size_t)NB * 4 * ldp));
+  CHK(grow(c, &c->dSout, &c->sout_cap, (size_t)ldp));
+  CHK(ensure_pinned(c, std::max<size_t>({(size_t)J * np, (size_t)np * p, (size_t)J * d, (size_t)ldp}) + 64));
+  // w, u (J x n_pad, zero padded), Z (n_pad x p column-major): staged one at a time
+  std::memcpy(c->hpin, w, (size_t)J * d * sizeof(double));
+  HIPCHK(c, hipMemcpyAsync(c->dSW, c->hpin, (size_t)J * d * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::memset(c->hpin, 0, (size_t)J * np * sizeof(double));
+  for (int j = 0; j < J; ++j) std::memcpy(c->hpin + (size_t)j * np, u + (size_t)j * n, (size_t)n * sizeof(double));
+  HIPCHK(c, hipMemcpyAsync(c->dSU, c->hpin, (size_t)J * np * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::memset(c->hpin, 0, (size_t)np * p * sizeof(double));
+  for (long long i = 0; i < n; ++i)
+    for (int k = 0; k < p; ++k) c->hpin[i + k * np] = Z[i * p + k];
+  HIPCHK(c, hipMemcpyAsync(c->dSZ, c->hpin, (size_t)np * p * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  const dim3 grid((unsigned)NB, (unsigned)J);
+#define SENSE_LAUNCH(DM, PM)                                                                              \
+  hipLaunchKernelGGL((k_sense_pairs<DM, PM>), grid, dim3(256), 0, c->stream, c->tr.A, np, c->dX, d, c->dSW, \
+                     c->dSU, np, c->dSZ, np, p, (int)n, c->dSpart, ldp)
+  if (need_d <= 4) SENSE_LAUNCH(4, 6);
+  else if (need_d <= 8) SENSE_LAUNCH(8, 10);
+  else if (need_d <= 16) SENSE_LAUNCH(16, 18);
+  else SENSE_LAUNCH(32, 34);
+#undef SENSE_LAUNCH
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(k_reduce_rows, dim3((unsigned)ldp), dim3(256), 0, c->stream, c->dSpart, NB * 4, (int)ldp,
+                     c->dSout);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->hpin, c->dSout, (size_t)ldp * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (int j = 0; j < J; ++j) {
+    const double* o = c->hpin + (size_t)j * (1 + p * p);
+    trace_out[j] = o[0];
+    std::memcpy(quad_out + (size_t)j * p * p, o + 1, (size_t)p * p * sizeof(double));
+  }
+  return GPE_OK;
+}
+
+int gpe_gauss_transform(gpe_ctx* c, int64_t m, int32_t ns, const int32_t* dims, const double* cw, const double* Y,
+                        const double* a, double* out) {
+  CHK(check_ready(c));
+  if (m <= 0 || m > (int64_t)1 << 30 || ns <= 0 || ns > 4 || !dims || !cw || !Y || !a || !out)
+    return fail(c, GPE_ERR_ARG, "bad gauss_transform args");
+  for (int s = 0; s < ns; ++s)
+    if (dims[s] < 0 || dims[s] >= c->d) return fail(c, GPE_ERR_ARG, "dims out of range");
+  const long long n = c->n;
+  // device layout: a (n) | Y (m x ns) | out (m)
+  const size_t need = (size_t)n + (size_t)m * ns + (size_t)m;
+  CHK(grow(c, &c->dSout, &c->sout_cap, need));
+  CHK(ensure_pinned(c, need + 64));
+  std::memcpy(c->hpin, a, (size_t)n * sizeof(double));
+  std::memcpy(c->hpin + n, Y, (size_t)m * ns * sizeof(double));
+  HIPCHK(c, hipMemcpyAsync(c->dSout, c->hpin, (n + (size_t)m * ns) * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  GaussArgs g;
+  g.x = c->dX; g.a = c->dSout; g.Y = c->dSout + n; g.out = c->dSout + n + (size_t)m * ns;
+  g.d = c->d; g.n = (int)n; g.m = (int)m; g.ns = ns;
+  for (int s = 0; s < 4; ++s) {
+    g.dims[s] = s < ns ? dims[s] : 0;
+    g.c[s] = s < ns ? cw[s] : 0.0;
+  }
+  hipLaunchKernelGGL(k_gauss_transform, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, c->stream, g);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->hpin, g.out, (size_t)m * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::memcpy(out, c->hpin, (size_t)m * sizeof(double));
   return GPE_OK;
 }
 

@@ -1439,6 +1439,124 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
   }
 }
 
+// ---------------------------------------------------------------------------
+// sensitivity pair sums (reference sensitivity/_sensitivityclasses.py:90-102 Rtt,
+// :599-626 P_prod / Pw): J Gaussian pair kernels on the raw training inputs x,
+//   K_j(k,l) = u_j[k] u_j[l] exp(-sum_i w_j[i] (x_ki - x_li)^2),
+// never stored: each is contracted with A^-1 (lower tiles; off-diagonal pairs
+// twice) and applied to Z (n x p, column-major): V = K_j Z, quad = Z^T V.
+// grid (NB, J): row block ti of 128 rows, two threads per row split the columns.
+// part[(ti*4 + wave) * ldp + j*(1+p*p)] = trace part, then the p*p quad part.
+// ---------------------------------------------------------------------------
+constexpr int SP_CT = 64;   // columns staged in LDS per pass
+template <int DMAX, int PMAX>
+static __global__ void __launch_bounds__(256) k_sense_pairs(const double* Ainv, long long lda, const double* x,
+                                                           int d, const double* w, const double* u,
+                                                           long long ldu, const double* Z, long long ldz,
+                                                           int p, int n_valid, double* part, long long ldp) {
+  __shared__ double xs[SP_CT * DMAX];
+  __shared__ double zs[SP_CT * PMAX];
+  __shared__ double us[SP_CT];
+  const int ti = blockIdx.x, j = blockIdx.y, tid = threadIdx.x;
+  const int r = tid & (TILE - 1), h = tid >> 7;
+  const int gi = ti * TILE + r;
+  const bool rv = gi < n_valid;
+  double xi[DMAX], wj[DMAX], v[PMAX];
+#pragma unroll
+  for (int k = 0; k < DMAX; ++k) {
+    xi[k] = (k < d && rv) ? x[(long long)gi * d + k] : 0.0;
+    wj[k] = (k < d) ? w[j * d + k] : 0.0;
+  }
+#pragma unroll
+  for (int q = 0; q < PMAX; ++q) v[q] = 0.0;
+  const double ui = rv ? u[j * ldu + gi] : 0.0;
+  double acc = 0.0;
+  for (int c0 = 0; c0 < n_valid; c0 += SP_CT) {
+    __syncthreads();
+    for (int e = tid; e < SP_CT * d; e += 256) {
+      const int c = e / d, k = e - c * d, g = c0 + c;
+      xs[c * DMAX + k] = g < n_valid ? x[(long long)g * d + k] : 0.0;
+    }
+    for (int e = tid; e < SP_CT * p; e += 256) {
+      const int c = e % SP_CT, k = e / SP_CT, g = c0 + c;
+      zs[c * PMAX + k] = g < n_valid ? Z[g + (long long)k * ldz] : 0.0;
+    }
+    if (tid < SP_CT) us[tid] = (c0 + tid < n_valid) ? u[j * ldu + c0 + tid] : 0.0;
+    __syncthreads();
+    if (rv) {
+      const int cend = min(SP_CT, n_valid - c0);
+      for (int c = h; c < cend; c += 2) {
+        const int gj = c0 + c;
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) {
+          if (k < d) {
+            const double df = xi[k] - xs[c * DMAX + k];
+            s = fma(wj[k] * df, df, s);
+          }
+        }
+        const double K = ui * us[c] * exp(-s);
+#pragma unroll
+        for (int q = 0; q < PMAX; ++q)
+          if (q < p) v[q] = fma(K, zs[c * PMAX + q], v[q]);
+        if (gj <= gi) acc = fma(gj == gi ? K : 2.0 * K, Ainv[gi + (long long)gj * lda], acc);
+      }
+    }
+  }
+  // per-wave partials: trace, then quad(a, b) = sum_rows Z(row, a) V(row, b)
+  const int lane = tid & 63, wave = tid >> 6;
+  double* out = part + (long long)(ti * 4 + wave) * ldp + (long long)j * (1 + p * p);
+  double t = acc;
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
+  if (lane == 0) out[0] = t;
+  for (int a = 0; a < p; ++a) {
+    const double za = rv ? Z[gi + (long long)a * ldz] : 0.0;
+#pragma unroll
+    for (int b = 0; b < PMAX; ++b) {
+      if (b < p) {
+        double s = za * v[b];
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+        if (lane == 0) out[1 + a * p + b] = s;
+      }
+    }
+  }
+}
+
+// Gauss transform over the training inputs (main / interaction effects,
+// _sensitivityclasses.py:628-633 Tw summed against e):
+//   out[t] = sum_k a[k] exp(-sum_s c[s] (Y[t,s] - x[k, dims[s]])^2),  one wave per t
+struct GaussArgs {
+  const double* x;
+  const double* a;
+  const double* Y;
+  double* out;
+  int d, n, m, ns;
+  int dims[4];
+  double c[4];
+};
+static __global__ void __launch_bounds__(256) k_gauss_transform(GaussArgs g) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= g.m) return;
+  double y[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) y[s] = s < g.ns ? g.Y[t * g.ns + s] : 0.0;
+  double acc = 0.0;
+  for (int k = lane; k < g.n; k += 64) {
+    double q = 0.0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (s < g.ns) {
+        const double df = y[s] - g.x[(long long)k * g.d + g.dims[s]];
+        q = fma(g.c[s] * df, df, q);
+      }
+    }
+    acc = fma(g.a[k], exp(-q), acc);
+  }
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+  if (lane == 0) g.out[t] = acc;
+}
+
 // xw(i,k) = X(i,k) / delta_k  for i < n, 0 for padded rows
 static __global__ void k_scale_points(const double* X, const double* inv_delta, int d, int n,
                                int n_pad, double* xw) {

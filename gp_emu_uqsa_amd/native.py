@@ -41,6 +41,10 @@ SIGNATURES = {
     "gpe_beta": (_ct.c_int, [_VP, _D]),
     "gpe_posterior": (_ct.c_int, [_VP, _ct.c_int64, _D, _D, _D, _ct.c_double, _ct.c_int32, _ct.c_int32,
                                   _D, _D]),
+    "gpe_solve": (_ct.c_int, [_VP, _ct.c_int32, _D, _D]),
+    "gpe_sense_pairs": (_ct.c_int, [_VP, _ct.c_int32, _D, _D, _ct.c_int32, _D, _D, _D]),
+    "gpe_gauss_transform": (_ct.c_int, [_VP, _ct.c_int64, _ct.c_int32, _ct.POINTER(_ct.c_int32), _D, _D, _D,
+                                        _D]),
     "gpe_kernel_var": (_ct.c_int, [_VP, _ct.c_int32, _D, _ct.c_int32, _ct.c_double, _ct.c_int32,
                                    _ct.c_int64, _D, _D, _ct.c_double, _D]),
     "gpe_kernel_covar": (_ct.c_int, [_VP, _ct.c_int32, _D, _ct.c_int32, _ct.c_double, _ct.c_int64,
@@ -239,6 +243,46 @@ class Context:
                                            1 if full_var else 0, int(precision), _ptr(mean), _ptr(var)),
                     "gpe_posterior")
         return mean, var
+
+    # -- sensitivity building blocks (resident factor)
+    def solve(self, B):
+        """A^-1 B for the resident factor (B: n or n x k)."""
+        B = _f64(B)
+        vec = B.ndim == 1
+        B2 = B.reshape(self.n, -1)
+        B2 = _np.ascontiguousarray(B2)
+        X = _np.zeros_like(B2)
+        self._check(self.lib.gpe_solve(self._h, B2.shape[1], _ptr(B2), _ptr(X)), "gpe_solve")
+        return X.ravel() if vec else X
+
+    def sense_pairs(self, w, u, Z):
+        """For K_j(k,l) = u[j,k] u[j,l] exp(-sum_i w[j,i] (x_ki - x_li)^2):
+        (tr(A^-1 K_j) for each j, Z^T K_j Z for each j)."""
+        w = _np.ascontiguousarray(_f64(w).reshape(-1, self.d))
+        J = w.shape[0]
+        u = _np.ascontiguousarray(_f64(u).reshape(J, self.n))
+        Z = _np.ascontiguousarray(_f64(Z).reshape(self.n, -1))
+        p = Z.shape[1]
+        tr = _np.zeros(J)
+        quad = _np.zeros((J, p, p))
+        self._check(self.lib.gpe_sense_pairs(self._h, J, _ptr(w), _ptr(u), p, _ptr(Z), _ptr(tr), _ptr(quad)),
+                    "gpe_sense_pairs")
+        return tr, quad
+
+    def gauss_transform(self, dims, c, Y, a):
+        """out[t] = sum_k a[k] exp(-sum_s c[s] (Y[t,s] - x[k, dims[s]])^2)."""
+        dims_a = _np.ascontiguousarray(_np.asarray(dims, dtype=_np.int32).ravel())
+        ns = dims_a.size
+        c = _np.ascontiguousarray(_f64(c).ravel())
+        Y = _np.ascontiguousarray(_f64(Y).reshape(-1, ns))
+        a = _np.ascontiguousarray(_f64(a).ravel())
+        if a.size != self.n or c.size != ns:
+            raise ValueError("gauss_transform: a must have n entries and c one per dimension")
+        out = _np.zeros(Y.shape[0])
+        self._check(self.lib.gpe_gauss_transform(self._h, Y.shape[0], ns,
+                                                 dims_a.ctypes.data_as(_ct.POINTER(_ct.c_int32)), _ptr(c),
+                                                 _ptr(Y), _ptr(a), _ptr(out)), "gpe_gauss_transform")
+        return out
 
     def kernel_var(self, kernel, delta, nu, X, predict=True, r=None, r_scale=0.0):
         X = _f64(X)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GPE_ABI_VERSION 3   /* 3: gpe_dist_objective gained want_grad / grad_out */
+#define GPE_ABI_VERSION 4   /* 3: gpe_dist_objective gained want_grad / grad_out; 4: sensitivity */
 
 enum gpe_status {
     GPE_OK = 0,
@@ -97,6 +97,27 @@ int gpe_beta(gpe_ctx* ctx, double* beta_out);
 int gpe_posterior(gpe_ctx* ctx, int64_t m, const double* Xs, const double* Hs,
                   const double* beta, double sigma, int32_t full_var, int32_t precision,
                   double* mean_out, double* var_out);
+
+/* ---- Sensitivity / UQ building blocks, resident factor --------
+ * Replace the O(n^2) parts of sensitivity/_sensitivityclasses.py (case2): the
+ * solves with emul.training.A (:40-44, :187-189, :436-441, :451-454) and the n x n
+ * pair matrices Rtt (:90-102) and Pw (:599-626), which are never formed here.
+ * Host arrays are row-major; x below is the resident raw training inputs (n x d). */
+
+/* X = A^-1 B  (B, X: n x ncols). */
+int gpe_solve(gpe_ctx* ctx, int32_t ncols, const double* B, double* X);
+
+/* J Gaussian pair kernels K_j(k,l) = u[j,k] u[j,l] exp(-sum_i w[j,i] (x_ki - x_li)^2)
+ * (w: J x d, u: J x n).  trace_out[j] = sum_kl (A^-1)_kl K_j(k,l) = tr(A^-1 K_j);
+ * quad_out[j] = Z^T K_j Z (p x p; Z: n x p, p <= 34, d <= 32). */
+int gpe_sense_pairs(gpe_ctx* ctx, int32_t J, const double* w, const double* u, int32_t p,
+                    const double* Z, double* trace_out, double* quad_out);
+
+/* out[t] = sum_k a[k] exp(-sum_s c[s] (Y[t,s] - x[k, dims[s]])^2), t < m, ns <= 4
+ * (Y: m x ns): the Tw . e sums of main effects (:277-285, ns = 1) and interaction
+ * effects (:353-373, ns = 2).  Needs set_data only. */
+int gpe_gauss_transform(gpe_ctx* ctx, int64_t m, int32_t ns, const int32_t* dims,
+                        const double* c, const double* Y, const double* a, double* out);
 
 /* K.var(X, predict) materialised (m x m, symmetric): _emulatorkernels.py:39-50 /
  * :112-123, plus make_A's r/s2 diagonal (r_scale * r, r may be NULL). */
