@@ -1211,7 +1211,11 @@ int gpe_sense_pairs(gpe_ctx* c, int32_t J, const double* w, const double* u, int
   CHK(grow(c, &c->dSU, &c->su_cap, (size_t)J * np));
   CHK(grow(c, &c->dSZ, &c->sz_cap, (size_t)np * p));
   CHK(grow(c, &c->dSW, &c->sw_cap, (size_t)J * d));
-  CHK(grow(c, &c->dSpart, &c->spart_cap, (size_t)NB * 4 * ldp));
+  // column slices: enough workgroups to fill the chip (>= 2048) when J is small
+  const int nct = (int)((n + SP_CT - 1) / SP_CT);
+  const int CS = std::max(1, std::min(nct, (2048 + NB * J - 1) / (NB * J)));
+  const int cslice = ((nct + CS - 1) / CS) * SP_CT;
+  CHK(grow(c, &c->dSpart, &c->spart_cap, (size_t)NB * CS * 4 * ldp));
   CHK(grow(c, &c->dSout, &c->sout_cap, (size_t)ldp));
   CHK(ensure_pinned(c, std::max<size_t>({(size_t)J * np, (size_t)np * p, (size_t)J * d, (size_t)ldp}) + 64));
   // w, u (J x n_pad, zero padded), Z (n_pad x p column-major): staged one at a time
@@ -1226,18 +1230,18 @@ int gpe_sense_pairs(gpe_ctx* c, int32_t J, const double* w, const double* u, int
   for (long long i = 0; i < n; ++i)
     for (int k = 0; k < p; ++k) c->hpin[i + k * np] = Z[i * p + k];
   HIPCHK(c, hipMemcpyAsync(c->dSZ, c->hpin, (size_t)np * p * sizeof(double), hipMemcpyHostToDevice, c->stream));
-  const dim3 grid((unsigned)NB, (unsigned)J);
+  const dim3 grid((unsigned)NB, (unsigned)J, (unsigned)CS);
 #define SENSE_LAUNCH(DM, PM)                                                                              \
   hipLaunchKernelGGL((k_sense_pairs<DM, PM>), grid, dim3(256), 0, c->stream, c->tr.A, np, c->dX, d, c->dSW, \
-                     c->dSU, np, c->dSZ, np, p, (int)n, c->dSpart, ldp)
+                     c->dSU, np, c->dSZ, np, p, (int)n, cslice, c->dSpart, ldp)
   if (need_d <= 4) SENSE_LAUNCH(4, 6);
   else if (need_d <= 8) SENSE_LAUNCH(8, 10);
   else if (need_d <= 16) SENSE_LAUNCH(16, 18);
   else SENSE_LAUNCH(32, 34);
 #undef SENSE_LAUNCH
   HIPCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(k_reduce_rows, dim3((unsigned)ldp), dim3(256), 0, c->stream, c->dSpart, NB * 4, (int)ldp,
-                     c->dSout);
+  hipLaunchKernelGGL(k_reduce_rows, dim3((unsigned)ldp), dim3(256), 0, c->stream, c->dSpart, NB * CS * 4,
+                     (int)ldp, c->dSout);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(c->hpin, c->dSout, (size_t)ldp * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

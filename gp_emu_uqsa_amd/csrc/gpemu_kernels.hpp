@@ -1445,15 +1445,17 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
 //   K_j(k,l) = u_j[k] u_j[l] exp(-sum_i w_j[i] (x_ki - x_li)^2),
 // never stored: each is contracted with A^-1 (lower tiles; off-diagonal pairs
 // twice) and applied to Z (n x p, column-major): V = K_j Z, quad = Z^T V.
-// grid (NB, J): row block ti of 128 rows, two threads per row split the columns.
-// part[(ti*4 + wave) * ldp + j*(1+p*p)] = trace part, then the p*p quad part.
+// grid (NB, J, CS): row block ti of 128 rows, column slice z of CS (each slice a
+// multiple of SP_CT columns), two threads per row split the slice's columns.
+// part[((ti*CS + z)*4 + wave) * ldp + j*(1+p*p)] = trace part, then the p*p quad part.
 // ---------------------------------------------------------------------------
 constexpr int SP_CT = 64;   // columns staged in LDS per pass
 template <int DMAX, int PMAX>
 static __global__ void __launch_bounds__(256) k_sense_pairs(const double* Ainv, long long lda, const double* x,
                                                            int d, const double* w, const double* u,
                                                            long long ldu, const double* Z, long long ldz,
-                                                           int p, int n_valid, double* part, long long ldp) {
+                                                           int p, int n_valid, int cslice, double* part,
+                                                           long long ldp) {
   __shared__ double xs[SP_CT * DMAX];
   __shared__ double zs[SP_CT * PMAX];
   __shared__ double us[SP_CT];
@@ -1471,7 +1473,8 @@ static __global__ void __launch_bounds__(256) k_sense_pairs(const double* Ainv, 
   for (int q = 0; q < PMAX; ++q) v[q] = 0.0;
   const double ui = rv ? u[j * ldu + gi] : 0.0;
   double acc = 0.0;
-  for (int c0 = 0; c0 < n_valid; c0 += SP_CT) {
+  const int cbeg = blockIdx.z * cslice, cfin = min(n_valid, cbeg + cslice);
+  for (int c0 = cbeg; c0 < cfin; c0 += SP_CT) {
     __syncthreads();
     for (int e = tid; e < SP_CT * d; e += 256) {
       const int c = e / d, k = e - c * d, g = c0 + c;
@@ -1484,7 +1487,7 @@ static __global__ void __launch_bounds__(256) k_sense_pairs(const double* Ainv, 
     if (tid < SP_CT) us[tid] = (c0 + tid < n_valid) ? u[j * ldu + c0 + tid] : 0.0;
     __syncthreads();
     if (rv) {
-      const int cend = min(SP_CT, n_valid - c0);
+      const int cend = min(SP_CT, cfin - c0);
       for (int c = h; c < cend; c += 2) {
         const int gj = c0 + c;
         double s = 0.0;
@@ -1505,7 +1508,7 @@ static __global__ void __launch_bounds__(256) k_sense_pairs(const double* Ainv, 
   }
   // per-wave partials: trace, then quad(a, b) = sum_rows Z(row, a) V(row, b)
   const int lane = tid & 63, wave = tid >> 6;
-  double* out = part + (long long)(ti * 4 + wave) * ldp + (long long)j * (1 + p * p);
+  double* out = part + (long long)((ti * gridDim.z + blockIdx.z) * 4 + wave) * ldp + (long long)j * (1 + p * p);
   double t = acc;
   for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
   if (lane == 0) out[0] = t;
