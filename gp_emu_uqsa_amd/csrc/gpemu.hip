@@ -135,6 +135,12 @@ struct gpe_ctx {
   double* dSout = nullptr;
   size_t su_cap = 0, sz_cap = 0, sw_cap = 0, spart_cap = 0, sout_cap = 0;
 
+  // noise_fit workspace (gpe_noise_sample): Dnew's r, the draws U^T, L U^T, e, z
+  double* dRn = nullptr;
+  size_t rn_cap = 0;
+  double* dNU = nullptr;
+  size_t nu_cap = 0;
+
   // resident factor (gpe_factor)
   bool factor_valid = false;
   bool ainv_valid = false;   // tr.A holds A^-1 (LAUUM of the resident L^-1)
@@ -897,7 +903,7 @@ void gpe_destroy(gpe_ctx* c) {
                     c->dX, c->dXw, c->dF, c->dr, c->tr.A, c->tr.B, c->tr.logdet, c->aux.A, c->aux.B,
                     c->aux.logdet, c->dinvdelta, c->dZ,
                     c->dR2, c->dWa, c->dskp, c->dgpart, c->dgram, c->dT2, c->dcpart, c->dcsum,
-                    c->dW1, c->dW2, c->dW3, c->dXs, c->dXsw, c->dsmall};
+                    c->dW1, c->dW2, c->dW3, c->dXs, c->dXsw, c->dsmall, c->dRn, c->dNU};
   for (double* b : bufs)
     if (b) hipFree(b);
   if (c->dinfo) hipFree(c->dinfo);
@@ -1297,11 +1303,18 @@ int gpe_beta(gpe_ctx* c, double* beta_out) {
   return GPE_OK;
 }
 
-int gpe_posterior(gpe_ctx* c, int64_t m, const double* Xs, const double* Hs, const double* beta,
-                  double sigma, int32_t full_var, int32_t precision, double* mean_out, double* var_out) {
+// Posterior mean and variance (gpe_posterior).  With keep_dev the full variance stays
+// on the device in c->dW3 (ld = m rounded up to TILE, identity padding) and var_out
+// is not written; rnew (m, device copy made here) adds s2 * rnew_scale * rnew to its
+// diagonal: Dnew's own r/s2 in Dnew.A (_emulatorclasses.py:572-575, :625).
+static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double* Hs, const double* beta,
+                          double sigma, int32_t full_var, int32_t precision, double* mean_out, double* var_out,
+                          const double* rnew, double rnew_scale, bool keep_dev) {
   CHK(check_ready(c));
   if (!c->factor_valid) return fail(c, GPE_ERR_STATE, "no resident factor (call gpe_factor)");
-  if (m <= 0 || !Xs || !Hs || !beta || !mean_out || !var_out) return fail(c, GPE_ERR_ARG, "bad posterior args");
+  if (m <= 0 || !Xs || !Hs || !beta || !mean_out || (!var_out && !keep_dev))
+    return fail(c, GPE_ERR_ARG, "bad posterior args");
+  if (keep_dev && (!full_var || m > 16384)) return fail(c, GPE_ERR_ARG, "device-resident variance: full, m <= 16384");
   if (precision != 64 && precision != 32) return fail(c, GPE_ERR_ARG, "precision must be 64 or 32");
   if (precision == 32 && full_var) return fail(c, GPE_ERR_UNSUPPORTED, "precision 32 is for the diagonal variance");
   const bool f32 = precision == 32;
@@ -1497,6 +1510,13 @@ int gpe_posterior(gpe_ctx* c, int64_t m, const double* Xs, const double* Hs, con
         a.xr = c->dXsw; a.xc = c->dXsw; a.out = dC; a.ld = mp; a.d = d;
         a.nr_valid = (int)mc; a.nc_valid = (int)mc; a.mt = mt; a.nt = mt; a.mode = 1 | 2 | 4;
         a.s2 = s2; a.coff = coff; a.cdiag = cdiag; a.rscale = 0.0; a.r = nullptr;
+        if (rnew) {
+          CHK(grow(c, &c->dRn, &c->rn_cap, (size_t)mp));
+          // synchronous copy: hpin is about to be reused for T below
+          HIPCHK(c, hipMemcpy(c->dRn, rnew + s0, (size_t)mc * sizeof(double), hipMemcpyHostToDevice));
+          a.r = c->dRn;
+          a.rscale = s2 * rnew_scale;
+        }
         CHK(launch_pairs(c, a, mt * (mt + 1) / 2));
       }
       std::vector<double> tth((size_t)mp * kq, 0.0);   // column-major mp x kq
@@ -1515,6 +1535,10 @@ int gpe_posterior(gpe_ctx* c, int64_t m, const double* Xs, const double* Hs, con
       CHK(launch_gemm_range(c, L1));
       Launch L2{0, ADHOC_DESC_BASE + 2, 1, mt * mt, 0.0};
       CHK(launch_gemm_range(c, L2));
+      if (keep_dev) {   // drain: the caller reuses the pinned staging buffer
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return GPE_OK;
+      }
       HIPCHK(c, hipStreamSynchronize(c->stream));
       // copy out m x m (col-major == row-major for the symmetric result)
       std::vector<double> hc((size_t)mp * mc);
@@ -1524,6 +1548,71 @@ int gpe_posterior(gpe_ctx* c, int64_t m, const double* Xs, const double* Hs, con
     }
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GPE_OK;
+}
+
+int gpe_posterior(gpe_ctx* c, int64_t m, const double* Xs, const double* Hs, const double* beta,
+                  double sigma, int32_t full_var, int32_t precision, double* mean_out, double* var_out) {
+  return posterior_impl(c, m, Xs, Hs, beta, sigma, full_var, precision, mean_out, var_out, nullptr, 0.0, false);
+}
+
+int gpe_noise_sample(gpe_ctx* c, int64_t m, const double* Xs, const double* Hs, const double* beta,
+                     double sigma, const double* r_new, double r_scale, const double* t, int32_t s,
+                     const double* U, double* mean_out, double* z_out) {
+  CHK(check_ready(c));
+  if (m <= 0 || m > 16384 || s <= 0 || !t || !U || !z_out)
+    return fail(c, GPE_ERR_ARG, "bad noise_sample args (1 <= m <= 16384, s >= 1)");
+  // V = posterior covariance at Xs, left in c->dW3 (mp x mp, identity padding)
+  CHK(posterior_impl(c, m, Xs, Hs, beta, sigma, 1, 64, mean_out, nullptr, r_new, r_scale, true));
+  const long long mp = ((m + TILE - 1) / TILE) * TILE;
+  const int mt = (int)(mp / TILE);
+  const long long sp = ((s + TILE - 1) / TILE) * TILE;
+  const int st = (int)(sp / TILE);
+  // L = chol(V) in the aux workspace (np.linalg.cholesky(post.var), noise_fit.py:131)
+  Fact& F = c->aux;
+  CHK(ensure_fact(c, F, mp));
+  CHK(build_plan(c, F));
+  HIPCHK(c, hipMemcpyAsync(F.A, c->dW3, (size_t)mp * mp * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->dinfo, 0, sizeof(int), c->stream));
+  CHK(potrf(c, F));
+  int info = 0;
+  double logdet = 0.0;
+  CHK(read_info_logdet(c, F, &info, &logdet));
+  if (info != 0) {
+    c->err = "posterior covariance not positive definite (pivot " + std::to_string(info) + ")";
+    return GPE_NOT_PD;
+  }
+  hipLaunchKernelGGL(k_zero_upper_diag_tiles, dim3((unsigned)mt), dim3(256), 0, c->stream, F.A, mp);
+  HIPCHK(c, hipGetLastError());
+  // U^T (mp x sp, column j = draw j, zero padding) and e = t - mean
+  CHK(grow(c, &c->dNU, &c->nu_cap, 2 * (size_t)mp * sp + 2 * (size_t)mp));
+  double* dU = c->dNU;
+  double* dY = c->dNU + (size_t)mp * sp;
+  double* dE = dY + (size_t)mp * sp;
+  double* dZs = dE + mp;
+  CHK(ensure_pinned(c, (size_t)mp * sp + 64));
+  std::memset(c->hpin, 0, (size_t)mp * sp * sizeof(double));
+  for (int j = 0; j < s; ++j) std::memcpy(c->hpin + (size_t)j * mp, U + (size_t)j * m, (size_t)m * sizeof(double));
+  HIPCHK(c, hipMemcpyAsync(dU, c->hpin, (size_t)mp * sp * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::memset(c->hpin, 0, (size_t)mp * sizeof(double));
+  for (long long i = 0; i < m; ++i) c->hpin[i] = t[i] - mean_out[i];
+  HIPCHK(c, hipMemcpyAsync(dE, c->hpin, (size_t)mp * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  // Y = L U^T: the s draws L.dot(u) of noise_fit.py:135-136 as one MFMA GEMM
+  std::vector<GemmProb> pv = {mkprob(F.A, mp, dU, mp, dY, mp, mt, st, (int)mp, G_KEND_TI, 1.0, 0.0)};
+  pv[0].tile_begin = 0;
+  pv[0].ntiles = mt * st;
+  HIPCHK(c, hipMemcpyAsync(c->dprobs + ADHOC_DESC_BASE + 3, pv.data(), sizeof(GemmProb), hipMemcpyHostToDevice,
+                           c->stream));
+  Launch L{3, ADHOC_DESC_BASE + 3, 1, mt * st, 0.0};
+  CHK(launch_gemm_range(c, L));
+  // z_i = sum_j 0.5 (e_i - Y_ij)^2  (noise_fit.py:137)
+  hipLaunchKernelGGL(k_noise_sq, dim3((unsigned)(mp / 256 + 1)), dim3(256), 0, c->stream, dY, mp, s, dE,
+                     (int)m, dZs);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->hpin, dZs, (size_t)m * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::memcpy(z_out, c->hpin, (size_t)m * sizeof(double));
   return GPE_OK;
 }
 

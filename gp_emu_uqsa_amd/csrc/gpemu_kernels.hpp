@@ -1579,4 +1579,30 @@ static __global__ void k_identity_tiles(double* M, long long ld, int t0) {
   }
 }
 
+// zero the strictly-upper part of every diagonal tile (t,t) of a factored matrix, so
+// a G_KEND_TI GEMM can read it as the triangle L
+static __global__ void k_zero_upper_diag_tiles(double* M, long long ld) {
+  double* base = M + (long long)blockIdx.x * TILE * (ld + 1);
+  for (int e = threadIdx.x; e < TILE * TILE; e += blockDim.x) {
+    int i = e & (TILE - 1), j = e >> 7;
+    if (i < j) base[i + (long long)j * ld] = 0.0;
+  }
+}
+
+// z_i = sum_{j<s} 0.5 (e_i - Y(i,j))^2, Y column-major (ld), one thread per row:
+// consecutive threads read consecutive rows of each column (coalesced).  The sum
+// runs in the reference's order j = 0..s-1 (noise_fit.py:134-137).
+static __global__ void __launch_bounds__(256) k_noise_sq(const double* Y, long long ld, int s,
+                                                         const double* e, int m, double* z) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const double ei = e[i];
+  double acc = 0.0;
+  for (int j = 0; j < s; ++j) {
+    const double r = ei - Y[i + (long long)j * ld];
+    acc += 0.5 * (r * r);
+  }
+  z[i] = acc;
+}
+
 }  // namespace gpe

@@ -325,7 +325,8 @@ class Posterior:
 
     mean = H* beta + K*^T A^-1 (f - H beta)
     var  = sigma^2 (A** - K*^T A^-1 K* + T (H^T A^-1 H)^-1 T^T),  T = H* - K*^T A^-1 H
-    with A = Dold.A as the reference holds it.  ``full_var=False`` returns only the
+    with A = Dold.A as the reference holds it and A** = Dnew.A (K.var plus Dnew's r/s2
+    for the alt-nugget kernel).  ``full_var=False`` returns only the
     diagonal (what plot / history matching use) and supports any number of points.
     The reference's ``predict`` flag has no effect (its use is commented out, :621).
     """
@@ -346,6 +347,15 @@ class Posterior:
         ctx.ensure_factor(self.K.kind, self.K.d, float(self.K.n), 1.0, self.Dold.r_scale())
         self.mean, self.var = ctx.posterior(self.Dnew.inputs, self.Dnew.H, self.par.beta,
                                             float(self.par.sigma), full_var=self.full_var)
+        rs = self.Dnew.r_scale()
+        if rs != 0.0:
+            # Dnew.A carries Dnew's own r/s2 on its diagonal (:572-575), so sigma^2 r/s2 is
+            # part of var (:625-631); noise_fit sets it (noise_fit.py:118-121)
+            add = float(self.par.sigma) ** 2 * rs * np.asarray(self.Dnew.r, dtype=float)
+            if self.var.ndim == 2:
+                self.var[np.diag_indices_from(self.var)] += add
+            else:
+                self.var = self.var + add
 
     # reference-compatible pieces
     def make_covar(self):

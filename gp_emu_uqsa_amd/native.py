@@ -41,6 +41,8 @@ SIGNATURES = {
     "gpe_beta": (_ct.c_int, [_VP, _D]),
     "gpe_posterior": (_ct.c_int, [_VP, _ct.c_int64, _D, _D, _D, _ct.c_double, _ct.c_int32, _ct.c_int32,
                                   _D, _D]),
+    "gpe_noise_sample": (_ct.c_int, [_VP, _ct.c_int64, _D, _D, _D, _ct.c_double, _D, _ct.c_double,
+                                     _D, _ct.c_int32, _D, _D, _D]),
     "gpe_solve": (_ct.c_int, [_VP, _ct.c_int32, _D, _D]),
     "gpe_sense_pairs": (_ct.c_int, [_VP, _ct.c_int32, _D, _D, _ct.c_int32, _D, _D, _D]),
     "gpe_gauss_transform": (_ct.c_int, [_VP, _ct.c_int64, _ct.c_int32, _ct.POINTER(_ct.c_int32), _D, _D, _D,
@@ -243,6 +245,28 @@ class Context:
                                            1 if full_var else 0, int(precision), _ptr(mean), _ptr(var)),
                     "gpe_posterior")
         return mean, var
+
+    def noise_sample(self, Xs, Hs, beta, sigma, t, U, r_new=None, r_scale=0.0):
+        """noise_fit's estimation step for the resident factor: the posterior at Xs
+        (full covariance V, plus r_scale * r_new on its diagonal), L = chol(V) and
+        sum_j 0.5 (t - mean - L U[j])^2 over the rows of U (s x m).  Returns
+        (mean, that sum).  NotPositiveDefinite when V is not."""
+        Xs = _f64(Xs)
+        if Xs.ndim == 1:
+            Xs = Xs.reshape(-1, 1)
+        m = Xs.shape[0]
+        Hs = _f64(Hs, (m, self.q))
+        beta = _f64(beta).ravel()
+        t = _f64(t, (m,))
+        U = _f64(U)
+        U = U.reshape(-1, m)
+        rn = None if r_new is None else _f64(r_new, (m,))
+        mean = _np.zeros(m)
+        z = _np.zeros(m)
+        self._check(self.lib.gpe_noise_sample(self._h, m, _ptr(Xs), _ptr(Hs), _ptr(beta), float(sigma),
+                                              _ptr(rn), float(r_scale), _ptr(t), U.shape[0], _ptr(U),
+                                              _ptr(mean), _ptr(z)), "gpe_noise_sample")
+        return mean, z
 
     # -- sensitivity building blocks (resident factor)
     def solve(self, B):

@@ -29,7 +29,8 @@
 extern "C" {
 #endif
 
-#define GPE_ABI_VERSION 4   /* 3: gpe_dist_objective gained want_grad / grad_out; 4: sensitivity */
+#define GPE_ABI_VERSION 5   /* 3: gpe_dist_objective gained want_grad / grad_out; 4: sensitivity;
+                                5: gpe_noise_sample (noise_fit) */
 
 enum gpe_status {
     GPE_OK = 0,
@@ -153,6 +154,20 @@ int gpe_test_gemm(gpe_ctx* ctx, int32_t trans_a, int32_t trans_b, int64_t M, int
  * ms per launch in *ms_out.  Uses its own device buffers. */
 int gpe_bench_gemm(gpe_ctx* ctx, int32_t trans_a, int32_t trans_b, int32_t mt, int32_t nt,
                    int32_t K, int32_t lower, double beta, int32_t reps, double* ms_out);
+
+/* noise_fit's noise-estimation step (noise_fit/noise_fit.py:130-139, :142-150):
+ * the posterior at Xs (m x d, Hs m x q; full m x m covariance V, built on the
+ * device with Dnew's own r/s2 diagonal: r_new (m, or NULL) times r_scale, as in
+ * Dnew.make_A(s2) after Dnew.set_r, _emulatorclasses.py:572-575), L = chol(V),
+ * and for the s draws u_j = U[j, :] (U row-major s x m: the reference's successive
+ * np.random.randn(m) calls) z_out[i] = sum_j 0.5 (t_i - mean_i - (L u_j)_i)^2
+ * (the caller divides by s and applies the log transform).  mean_out (m) is the
+ * posterior mean.  Needs the resident factor of gpe_factor.  m <= 16384.
+ * GPE_NOT_PD when V is not positive definite (np.linalg.cholesky's LinAlgError). */
+int gpe_noise_sample(gpe_ctx* ctx, int64_t m, const double* Xs, const double* Hs,
+                     const double* beta, double sigma, const double* r_new, double r_scale,
+                     const double* t, int32_t s, const double* U, double* mean_out,
+                     double* z_out);
 
 /* Per-phase device time of the most recent gpe_objective call, in ms:
  * [0] K-build, [1] Cholesky, [2] triangular inverse, [3] A^-1 (L^-T L^-1),

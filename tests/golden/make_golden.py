@@ -14,6 +14,9 @@ Fixtures:
   G8 sensitivity_*.npz uncertainty / sensitivity / main + interaction effects / total-effect
                        variance (case2) on the reconstructed toysim3D emulators and on a
                        synthetic untrained n=300, d=4 emulator, with the intermediates
+  G9 noise_fit.npz     seeded noisefit() on a 2-D heteroscedastic data set (n=60): every
+                       posterior and Cholesky of the noise loop, the randn draws, each
+                       z' written to zp-outputs, the final noise-inputs/-outputs and beliefs
 Versions of numpy/scipy used are stored in every file ("meta").
 """
 from __future__ import annotations
@@ -436,9 +439,120 @@ def make_g8():
         shutil.rmtree(tmp)
 
 
+NOISE_DATA_CONFIG = ("beliefs beliefs-data\ninputs INPUTS\noutputs OUTPUTS\ntv_config 10 0 0\n"
+                     "delta_bounds [[0.05,10.0],[0.05,10.00]]\nsigma_bounds [[0.1,3.0]]\n"
+                     "nugget_bounds [[0.001,1.05]]\ntries 3\nconstraints none\n")
+NOISE_NOISE_CONFIG = ("beliefs beliefs-noise\ninputs INPUTS\noutputs zp-outputs\ntv_config 10 0 0\n"
+                      "delta_bounds [[0.05,1.0],[0.05,10.00]]\nsigma_bounds [[0.001,10.0]]\n"
+                      "nugget_bounds [[0.0001,1.0]]\ntries 3\nconstraints bounds\n")
+NOISE_BELIEFS = ("active all\noutput 0\nbasis_str 1.0\nbasis_inf NA\nbeta 1.0\ndelta 1.0 1.0\n"
+                 "sigma 1.0\nnugget 0.00001\nfix_nugget F\nalt_nugget {alt}\nmucm F\n")
+
+
+def noise_fit_files(n=60, seed=3):
+    """The noisefit2D example's configuration (examples/noisefit2D/config-*, beliefs-*)
+    on n points of its 2-D mean + heteroscedastic-noise functions (emulator.py:12-17),
+    drawn from RandomState(seed) instead of an oLHC design.  Writes into the cwd."""
+    rng = np.random.RandomState(seed)
+    X = rng.uniform(size=(n, 2))
+    y = 3.0 * X[:, 0] ** 3 + np.exp(np.cos(10.0 * X[:, 1]) * np.cos(5.0 * X[:, 0]) ** 2)
+    sd = np.abs(0.5 * X[:, 1] * (np.cos(6 * X[:, 0]) ** 2 + 0.1))
+    y = y + sd * rng.normal(size=n)
+    np.savetxt("INPUTS", X)
+    np.savetxt("OUTPUTS", y)
+    with open("config-data", "w") as fh:
+        fh.write(NOISE_DATA_CONFIG)
+    with open("config-noise", "w") as fh:
+        fh.write(NOISE_NOISE_CONFIG)
+    with open("beliefs-data", "w") as fh:
+        fh.write(NOISE_BELIEFS.format(alt="T"))
+    with open("beliefs-noise", "w") as fh:
+        fh.write(NOISE_BELIEFS.format(alt="F"))
+    return X, y
+
+
+def make_g9():
+    """noise_fit: np.random.seed(9); noisefit('config-data',
+    'config-noise', stopat=2, olhcmult=10, samples=50).  The reference is observed, not
+    changed: Posterior, np.linalg.cholesky, np.random.randn and np.savetxt are wrapped
+    only to record what noisefit passes through them.  design_inputs.py:55 needs the
+    np.int alias (removed in NumPy 1.24), restored as in G7."""
+    np.int = int
+    with contextlib.redirect_stdout(io.StringIO()):
+        import gp_emu_uqsa.noise_fit.noise_fit as nf
+    tmp = tempfile.mkdtemp()
+    os.makedirs(os.path.join(tmp, "w"))
+    cwd = os.getcwd()
+    os.chdir(os.path.join(tmp, "w"))
+    posts, chols, draws, zps = [], [], [], []
+    orig_post, orig_chol, orig_randn, orig_savetxt = (emuc.Posterior, np.linalg.cholesky,
+                                                      np.random.randn, np.savetxt)
+
+    class RecPosterior(orig_post):
+        def __init__(self, Dnew, Dold, par, beliefs, K, predict=True):
+            super().__init__(Dnew, Dold, par, beliefs, K, predict)
+            if Dnew.outputs is None:        # the noise loop's posteriors (train's have outputs)
+                posts.append(dict(xs=np.copy(Dnew.inputs), rs=np.copy(Dnew.r) * np.ones(1),
+                                  As_diag=np.copy(np.diag(Dnew.A)),
+                                  x=np.copy(Dold.inputs), f=np.copy(Dold.outputs),
+                                  r=np.copy(Dold.r) * np.ones(1), A_diag=np.copy(np.diag(Dold.A)),
+                                  delta=np.copy(par.delta), nugget=np.array(par.nugget),
+                                  sigma=np.array(par.sigma), beta=np.copy(par.beta),
+                                  alt=np.array(beliefs.alt_nugget == "T"),
+                                  mean=np.copy(self.mean), var=np.copy(self.var)))
+
+    def rec_chol(a):
+        L = orig_chol(a)
+        if posts and np.shape(a) == posts[-1]["var"].shape and np.array_equal(a, posts[-1]["var"]):
+            chols.append(np.copy(L))        # the noise loop's, not the objective's
+        return L
+
+    def rec_randn(*a):
+        u = orig_randn(*a)
+        draws.append(np.copy(u))
+        return u
+
+    def rec_savetxt(fname, X, *a, **k):
+        if fname == "zp-outputs":
+            zps.append(np.copy(X))
+        return orig_savetxt(fname, X, *a, **k)
+
+    try:
+        X, y = noise_fit_files()
+        emuc.Posterior, np.linalg.cholesky, np.random.randn, np.savetxt = (
+            RecPosterior, rec_chol, rec_randn, rec_savetxt)
+        np.random.seed(9)
+        quiet(nf.noisefit, "config-data", "config-noise", stopat=2, olhcmult=10, samples=50)
+        emuc.Posterior, np.linalg.cholesky, np.random.randn, np.savetxt = (
+            orig_post, orig_chol, orig_randn, orig_savetxt)
+        out = {"X": X, "y": y, "noise_inputs": np.loadtxt("noise-inputs"),
+               "noise_outputs": np.loadtxt("noise-outputs"), "x_range": np.loadtxt("x_range_input"),
+               "n_post": np.array(len(posts)), "n_draws": np.array(len(draws)),
+               "n_chol": np.array(len(chols))}
+        for i, z in enumerate(zps):
+            out[f"zp{i}"] = z
+        for i, p in enumerate(posts):
+            for k, v in p.items():
+                out[f"p{i}_{k}"] = v
+        for i, L in enumerate(chols):
+            out[f"chol{i}"] = L
+        out["draws"] = np.concatenate([np.ravel(u) for u in draws])
+        out["draw_sizes"] = np.array([np.size(u) for u in draws])
+        for f in ("config-data", "config-noise", "beliefs-data", "beliefs-noise"):
+            out["in_" + f.replace("-", "_")] = np.array(open(f).read())
+        for f in ("beliefs-data-0f", "beliefs-noise-0f"):
+            out[f.replace("-", "_")] = np.array(open(f).read())
+        save("noise_fit.npz", **out)
+    finally:
+        emuc.Posterior, np.linalg.cholesky, np.random.randn, np.savetxt = (
+            orig_post, orig_chol, orig_randn, orig_savetxt)
+        os.chdir(cwd)
+        shutil.rmtree(tmp)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["G1", "G2", "G3", "G4", "G5", "G6", "G7", "G8"]
+    which = sys.argv[1:] or ["G1", "G2", "G3", "G4", "G5", "G6", "G7", "G8", "G9"]
     for w in which:
         print("==", w)
         {"G1": make_g1, "G2": make_g2, "G3": make_g3, "G4": make_g4, "G5": make_g5,
-         "G6": make_g6, "G7": make_g7, "G8": make_g8}[w]()
+         "G6": make_g6, "G7": make_g7, "G8": make_g8, "G9": make_g9}[w]()
