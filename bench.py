@@ -1,10 +1,12 @@
 """Headline benchmark: log-marginal-likelihood evals/s at n=16384, d=10, fp64.
 
-One step = one evaluation of the reference objective (loglikelihood_gp4ml,
-_emulatoroptimise.py:412-493) returning (LLH, gradient) -- the unit L-BFGS-B
+The unit is one evaluation of the reference objective (loglikelihood_gp4ml,
+_emulatoroptimise.py:412-493) returning (LLH, gradient) -- what L-BFGS-B
 consumes with jac=True -- on synthetic oLHC data: std Gaussian
-kernel, nugget fitted, gp4ml, 12 hyperparameters, evaluated at delta=1, nu=1e-3,
-sigma=1 (rank r evaluates its own point: a different multistart chain).
+kernel, nugget fitted, gp4ml, 12 hyperparameters, at delta near 1, nu=1e-3,
+sigma=1.  Each GPU keeps --concurrent (default 2) multistart tries in flight, as
+g.train() does at this size: one context (HIP stream, workspaces) and one host
+thread per try, each at its own point.  One step = one evaluation of every try.
 
 Multi-GPU: `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`
 runs one replica per GPU (independent multistart evaluations, no data-path
@@ -24,6 +26,7 @@ import glob
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -45,6 +48,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true",
                     help="time without per-launch HIP events (roofline omitted)")
+    ap.add_argument("--concurrent", type=int, default=2,
+                    help="multistart tries in flight per GPU (own context and HIP stream each), "
+                         "as g.train() runs them at this size (optimize.Optimize._concurrency)")
     return ap.parse_args()
 
 
@@ -113,11 +119,17 @@ def main():
     from gp_emu_uqsa_amd import native
     from gp_emu_uqsa_amd import synthetic
 
-    ctx = native.Context(local)
+    K = max(1, args.concurrent)
     X, f, H = synthetic.problem(args.n, args.d, seed=0)
-    ctx.set_data(X, f, H)
-    hp = eval_point(args.d, rank)
+    ctxs = []
+    for k in range(K):
+        c = native.Context(local)
+        c.set_data(X, f, H)
+        ctxs.append(c)
+    ctx = ctxs[0]
+    hps = [eval_point(args.d, rank * K + k) for k in range(K)]   # one multistart point per try
     prof = not args.no_profile
+    last = [None] * K
 
     def sync_all():
         if have_torch_gpu:
@@ -125,42 +137,61 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        ctx.objective(native.GP4ML, native.KERNEL_STD, hp)
+    def run_tries(count):
+        """Each of the K contexts evaluates `count` times, all K in flight at once
+        (one host thread per context; ctypes releases the GIL during the call)."""
+        def work(k):
+            for _ in range(count):
+                last[k] = ctxs[k].objective(native.GP4ML, native.KERNEL_STD, hps[k])
+        if K == 1:
+            work(0)
+            return
+        th = [threading.Thread(target=work, args=(k,)) for k in range(K)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+
+    run_tries(args.warmup)
     gemm_ms = gemm_fl = gemm_n = 0.0
     phase_acc = {}
     prof_steps = 0
     sync_all()
     t0 = time.perf_counter()
-    for step in range(args.steps):
-        # HIP events around every GEMM launch cost ~1.5 ms per eval; they are
-        # recorded live inside the timed region on its last step only
-        on = prof and step == args.steps - 1
-        if on:
-            ctx.set_profiling(True)
-        llh, grad, _ = ctx.objective(native.GP4ML, native.KERNEL_STD, hp)
-        if on:
-            gs = ctx.gemm_stats()
+    # steps 1..K-1: the K tries concurrently.  The last step evaluates the K tries
+    # one after another with HIP events around every GEMM launch (~1.5 ms per eval),
+    # so the roofline's per-launch times are those of a launch that has the GPU to
+    # itself; that step is inside the timed region, at single-stream speed.
+    run_tries(args.steps - 1 if prof else args.steps)
+    if prof:
+        for k in range(K):
+            ctxs[k].set_profiling(True)
+            last[k] = ctxs[k].objective(native.GP4ML, native.KERNEL_STD, hps[k])
+            gs = ctxs[k].gemm_stats()
             gemm_ms += gs["ms"]
             gemm_fl += gs["flops"]
             gemm_n += gs["launches"]
-            for k, v in ctx.phase_times().items():
-                phase_acc[k] = phase_acc.get(k, 0.0) + v
+            for key, v in ctxs[k].phase_times().items():
+                phase_acc[key] = phase_acc.get(key, 0.0) + v
             prof_steps += 1
-            ctx.set_profiling(False)
+            ctxs[k].set_profiling(False)
     sync_all()
     elapsed = time.perf_counter() - t0
+    llh = last[0][0]
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    # value-only throughput (outside the timed region, informational)
+    # informational, outside the timed region: one eval alone (latency) and value-only
     t1 = time.perf_counter()
-    ctx.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=False)
+    ctx.objective(native.GP4ML, native.KERNEL_STD, hps[0])
+    single_s = time.perf_counter() - t1
+    t1 = time.perf_counter()
+    ctx.objective(native.GP4ML, native.KERNEL_STD, hps[0], want_grad=False)
     value_only_s = time.perf_counter() - t1
 
     if rank == 0:
-        n_units = world * args.steps
+        n_units = world * args.steps * K
         out = {
             "metric": METRIC,
             "value": n_units / elapsed,
@@ -175,8 +206,9 @@ def main():
             "dtype": "f64",
             "data": "synthetic (oLHC design, toysim3D-style outputs + 0.01 N(0,1) noise)",
             "config": {"workload": f"gp4ml LLH+grad, n={args.n} d={args.d}, std Gaussian kernel, "
-                                   f"nugget fitted ({args.d + 2} hp), one eval per step",
-                       "n": args.n, "d": args.d, "q": args.d + 1,
+                                   f"nugget fitted ({args.d + 2} hp); a step = one eval of each of "
+                                   f"{K} multistart tries in flight per GPU",
+                       "n": args.n, "d": args.d, "q": args.d + 1, "tries_in_flight_per_gpu": K,
                        "parallelism": f"replicas{world}"},
         }
         if prof and gemm_ms > 0:
@@ -188,16 +220,19 @@ def main():
                                "kernel": "k_gemm (fp64 v_mfma_f64_16x16x4_f64)",
                                "flops_per_launch": gemm_fl / gemm_n,
                                "ms_per_launch": gemm_ms / gemm_n}
-            whole = 4398e9 * (args.n / 16384) ** 3 / 1e12   # ~n^3 algorithmic flops per eval
+            whole = K * 4398e9 * (args.n / 16384) ** 3 / 1e12   # ~n^3 algorithmic flops per eval
             out["extra"] = {"phase_ms": {k: v / max(prof_steps, 1) for k, v in phase_acc.items()},
-                            "roofline_sample": f"HIP events around every GEMM launch of timed step {args.steps}",
+                            "roofline_sample": f"HIP events around every GEMM launch of timed step "
+                                               f"{args.steps} (its {K} evals run one at a time)",
                             "eval_tflops_algorithmic": whole / (elapsed / args.steps),
+                            "single_eval_ms": 1000.0 * single_s,
                             "value_only_ms": 1000.0 * value_only_s,
                             "llh": llh}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.d)
         print(json.dumps(out), flush=True)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -386,14 +386,49 @@ _default_ctx = None
 _ctx_lock = _threading.Lock()
 
 
+_tls = _threading.local()
+_extra_ctxs: list = []
+
+
 def default_context() -> Context:
-    """Process-wide context on the GPU chosen by LOCAL_RANK (or 0)."""
+    """The calling thread's bound context (bind_context), else the process-wide
+    context on the GPU chosen by GPEMU_DEVICE / LOCAL_RANK (or 0)."""
+    bound = getattr(_tls, "ctx", None)
+    if bound is not None:
+        return bound
     global _default_ctx
     with _ctx_lock:
         if _default_ctx is None:
             dev = int(_os.environ.get("GPEMU_DEVICE", _os.environ.get("LOCAL_RANK", "0")))
             _default_ctx = Context(dev)
         return _default_ctx
+
+
+class bind_context:
+    """Route default_context() of the current thread to `ctx` inside the block
+    (worker threads of concurrent multistart tries, optimize.py)."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def __enter__(self):
+        self.prev = getattr(_tls, "ctx", None)
+        _tls.ctx = self.ctx
+        return self.ctx
+
+    def __exit__(self, *exc):
+        _tls.ctx = self.prev
+        return False
+
+
+def worker_contexts(k: int) -> list:
+    """k contexts on the default context's GPU: the default one plus k-1 extra,
+    created once and kept (each has its own HIP stream and workspaces)."""
+    base = default_context()
+    with _ctx_lock:
+        while len(_extra_ctxs) < k - 1:
+            _extra_ctxs.append(Context(base.device))
+        return [base] + _extra_ctxs[:k - 1]
 
 
 class DistContext:

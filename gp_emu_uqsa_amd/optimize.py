@@ -12,8 +12,13 @@ exchange) and only the (fun, x) results are gathered -- the guess grid is drawn
 identically on every rank, so the chosen optimum equals the sequential one.
 With distributed.enable_objective() each evaluation is instead spread over all
 ranks (row-block partition) and every rank runs every try in lockstep.
+On one GPU, large problems run two tries at a time on two contexts
+(Optimize._concurrency): the evaluations' idle CUs overlap.
 """
 from __future__ import annotations
+
+import os
+import threading
 
 import numpy as np
 from scipy.optimize import minimize
@@ -124,6 +129,59 @@ class Optimize:
             return minimize(fn, x_guess, method="L-BFGS-B", jac=True, bounds=self.cons)
         return minimize(fn, x_guess, method="L-BFGS-B", jac=True)
 
+    def _run_try(self, x_guess):
+        """One L-BFGS-B chain; None when it hit a non-PD matrix (the reference's
+        TypeError -> "Trying next guess" path, :248-251)."""
+        try:
+            res = self._minimize(list(x_guess))
+        except TypeError:
+            return None
+        return (float(res.fun), np.array(res.x, dtype=float), res)
+
+    def _concurrency(self, ntries):
+        """Chains in flight at once on this rank's GPU.  GPEMU_CONCURRENT_TRIES=k
+        forces k (1: sequential); by default 2 when n >= 4096 and there are >= 2
+        tries: one evaluation's latency-bound Cholesky steps leave CUs idle that a
+        second chain's evaluation fills (+10% evaluations/s at n=16384).  Never
+        with the row-block distributed objective (each evaluation is collective)."""
+        if distributed.active_objective() is not None or ntries < 2:
+            return 1
+        env = os.environ.get("GPEMU_CONCURRENT_TRIES")
+        if env is not None:
+            return max(1, min(int(env), ntries))
+        n = self.data.inputs.shape[0]
+        return 2 if 4096 <= n <= 32768 else 1
+
+    def _run_concurrent(self, items, guessgrid, k):
+        """Tries dealt round-robin over k host threads, each bound to its own
+        context (own HIP stream and workspaces) on the same GPU.  Every chain is
+        the same deterministic computation as in the sequential loop, so results
+        are identical; only the wall clock (and the order of "not PSD" messages)
+        changes.  The objective's host-side bookkeeping (K.set_params, par.sigma)
+        is overwritten from the best x after the loop, as in the sequential path."""
+        ctxs = native.worker_contexts(k)
+        r = None if np.isscalar(self.data.r) else self.data.r
+        for c in ctxs:
+            c.ensure_data(self.data.inputs, self.data.outputs, self.data.H, r)
+        results, errors = {}, []
+
+        def work(w):
+            try:
+                with native.bind_context(ctxs[w]):
+                    for C in items[w::k]:
+                        results[C] = self._run_try(guessgrid[:, C])
+            except BaseException as e:   # re-raised on the caller's thread
+                errors.append(e)
+
+        threads = [threading.Thread(target=work, args=(w,)) for w in range(k)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        if errors:
+            raise errors[0]
+        return results
+
     def optimal(self, numguesses, bounds):
         params = self._n_params()
         guessgrid = np.zeros([params, numguesses])
@@ -142,14 +200,14 @@ class Optimize:
 
         if distributed.active_objective() is None:
             upload_training(self.data)
-        results = {}
-        for C in replicas.my_items(numguesses):
-            try:
-                res = self._minimize(list(guessgrid[:, C]))
-            except TypeError:
-                results[C] = None
-                continue
-            results[C] = (float(res.fun), np.array(res.x, dtype=float), res)
+        items = replicas.my_items(numguesses)
+        k = self._concurrency(len(items))
+        if k > 1:
+            results = self._run_concurrent(items, guessgrid, k)
+        else:
+            results = {}
+            for C in items:
+                results[C] = self._run_try(guessgrid[:, C])
         results = replicas.gather_results(results, numguesses)
 
         first_try, best_min, best_x = True, 10000000.0, None

@@ -96,6 +96,8 @@ def main():
            "objective": mode,
            "setup_s": t1 - t0, "train_s": t2 - t1, "objective_evals": calls["n"],
            "objective_s": calls["s"], "s_per_eval": calls["s"] / max(calls["n"], 1),
+           "evals_per_s_of_train": calls["n"] / (t2 - t1),
+           "concurrent_tries": os.environ.get("GPEMU_CONCURRENT_TRIES", "default"),
            "delta": np.asarray(E.par.delta).tolist(), "nugget": float(E.par.nugget),
            "sigma": float(E.par.sigma)}
     if rank == 0:
