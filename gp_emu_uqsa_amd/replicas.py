@@ -11,14 +11,17 @@ runs locally in order.
 """
 from __future__ import annotations
 
+import sys
+
 
 def _group():
     from . import distributed
     if distributed.active_objective() is not None:
         return None   # collective objective: every rank runs every unit in lockstep
-    try:
-        import torch.distributed as dist
-    except Exception:  # torch absent: single process
+    # a process group exists only if the caller imported torch.distributed and
+    # initialised it; importing torch here would cost seconds per train()
+    dist = sys.modules.get("torch.distributed")
+    if dist is None:
         return None
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         return dist

@@ -20,7 +20,7 @@ for counter in ("FETCH_SIZE", "WRITE_SIZE"):
     odir = os.path.join(root, "gpurun_out", f"pmc_{counter}")
     cmd = ["rocprofv3", "--pmc", counter, "-d", odir, "-o", "run", "--output-format", "csv", "--",
            sys.executable, os.path.join(root, "tools", "prof_objective.py"), str(n), str(d), "1"]
-    subprocess.run(cmd, check=True, cwd=root, env=dict(os.environ, TMPDIR="/tmp"))
+    subprocess.run(cmd, check=True, cwd=root, env=dict(os.environ, TMPDIR="/tmp"), timeout=180)
     files = glob.glob(os.path.join(odir, "**", "*counter_collection*.csv"), recursive=True)
     tot, launches = 0.0, set()
     for f in files:
