@@ -107,6 +107,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("GPEMU_BENCH_ONE_DEVICE") == "1":
+        local = 0   # rehearsal of the N-rank path with every rank on GPU 0 (one-GPU box)
     dist = None
     if world > 1:
         import torch.distributed as dist
