@@ -64,10 +64,10 @@ def cpu_baseline(d):
     """Op-for-op NumPy/SciPy restatement of the reference objective (oracle
     ref-mode: pdist/squareform, np.linalg.cholesky, LU-based np.linalg.solve for
     every triangular solve, one dense dA per hyperparameter) timed once at
-    n=2048 and once at n=4096 on this host; the n=16384 time is extrapolated
-    with the exponent fitted between them, t ~ n^p.  (In the survey container the
-    reference itself measured 45.8 s at n=4096 and 1230.7 s at n=16384, i.e.
-    p = 2.38 over that range.)"""
+    n=1536 and once at n=3072 on this host (~30 s of CPU work in all); the
+    n=16384 time is extrapolated with the exponent fitted between them, t ~ n^p.
+    (In the survey container the reference itself measured 45.8 s at n=4096 and
+    1230.7 s at n=16384, i.e. p = 2.38 over that range.)"""
     from oracle import gp_oracle as orc
     try:
         from threadpoolctl import threadpool_info
@@ -76,16 +76,17 @@ def cpu_baseline(d):
     except Exception:
         threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     times = {}
-    for n in (2048, 4096):
+    lo, hi = 1536, 3072
+    for n in (lo, hi):
         X, f, H = orc.synthetic_problem(n, d, seed=0)
         t = time.perf_counter()
         orc.objective_ref(X, f, H, eval_point(d, 0), orc.GP4ML, orc.STD, True)
         times[n] = time.perf_counter() - t
-    p = np.log(times[4096] / times[2048]) / np.log(2.0)
-    t16k = times[4096] * (16384 / 4096) ** p
+    p = np.log(times[hi] / times[lo]) / np.log(hi / lo)
+    t16k = times[hi] * (16384 / hi) ** p
     return {"value": 1.0 / t16k, "unit": "evals/s", "cores": int(threads), "kind": "port",
             "sample": (f"oracle ref-mode (reference op order, NumPy/OpenBLAS, {threads} threads), d={d}: "
-                       f"n=2048 {times[2048]:.2f} s/eval, n=4096 {times[4096]:.2f} s/eval; "
+                       f"n={lo} {times[lo]:.2f} s/eval, n={hi} {times[hi]:.2f} s/eval; "
                        f"n=16384 extrapolated as t ~ n^{p:.2f} -> {t16k:.0f} s/eval")}
 
 

@@ -771,8 +771,24 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
   const GemmProb P = probs[p];
   if (!tiles) {
     const int local = blockIdx.x - P.tile_begin;
-    if (P.flags & G_CLOWER) tri_decode(local, ti, tj);
-    else { ti = local % P.mt; tj = local / P.mt; }
+    if (P.flags & G_CLOWER) {
+      tri_decode(local, ti, tj);
+    } else if ((P.flags & G_KEND_TI) && nprob == 1) {
+      // triangle times a full block (the posterior's L^-1 K*, noise_fit's L U^T):
+      // row ti has K = (ti+1)*128, so rows go longest first, and with mt % 8 == 0
+      // XCD b % 8 takes whole rows (its A panel stays in that XCD's L2); as k_gemm_f32
+      if ((P.mt & 7) == 0) {
+        const int x = local & 7, r = local >> 3;
+        ti = P.mt - 1 - (x + 8 * (r / P.nt));
+        tj = r % P.nt;
+      } else {
+        ti = P.mt - 1 - local / P.nt;
+        tj = local % P.nt;
+      }
+    } else {
+      ti = local % P.mt;
+      tj = local / P.mt;
+    }
   }
   int kbeg = 0, kend = P.K;
   if (P.flags & G_KBEG_TI) kbeg = ti * TILE;
@@ -921,7 +937,20 @@ static __global__ void __launch_bounds__(256, 2) k_gemm_f32(const float* A, long
                                                              long long ldb, float* C, long long ldc, int mt,
                                                              int K, int kend_ti) {
   extern __shared__ __attribute__((aligned(16))) float lds32[];
-  const int ti = blockIdx.x % mt, tj = blockIdx.x / mt;
+  // Tile order: with the triangle (kend_ti), row ti has K = (ti+1)*128, so rows go
+  // longest first (no long tile starts last).  When mt % 8 == 0, workgroup b runs on
+  // XCD b % 8 under round-robin dispatch and that XCD takes rows mt-1-(b%8), -8, ...
+  // whole, so each row's A panel is read into one XCD's L2.
+  const int nt = gridDim.x / mt;
+  int ti, tj;
+  if ((mt & 7) == 0) {
+    const int x = blockIdx.x & 7, r = blockIdx.x >> 3;
+    ti = mt - 1 - (x + 8 * (r / nt));
+    tj = r % nt;
+  } else {
+    ti = mt - 1 - (int)blockIdx.x / nt;
+    tj = (int)blockIdx.x % nt;
+  }
   const int kend = kend_ti ? min(K, (ti + 1) * TILE) : K;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
@@ -935,30 +964,61 @@ static __global__ void __launch_bounds__(256, 2) k_gemm_f32(const float* A, long
     for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   const int nk = kend / F32_GK;
   float ra[16], rb[16];
+  // fragments of k-step ks (4 deep) of the stage at As/Bs
+  auto frags = [&](const float* As, const float* Bs, int ks, float (&af)[4], float (&bf)[4]) {
+    const int krow = 4 * ks + (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = As[krow * F32_PA + wm + i * 16 + (lane & 15)];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = Bs[(wn + j * 16 + (lane & 15)) * F32_PB + krow];
+  };
+  // MFMAs u0 <= u < u1 (u = 4 i + j) of one k-step
+  auto mfmas = [&](int u0, int u1, const float (&af)[4], const float (&bf)[4]) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (u >= u0 && u < u1)
+        acc[u >> 2][u & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(bf[u & 3], af[u >> 2], acc[u >> 2][u & 3], 0, 0, 0);
+  };
+  float fa0[4], fb0[4], fa1[4], fb1[4];
   if (nk > 0) {
     g32_gload(Ab, Bb, lda, ldb, 0, tid, ra, rb);
     g32_sstore(lds32, tid, ra, rb);
     __syncthreads();
+    frags(lds32, lds32 + F32_GK * F32_PA, 0, fa0, fb0);
   }
+  // Software pipeline (as gemm_kloop): the fragments of k-step ks+1 are read before
+  // the 16 MFMAs of k-step ks issue, so their LDS latency hides behind them; at the
+  // stage boundary the last 4 MFMAs wait until the next stage's first fragments
+  // are in flight.  sched_barrier keeps the compiler from regrouping.
   for (int s = 0; s < nk; ++s) {
-    if (s + 1 < nk) g32_gload(Ab, Bb, lda, ldb, (s + 1) * F32_GK, tid, ra, rb);
+    const bool more = s + 1 < nk;
+    if (more) g32_gload(Ab, Bb, lda, ldb, (s + 1) * F32_GK, tid, ra, rb);
     const float* As = lds32 + (s & 1) * F32_STAGE;
     const float* Bs = As + F32_GK * F32_PA;
 #pragma unroll
-    for (int ks = 0; ks < F32_GK / 4; ++ks) {
-      const int krow = 4 * ks + (lane >> 4);
-      float af[4], bf[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = As[krow * F32_PA + wm + i * 16 + (lane & 15)];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bf[j] = Bs[(wn + j * 16 + (lane & 15)) * F32_PB + krow];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bf[j], af[i], acc[i][j], 0, 0, 0);
+    for (int ks = 0; ks < F32_GK / 4; ks += 2) {
+      frags(As, Bs, ks + 1, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(0, 16, fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks + 2 < F32_GK / 4) {
+        frags(As, Bs, ks + 2, fa0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfmas(0, 16, fa1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
-    if (s + 1 < nk) g32_sstore(lds32 + ((s + 1) & 1) * F32_STAGE, tid, ra, rb);
-    __syncthreads();
+    mfmas(0, 12, fa1, fb1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) {
+      g32_sstore(lds32 + ((s + 1) & 1) * F32_STAGE, tid, ra, rb);
+      __syncthreads();
+      const float* An = lds32 + ((s + 1) & 1) * F32_STAGE;
+      frags(An, An + F32_GK * F32_PA, 0, fa0, fb0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas(12, 16, fa1, fb1);
+    __builtin_amdgcn_sched_barrier(0);
   }
   float* Cb = C + (long long)ti * TILE + (long long)tj * TILE * ldc;
 #pragma unroll
