@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true",
                     help="time without per-launch HIP events (roofline omitted)")
+    ap.add_argument("--no-other-configs", dest="other_configs", action="store_false",
+                    help="skip the informational configs[1] / configs[4] timings")
     ap.add_argument("--concurrent", type=int, default=2,
                     help="multistart tries in flight per GPU (own context and HIP stream each), "
                          "as g.train() runs them at this size (optimize.Optimize._concurrency)")
@@ -88,6 +90,38 @@ def cpu_baseline(d):
             "sample": (f"oracle ref-mode (reference op order, NumPy/OpenBLAS, {threads} threads), d={d}: "
                        f"n={lo} {times[lo]:.2f} s/eval, n={hi} {times[hi]:.2f} s/eval; "
                        f"n=16384 extrapolated as t ~ n^{p:.2f} -> {t16k:.0f} s/eval")}
+
+
+def other_configs(native, synthetic, ctx, args):
+    """Informational, after the timed region (rank 0): BASELINE.json configs[1]
+    (n=4096, d=10: one LLH+grad and one value-only evaluation, single stream) and
+    configs[4] (n=16384, d=10 emulator, posterior mean + diagonal variance at m=1e6
+    points, precision 32).  The headline metric stays configs[2]."""
+    out = {}
+    X, f, H = synthetic.problem(4096, 10, seed=0)
+    c = native.Context(ctx.device)
+    c.set_data(X, f, H)
+    hp = eval_point(10, 0)
+    c.objective(native.GP4ML, native.KERNEL_STD, hp)
+    t = time.perf_counter()
+    c.objective(native.GP4ML, native.KERNEL_STD, hp)
+    out["c2_n4096_llh_grad_ms"] = 1000.0 * (time.perf_counter() - t)
+    t = time.perf_counter()
+    c.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=False)
+    out["c2_n4096_value_only_ms"] = 1000.0 * (time.perf_counter() - t)
+    c.close()
+    if args.n == 16384 and args.d == 10:
+        m = 1000000
+        xs = synthetic.design(m, 10, seed=7)
+        hs = synthetic.linear_basis(xs)
+        ctx.factor(native.KERNEL_STD, np.ones(10), 1e-3, 1.0, 0.0)
+        beta = ctx.beta()
+        t = time.perf_counter()
+        ctx.posterior(xs, hs, beta, 1.0, full_var=False, precision=32)
+        dt = time.perf_counter() - t
+        out["c5_posterior_fp32_points_per_s"] = m / dt
+        out["c5_posterior_fp32_s"] = dt
+    return out
 
 
 def pmc_traffic(n, d):
@@ -192,6 +226,7 @@ def main():
     t1 = time.perf_counter()
     ctx.objective(native.GP4ML, native.KERNEL_STD, hps[0], want_grad=False)
     value_only_s = time.perf_counter() - t1
+    other = other_configs(native, synthetic, ctx, args) if (rank == 0 and args.other_configs) else None
 
     if rank == 0:
         n_units = world * args.steps * K
@@ -230,6 +265,7 @@ def main():
                             "eval_tflops_algorithmic": whole / (elapsed / args.steps),
                             "single_eval_ms": 1000.0 * single_s,
                             "value_only_ms": 1000.0 * value_only_s,
+                            "other_configs": other,
                             "llh": llh}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.d)
