@@ -1669,6 +1669,56 @@ int gpe_kernel_var(gpe_ctx* c, int32_t kernel, const double* delta, int32_t d, d
   return rc;
 }
 
+int gpe_kernel_grad(gpe_ctx* c, const double* delta, int32_t d, int64_t m, const double* X,
+                    const double* col, double col_scale, double pre, double* G_out) {
+  if (!c) return GPE_ERR_ARG;
+  if (!delta || !X || !G_out || m <= 0 || d <= 0 || d > 32) return fail(c, GPE_ERR_ARG, "bad kernel_grad args");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const long long mp = ((m + TILE - 1) / TILE) * TILE;
+  const int mt = (int)(mp / TILE);
+  double *dx = nullptr, *dxw = nullptr, *dout = nullptr, *dcol = nullptr;
+  CHK(dalloc(c, &dx, (size_t)mp * d));
+  CHK(dalloc(c, &dxw, (size_t)mp * d));
+  int rc = dalloc(c, &dout, (size_t)mp * mp);
+  if (rc == GPE_OK && col) rc = dalloc(c, &dcol, (size_t)mp);
+  if (rc == GPE_OK) rc = ensure_pinned(c, (size_t)mp * d + 64 + (size_t)mp);
+  if (rc == GPE_OK) {
+    std::memset(c->hpin, 0, (size_t)mp * d * sizeof(double));
+    std::memcpy(c->hpin, X, (size_t)m * d * sizeof(double));
+    for (int k = 0; k < d; ++k) c->hpin[(size_t)mp * d + k] = 1.0 / delta[k];
+    (void)hipMemcpy(dx, c->hpin, (size_t)mp * d * sizeof(double), hipMemcpyHostToDevice);
+    (void)hipMemcpy(c->dinvdelta, c->hpin + (size_t)mp * d, d * sizeof(double), hipMemcpyHostToDevice);
+    if (col) {
+      std::memset(c->hpin, 0, (size_t)mp * sizeof(double));
+      std::memcpy(c->hpin, col, (size_t)m * sizeof(double));
+      (void)hipMemcpy(dcol, c->hpin, (size_t)mp * sizeof(double), hipMemcpyHostToDevice);
+    }
+    const long long tot = mp * d;
+    hipLaunchKernelGGL(k_scale_points, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
+                       dx, c->dinvdelta, d, (int)m, (int)mp, dxw);
+    PairArgs a;
+    a.xr = dxw; a.xc = dxw; a.out = dout; a.ld = mp; a.d = d; a.nr_valid = (int)m; a.nc_valid = (int)m;
+    a.mt = mt; a.nt = mt; a.mode = 1 | 4 | 8;
+    a.s2 = 1.0; a.coff = pre; a.cdiag = 0.0; a.rscale = 0.0; a.r = nullptr;
+    a.fcol = dcol; a.fscale = col_scale;
+    rc = launch_pairs(c, a, mt * (mt + 1) / 2);
+    if (rc == GPE_OK) {
+      hipError_t e = hipStreamSynchronize(c->stream);
+      if (e != hipSuccess) rc = fail(c, GPE_ERR_HIP, hipGetErrorString(e));
+    }
+    if (rc == GPE_OK) {
+      for (long long j = 0; j < m; ++j)
+        (void)hipMemcpy(G_out + j * m, dout + j * mp, (size_t)m * sizeof(double), hipMemcpyDeviceToHost);
+    }
+  }
+  (void)hipFree(dx);
+  (void)hipFree(dxw);
+  if (dout) hipFree(dout);
+  if (dcol) hipFree(dcol);
+  return rc;
+}
+
 int gpe_kernel_covar(gpe_ctx* c, int32_t kernel, const double* delta, int32_t d, double nu,
                      int64_t n, const double* XT, int64_t m, const double* XV, double* C_out) {
   if (!c) return GPE_ERR_ARG;

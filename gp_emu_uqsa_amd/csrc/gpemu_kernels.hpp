@@ -34,6 +34,9 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // mode bit1: "training" diagonal/padding rules: gi==gj -> s2*cdiag + rscale*r[gi];
 //            gi or gj >= n_valid -> identity.  Without bit1 padded -> 0.
 // mode bit2: mirror: also write out(j,i) (full symmetric materialisation)
+// mode bit3: zero diagonal (the reference's dA matrices, _emulatorkernels.py:53-71)
+// fcol: if set, every entry is also multiplied by ((fcol[gi] - fcol[gj]) * fscale)^2
+// (dA/d(2 log delta_i): the per-dimension squared distance, :53-63)
 // ---------------------------------------------------------------------------
 struct PairArgs {
   const double* xr;   // rows point set, row-major [*, d]
@@ -43,6 +46,8 @@ struct PairArgs {
   int d, nr_valid, nc_valid, mt, nt, mode;
   double s2, coff, cdiag, rscale;
   const double* r;
+  const double* fcol = nullptr;
+  double fscale = 0.0;
 };
 
 __device__ inline void tri_decode(int e, int& ti, int& tj) {
@@ -92,7 +97,12 @@ static __global__ void __launch_bounds__(256) k_pairs(PairArgs a) {
         }
       }
       v = pre * exp(-s);
+      if (a.fcol) {
+        const double df = (a.fcol[gi] - a.fcol[gj]) * a.fscale;
+        v *= df * df;
+      }
     }
+    if ((a.mode & 8) && gi == gj) v = 0.0;
     a.out[(long long)gi + (long long)gj * a.ld] = v;
     if ((a.mode & 4) && ti != tj) a.out[(long long)gj + (long long)gi * a.ld] = v;
   }

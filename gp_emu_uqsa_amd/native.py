@@ -51,6 +51,7 @@ SIGNATURES = {
                                    _ct.c_int64, _D, _D, _ct.c_double, _D]),
     "gpe_kernel_covar": (_ct.c_int, [_VP, _ct.c_int32, _D, _ct.c_int32, _ct.c_double, _ct.c_int64,
                                      _D, _ct.c_int64, _D, _D]),
+    "gpe_kernel_grad": (_ct.c_int, [_VP, _D, _ct.c_int32, _ct.c_int64, _D, _D, _ct.c_double, _ct.c_double, _D]),
     "gpe_cholesky": (_ct.c_int, [_VP, _ct.c_int64, _D, _D, _D, _D, _D]),
     "gpe_test_gemm": (_ct.c_int, [_VP, _ct.c_int32, _ct.c_int32, _ct.c_int64, _ct.c_int64,
                                   _ct.c_int64, _D, _D, _D, _ct.c_double, _ct.c_double]),
@@ -334,6 +335,20 @@ class Context:
         out = _np.zeros((n, m))
         self._check(self.lib.gpe_kernel_covar(self._h, int(kernel), _ptr(delta), d, float(nu), n,
                                               _ptr(XT), m, _ptr(XV), _ptr(out)), "gpe_kernel_covar")
+        return out
+
+    def kernel_grad(self, delta, X, col, col_scale, pre):
+        """pre * ((col_k - col_l) col_scale)^2 * exp(-|(x_k - x_l)/delta|^2), zero
+        diagonal (col None: no squared factor); m x m."""
+        X = _f64(X)
+        if X.ndim == 1:
+            X = X.reshape(-1, 1)
+        m, d = X.shape
+        delta = _f64(delta).ravel()
+        cc = None if col is None else _f64(col, (m,))
+        out = _np.zeros((m, m))
+        self._check(self.lib.gpe_kernel_grad(self._h, _ptr(delta), d, m, _ptr(X), _ptr(cc),
+                                             float(col_scale), float(pre), _ptr(out)), "gpe_kernel_grad")
         return out
 
     def cholesky(self, A, want=("L",)):

@@ -29,8 +29,8 @@
 extern "C" {
 #endif
 
-#define GPE_ABI_VERSION 5   /* 3: gpe_dist_objective gained want_grad / grad_out; 4: sensitivity;
-                                5: gpe_noise_sample (noise_fit) */
+#define GPE_ABI_VERSION 6   /* 3: gpe_dist_objective gained want_grad / grad_out; 4: sensitivity;
+                                5: gpe_noise_sample (noise_fit); 6: gpe_kernel_grad */
 
 enum gpe_status {
     GPE_OK = 0,
@@ -125,6 +125,16 @@ int gpe_gauss_transform(gpe_ctx* ctx, int64_t m, int32_t ns, const int32_t* dims
 int gpe_kernel_var(gpe_ctx* ctx, int32_t kernel, const double* delta, int32_t d,
                    double nu, int32_t predict, int64_t m, const double* X,
                    const double* r, double r_scale, double* A_out);
+
+/* The reference's dense derivative matrices, m x m row-major, zero diagonal:
+ *   G(k,l) = pre * ((col_k - col_l) * col_scale)^2 * exp(-sum_i ((X_ki - X_li)/delta_i)^2)
+ * (col NULL: the squared factor is 1).  kernel.grad_delta_A(X[:,i], i, s2)
+ * (_emulatorkernels.py:53-63, alt :126-136): col = X[:,i], col_scale = 1/delta_i,
+ * pre = s2 (1 - nu) (alt: s2), delta / X those of the preceding var() (its exp_save).
+ * kernel.grad_nugget_A (std :66-71): col NULL, pre = -nu s2 / 2.  (The alt-nugget
+ * form, s2 nu^2 I, is diagonal and built by the host.) */
+int gpe_kernel_grad(gpe_ctx* ctx, const double* delta, int32_t d, int64_t m, const double* X,
+                    const double* col, double col_scale, double pre, double* G_out);
 
 /* K.covar(XT, XV) -> n x m row-major: _emulatorkernels.py:75-79 / :148-152. */
 int gpe_kernel_covar(gpe_ctx* ctx, int32_t kernel, const double* delta, int32_t d,

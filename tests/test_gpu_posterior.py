@@ -78,3 +78,29 @@ def test_posterior_precision32_diagonal(ctx):
     assert np.max(np.abs(v32 - v64)) < 2e-5 * 0.81, np.max(np.abs(v32 - v64))
     with pytest.raises(RuntimeError):
         ctx.posterior(xs[:10], hs[:10], beta, 0.9, full_var=True, precision=32)
+
+
+@pytest.mark.parametrize("kind", [orc.STD, orc.ALT])
+def test_kernel_gradients_golden(kind):
+    """kernel.grad_delta_A / grad_nugget_A through the kernel objects (gpe_kernel_grad)
+    against the reference's own matrices (G1): exp_save from the preceding var()."""
+    from gp_emu_uqsa_amd import kernels
+
+    z = np.load(os.path.join(GOLD, "kernel_std.npz" if kind == orc.STD else "kernel_alt.npz"))
+
+    class Par:
+        delta = z["delta"]
+        nugget = float(z["nu"])
+
+    K = (kernels.kernel if kind == orc.STD else kernels.kernel_alt_nug)(3, Par)
+    X, s2 = z["X"], float(z["s2"])
+    with pytest.raises(AttributeError):
+        K.grad_delta_A(X[:, 0], 0, s2)          # no var() yet: the reference has no exp_save
+    K.var(X, False)
+    for i in range(3):
+        G = K.grad_delta_A(X[:, i], i, s2)
+        ref = z["grad_delta"][i]
+        assert np.max(np.abs(G - ref)) <= 1e-14 * np.max(np.abs(ref)), i
+    Gn = K.grad_nugget_A(X, s2)
+    refn = z["grad_nugget"]
+    assert np.max(np.abs(Gn - refn)) <= 1e-14 * np.max(np.abs(refn))
