@@ -71,6 +71,14 @@ class Basis:
     def _compile(expr):
         return eval("lambda x: " + expr, {"np": np, "numpy": np, "_np": np})
 
+    def make_h(self, basis_str):
+        """Append one basis function per expression (reference :293-299)."""
+        self.h.extend(self._compile(expr) for expr in basis_str)
+
+    def print_mean_function(self, basis_inf, basis_str, include):
+        """(reference :301-317)"""
+        self._print_mean_function(basis_inf, basis_str, include)
+
     def _print_mean_function(self, basis_inf, basis_str, include):
         meanf = "m(x) ="
         for i in range(len(self.h)):
