@@ -1616,6 +1616,17 @@ int gpe_noise_sample(gpe_ctx* c, int64_t m, const double* Xs, const double* Hs, 
   return GPE_OK;
 }
 
+}  // extern "C"
+
+// hipMemcpy whose failure is kept in rc (the first failure wins, later copies are skipped)
+static void copy_checked(gpe_ctx* c, int& rc, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+  if (rc != GPE_OK) return;
+  const hipError_t e = hipMemcpy(dst, src, bytes, kind);
+  if (e != hipSuccess) rc = fail(c, GPE_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
+}
+
+extern "C" {
+
 int gpe_kernel_var(gpe_ctx* c, int32_t kernel, const double* delta, int32_t d, double nu,
                    int32_t predict, int64_t m, const double* X, const double* r, double r_scale,
                    double* A_out) {
@@ -1636,12 +1647,12 @@ int gpe_kernel_var(gpe_ctx* c, int32_t kernel, const double* delta, int32_t d, d
     std::memset(c->hpin, 0, (size_t)mp * d * sizeof(double));
     std::memcpy(c->hpin, X, (size_t)m * d * sizeof(double));
     for (int k = 0; k < d; ++k) c->hpin[(size_t)mp * d + k] = 1.0 / delta[k];
-    (void)hipMemcpy(dx, c->hpin, (size_t)mp * d * sizeof(double), hipMemcpyHostToDevice);
-    (void)hipMemcpy(c->dinvdelta, c->hpin + (size_t)mp * d, d * sizeof(double), hipMemcpyHostToDevice);
+    copy_checked(c, rc, dx, c->hpin, (size_t)mp * d * sizeof(double), hipMemcpyHostToDevice);
+    copy_checked(c, rc, c->dinvdelta, c->hpin + (size_t)mp * d, d * sizeof(double), hipMemcpyHostToDevice);
     if (r) {
       std::memset(c->hpin, 0, (size_t)mp * sizeof(double));
       std::memcpy(c->hpin, r, (size_t)m * sizeof(double));
-      (void)hipMemcpy(dr, c->hpin, (size_t)mp * sizeof(double), hipMemcpyHostToDevice);
+      copy_checked(c, rc, dr, c->hpin, (size_t)mp * sizeof(double), hipMemcpyHostToDevice);
     }
     const long long tot = mp * d;
     hipLaunchKernelGGL(k_scale_points, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
@@ -1659,7 +1670,7 @@ int gpe_kernel_var(gpe_ctx* c, int32_t kernel, const double* delta, int32_t d, d
     }
     if (rc == GPE_OK) {
       for (long long j = 0; j < m; ++j)
-        (void)hipMemcpy(A_out + j * m, dout + j * mp, (size_t)m * sizeof(double), hipMemcpyDeviceToHost);
+        copy_checked(c, rc, A_out + j * m, dout + j * mp, (size_t)m * sizeof(double), hipMemcpyDeviceToHost);
     }
   }
   (void)hipFree(dx);
@@ -1687,12 +1698,12 @@ int gpe_kernel_grad(gpe_ctx* c, const double* delta, int32_t d, int64_t m, const
     std::memset(c->hpin, 0, (size_t)mp * d * sizeof(double));
     std::memcpy(c->hpin, X, (size_t)m * d * sizeof(double));
     for (int k = 0; k < d; ++k) c->hpin[(size_t)mp * d + k] = 1.0 / delta[k];
-    (void)hipMemcpy(dx, c->hpin, (size_t)mp * d * sizeof(double), hipMemcpyHostToDevice);
-    (void)hipMemcpy(c->dinvdelta, c->hpin + (size_t)mp * d, d * sizeof(double), hipMemcpyHostToDevice);
+    copy_checked(c, rc, dx, c->hpin, (size_t)mp * d * sizeof(double), hipMemcpyHostToDevice);
+    copy_checked(c, rc, c->dinvdelta, c->hpin + (size_t)mp * d, d * sizeof(double), hipMemcpyHostToDevice);
     if (col) {
       std::memset(c->hpin, 0, (size_t)mp * sizeof(double));
       std::memcpy(c->hpin, col, (size_t)m * sizeof(double));
-      (void)hipMemcpy(dcol, c->hpin, (size_t)mp * sizeof(double), hipMemcpyHostToDevice);
+      copy_checked(c, rc, dcol, c->hpin, (size_t)mp * sizeof(double), hipMemcpyHostToDevice);
     }
     const long long tot = mp * d;
     hipLaunchKernelGGL(k_scale_points, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
@@ -1709,7 +1720,7 @@ int gpe_kernel_grad(gpe_ctx* c, const double* delta, int32_t d, int64_t m, const
     }
     if (rc == GPE_OK) {
       for (long long j = 0; j < m; ++j)
-        (void)hipMemcpy(G_out + j * m, dout + j * mp, (size_t)m * sizeof(double), hipMemcpyDeviceToHost);
+        copy_checked(c, rc, G_out + j * m, dout + j * mp, (size_t)m * sizeof(double), hipMemcpyDeviceToHost);
     }
   }
   (void)hipFree(dx);
@@ -1737,13 +1748,13 @@ int gpe_kernel_covar(gpe_ctx* c, int32_t kernel, const double* delta, int32_t d,
   if (rc == GPE_OK) rc = ensure_pinned(c, (size_t)std::max(np, mp) * d + 64);
   if (rc == GPE_OK) {
     for (int k = 0; k < d; ++k) c->hpin[k] = 1.0 / delta[k];
-    (void)hipMemcpy(c->dinvdelta, c->hpin, d * sizeof(double), hipMemcpyHostToDevice);
+    copy_checked(c, rc, c->dinvdelta, c->hpin, d * sizeof(double), hipMemcpyHostToDevice);
     std::memset(c->hpin, 0, (size_t)np * d * sizeof(double));
     std::memcpy(c->hpin, XT, (size_t)n * d * sizeof(double));
-    (void)hipMemcpy(dxt, c->hpin, (size_t)np * d * sizeof(double), hipMemcpyHostToDevice);
+    copy_checked(c, rc, dxt, c->hpin, (size_t)np * d * sizeof(double), hipMemcpyHostToDevice);
     std::memset(c->hpin, 0, (size_t)mp * d * sizeof(double));
     std::memcpy(c->hpin, XV, (size_t)m * d * sizeof(double));
-    (void)hipMemcpy(dxv, c->hpin, (size_t)mp * d * sizeof(double), hipMemcpyHostToDevice);
+    copy_checked(c, rc, dxv, c->hpin, (size_t)mp * d * sizeof(double), hipMemcpyHostToDevice);
     hipLaunchKernelGGL(k_scale_points, dim3((unsigned)((np * d + 255) / 256)), dim3(256), 0, c->stream,
                        dxt, c->dinvdelta, d, (int)n, (int)np, dxtw);
     hipLaunchKernelGGL(k_scale_points, dim3((unsigned)((mp * d + 255) / 256)), dim3(256), 0, c->stream,
@@ -1762,7 +1773,7 @@ int gpe_kernel_covar(gpe_ctx* c, int32_t kernel, const double* delta, int32_t d,
     if (rc == GPE_OK) {
       // dout column j (= training point j) holds C[j, 0:m]
       for (long long j = 0; j < n; ++j)
-        (void)hipMemcpy(C_out + j * m, dout + j * mp, (size_t)m * sizeof(double), hipMemcpyDeviceToHost);
+        copy_checked(c, rc, C_out + j * m, dout + j * mp, (size_t)m * sizeof(double), hipMemcpyDeviceToHost);
     }
   }
   (void)hipFree(dxt); hipFree(dxtw); hipFree(dxv); hipFree(dxvw);
@@ -1844,13 +1855,13 @@ int gpe_test_gemm(gpe_ctx* c, int32_t trans_a, int32_t trans_b, int64_t M, int64
     if (trans_b) { for (long long k = 0; k < K; ++k) for (long long n = 0; n < N; ++n) hb[k + n * K] = B[k * N + n]; ldb = K; }
     else { for (long long k = 0; k < K; ++k) for (long long n = 0; n < N; ++n) hb[n + k * N] = B[k * N + n]; ldb = N; }
     for (long long m = 0; m < M; ++m) for (long long n = 0; n < N; ++n) hc[m + n * M] = C[m * N + n];
-    (void)hipMemcpy(da, ha.data(), ha.size() * sizeof(double), hipMemcpyHostToDevice);
-    (void)hipMemcpy(db, hb.data(), hb.size() * sizeof(double), hipMemcpyHostToDevice);
-    (void)hipMemcpy(dc, hc.data(), hc.size() * sizeof(double), hipMemcpyHostToDevice);
+    copy_checked(c, rc, da, ha.data(), ha.size() * sizeof(double), hipMemcpyHostToDevice);
+    copy_checked(c, rc, db, hb.data(), hb.size() * sizeof(double), hipMemcpyHostToDevice);
+    copy_checked(c, rc, dc, hc.data(), hc.size() * sizeof(double), hipMemcpyHostToDevice);
     GemmProb p = mkprob(da, lda, db, ldb, dc, M, (int)(M / TILE), (int)(N / TILE), (int)K, 0, alpha, beta);
     p.tile_begin = 0;
     p.ntiles = p.mt * p.nt;
-    (void)hipMemcpy(c->dprobs + ADHOC_DESC_BASE + 8, &p, sizeof(GemmProb), hipMemcpyHostToDevice);
+    copy_checked(c, rc, c->dprobs + ADHOC_DESC_BASE + 8, &p, sizeof(GemmProb), hipMemcpyHostToDevice);
     HIPCHK(c, hipMemsetAsync(c->dinfo, 0, sizeof(int), c->stream));
     const int kind = trans_a ? (trans_b ? 2 : 1) : (trans_b ? 3 : 0);
     Launch L{kind, ADHOC_DESC_BASE + 8, 1, p.ntiles, 0.0};
@@ -1860,7 +1871,7 @@ int gpe_test_gemm(gpe_ctx* c, int32_t trans_a, int32_t trans_b, int64_t M, int64
       if (e != hipSuccess) rc = fail(c, GPE_ERR_HIP, hipGetErrorString(e));
     }
     if (rc == GPE_OK) {
-      (void)hipMemcpy(hc.data(), dc, hc.size() * sizeof(double), hipMemcpyDeviceToHost);
+      copy_checked(c, rc, hc.data(), dc, hc.size() * sizeof(double), hipMemcpyDeviceToHost);
       for (long long m = 0; m < M; ++m) for (long long n = 0; n < N; ++n) C[m * N + n] = hc[m + n * M];
     }
   }
