@@ -6,12 +6,16 @@
 // t = li P + r).  Tile row NB (below the n_pad x n_pad matrix) holds [f H]^T: the
 // sweep turns it into (L^-1 [f H])^T and its diagonal tile into -Gram.
 //
-// Step k (k = 0 .. NB-1), every rank, one HIP stream:
-//   owner(k): A(k,k) -> L_kk (in place), Dinv = L_kk^-1   (k_gemm G_DIAG, 1 workgroup)
+// Step k (k = 0 .. NB-1) in column group [gb, ge) (widths as the single-GPU fused
+// Cholesky, one wider: 8 while > 160 tile columns remain, then 4, 2, 1), every rank:
+//   owner(k): A(k,k) -= L(k,gb:k) L(k,gb:k)^T, -> L_kk (in place), Dinv = L_kk^-1
+//             (k_gemm G_DIAG, 1 workgroup); every rank: its panel tiles
+//             A(i,k) -= L(i,gb:k) L(k,gb:k)^T (same launch; row k from the gathered panels)
 //   RCCL broadcast of Dinv from owner(k)                    (128 KB)
 //   panel:   L(i,k) = A(i,k) Dinv^T for its rows i > k      (k_gemm)
-//   pack its panel tiles, RCCL all-gather, unpermute into the panel column
-//   update:  A(i,j) -= L(i,k) L(j,k)^T, its rows i > k, k < j <= i (k_gemm, tile list)
+//   pack its panel tiles, RCCL all-gather, unpermute into the group's panel block k-gb
+//   k = ge-1: A(i,j) -= L(i,gb:ge) L(j,gb:ge)^T, its rows, ge <= j <= i
+//             (k_gemm, tile list, K = 128 (ge-gb))
 //
 // Gradient (want_grad), same partition, no n x n collective:
 //   X = L^-1 by rows, right-looking: step k, owner(k) finishes its row
@@ -29,6 +33,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -207,7 +212,12 @@ struct gpe_dist {
   std::vector<Rank> ranks;   // local ranks (all P in loopback, one otherwise)
 
   double* dinv = nullptr;    // 128 x 128
-  double* panel = nullptr;   // (NB+1)*128 x 128
+  double* panel = nullptr;   // (NB+1)*128 x wmax*128: the current column group's gathered panels
+  // column groups (as the single-GPU fused Cholesky): {width, min remaining tile
+  // columns}, first match wins, else 1 (GPEMU_DIST_W="8:160,4:80,2:40" style)
+  std::vector<std::pair<int, int>> groups = {{8, 160}, {4, 80}, {2, 40}};
+  std::vector<int> gstart;   // per step: first column of its group
+  int wmax = 1;
   double* recv = nullptr;    // RCCL all-gather buffer
   double* gram = nullptr;    // Pc x Pc
   int* dinfo = nullptr;
@@ -305,6 +315,31 @@ GemmProb dprob(const double* A, long long lda, const double* B, long long ldb, d
   return p;
 }
 
+// Column groups [gb, ge): step k = gb + w applies the pending update by the group's
+// earlier columns [gb, k) to its own diagonal tile and panel tiles (K = 128 w, in the
+// diagonal launch, before the Dinv broadcast), and the step that closes the group
+// applies the whole group to the trailing matrix in one K = 128 (ge - gb) update.
+void build_groups(gpe_dist* h) {
+  const int NB = h->NB;
+  h->gstart.assign(NB, 0);
+  h->wmax = 1;
+  for (int g = 0; g < NB;) {
+    int w = 1;
+    for (const auto& r : h->groups)
+      if (NB - g > r.second) { w = r.first; break; }
+    w = std::max(1, std::min(w, NB - g));
+    for (int k = g; k < g + w; ++k) h->gstart[k] = g;
+    h->wmax = std::max(h->wmax, w);
+    g += w;
+  }
+}
+
+int group_end(const gpe_dist* h, int k) {   // one past the last column of k's group
+  int e = k + 1;
+  while (e < h->NB && h->gstart[e] == h->gstart[k]) ++e;
+  return e;
+}
+
 // every per-step GEMM descriptor and tile list, for the current n and partition
 int build_schedule(gpe_dist* h) {
   const int NB = h->NB, P = h->P;
@@ -317,25 +352,51 @@ int build_schedule(gpe_dist* h) {
   h->maxT.assign(NB, 0);
   std::vector<int> li0((size_t)NB * P), cnt((size_t)NB * P);
   for (int k = 0; k < NB; ++k) {
+    const int gb = h->gstart[k], ge = group_end(h, k);
+    const int Kp = (k - gb) * TILE;   // pending columns [gb, k)
     for (int r = 0; r < P; ++r) {
       li0[(size_t)k * P + r] = li0_of(k, P, r);
       cnt[(size_t)k * P + r] = std::max(0, nloc_of(NB, P, r) - li0_of(k, P, r));
       h->maxT[k] = std::max(h->maxT[k], cnt[(size_t)k * P + r]);
     }
-    // diagonal tile: owner's local row k / P, column k
+    // diagonal tile: owner's local row k / P, column k, less the pending update
+    // L(k, gb:k) L(k, gb:k)^T from its own row; then factored and inverted
+    DLaunch dl;
+    dl.first = (int)probs.size();
     const int owner = k % P;
     for (Rank& R : h->ranks) {
       if (R.rank != owner) continue;
       double* Ckk = R.A + (long long)(k / P) * TILE + (long long)k * TILE * R.ld;
-      GemmProb p = dprob(nullptr, R.ld, nullptr, R.ld, Ckk, R.ld, 1, 1, 0, G_DIAG, 1.0, 1.0);
+      const double* Lk = R.A + (long long)(k / P) * TILE + (long long)gb * TILE * R.ld;
+      GemmProb p = dprob(Kp ? Lk : nullptr, R.ld, Kp ? Lk : nullptr, R.ld, Ckk, R.ld, 1, 1, Kp, G_DIAG,
+                         Kp ? -1.0 : 1.0, 1.0);
       p.X = h->dinv;
       p.ldx = TILE;
       p.logdet = R.logdet + k;
       p.diag_col0 = k * TILE;
+      p.tile_begin = dl.tiles;
       p.ntiles = 1;
-      h->diag[k] = {(int)probs.size(), 1, 1, -1};
+      dl.tiles += 1;
       probs.push_back(p);
+      ++dl.count;
     }
+    // pending update of the panel tiles: A(i,k) -= L(i, gb:k) L(k, gb:k)^T over each
+    // local rank's rows i > k; L(k, gb:k) is row k of the group's gathered panels
+    if (Kp > 0) {
+      for (Rank& R : h->ranks) {
+        const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
+        if (c == 0) continue;
+        GemmProb p = dprob(R.A + (long long)a * TILE + (long long)gb * TILE * R.ld, R.ld,
+                           h->panel + (long long)k * TILE, ldp,
+                           R.A + (long long)a * TILE + (long long)k * TILE * R.ld, R.ld, c, 1, Kp, 0, -1.0, 1.0);
+        p.tile_begin = dl.tiles;
+        p.ntiles = c;
+        dl.tiles += c;
+        probs.push_back(p);
+        ++dl.count;
+      }
+    }
+    h->diag[k] = dl;
     // panel: L(i,k) = A(i,k) Dinv^T over each local rank's rows i > k
     DLaunch pl;
     pl.first = (int)probs.size();
@@ -351,7 +412,9 @@ int build_schedule(gpe_dist* h) {
       ++pl.count;
     }
     h->panel_l[k] = pl;
-    // trailing update of each local rank's rows i > k, columns k < j <= i
+    // the step closing a group: trailing update of each local rank's rows by the
+    // whole group, columns ge <= j <= i, K = 128 (ge - gb)
+    if (k + 1 != ge) continue;
     DLaunch ul;
     ul.first = (int)probs.size();
     ul.list = (long long)tiles.size();
@@ -359,11 +422,11 @@ int build_schedule(gpe_dist* h) {
     for (Rank& R : h->ranks) {
       const int a = li0_of(k, P, R.rank);
       if (a >= R.nloc) continue;
-      GemmProb p = dprob(R.A + (long long)k * TILE * R.ld, R.ld, h->panel, ldp, R.A, R.ld,
-                         R.nloc, NB + 1, TILE, 0, -1.0, 1.0);
+      GemmProb p = dprob(R.A + (long long)gb * TILE * R.ld, R.ld, h->panel, ldp, R.A, R.ld,
+                         R.nloc, NB + 1, (ge - gb) * TILE, 0, -1.0, 1.0);
       for (int li = a; li < R.nloc; ++li) {
         const int gt = li * P + R.rank;
-        for (int j = k + 1; j <= gt; ++j) tiles.push_back(((unsigned)pi << 24) | ((unsigned)li << 12) | (unsigned)j);
+        for (int j = ge; j <= gt; ++j) tiles.push_back(((unsigned)pi << 24) | ((unsigned)li << 12) | (unsigned)j);
       }
       probs.push_back(p);
       ++pi;
@@ -568,13 +631,14 @@ int step(gpe_dist* h, int k, int& ev) {
   }
   DCHK(launch(h, h->panel_l[k]));
   const long long ldp = (long long)(h->NB + 1) * TILE;
+  double* pcol = h->panel + (long long)(k - h->gstart[k]) * TILE * ldp;   // the group's panel block
   if (h->loop) {
     if (h->cev.size() > (size_t)ev + 1) DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
     for (Rank& R : h->ranks) {
       const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
       if (c == 0) continue;
       hipLaunchKernelGGL(k_dist_to_panel, dim3(c), dim3(256), 0, h->stream, R.A, R.ld, a, k, P, R.rank,
-                         h->panel, ldp);
+                         pcol, ldp);
       DCHK_HIP(h, hipGetLastError());
     }
     if (h->cev.size() > (size_t)ev) DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
@@ -594,7 +658,7 @@ int step(gpe_dist* h, int k, int& ev) {
                                  h->stream));
       DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
       hipLaunchKernelGGL(k_dist_unpermute, dim3(T, P), dim3(256), 0, h->stream, h->recv, seg,
-                         h->dli0 + (size_t)k * P, h->dcnt + (size_t)k * P, P, h->panel, ldp);
+                         h->dli0 + (size_t)k * P, h->dcnt + (size_t)k * P, P, pcol, ldp);
       DCHK_HIP(h, hipGetLastError());
     }
   }
@@ -642,6 +706,21 @@ gpe_dist* gpe_dist_create(int32_t device, int32_t nranks, int32_t rank, const ui
   h->P = nranks;
   h->rank = unique_id ? rank : 0;
   h->loop = unique_id == nullptr;
+  if (const char* e = std::getenv("GPEMU_DIST_W")) {   // "4:80,2:40": {width, min remaining}
+    h->groups.clear();
+    std::string spec(e);
+    size_t pos = 0;
+    while (pos < spec.size()) {
+      size_t end = spec.find(',', pos);
+      if (end == std::string::npos) end = spec.size();
+      const std::string item = spec.substr(pos, end - pos);
+      const size_t colon = item.find(':');
+      const int w = std::atoi(item.substr(0, colon).c_str());
+      const int lim = colon == std::string::npos ? 0 : std::atoi(item.substr(colon + 1).c_str());
+      if (w >= 1 && w <= 16) h->groups.push_back({w, lim});
+      pos = end + 1;
+    }
+  }
   bool ok = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess &&
             hipEventCreate(&h->e0) == hipSuccess && hipEventCreate(&h->e1) == hipSuccess &&
             hipMalloc((void**)&h->dinfo, sizeof(int)) == hipSuccess &&
@@ -745,7 +824,8 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
     DCHK(dalloc(h, &B.A, (size_t)B.ld * (size_t)(h->NB + 1) * TILE));
     DCHK(dalloc(h, &B.logdet, (size_t)h->NB + 1));
   }
-  DCHK(dalloc(h, &h->panel, (size_t)(h->NB + 1) * TILE * TILE));
+  build_groups(h);
+  DCHK(dalloc(h, &h->panel, (size_t)(h->NB + 1) * TILE * TILE * h->wmax));
   if (!h->loop) {
     const int T0 = nloc_of(h->NB, h->P, 0);   // the most tiles any rank contributes
     DCHK(dalloc(h, &h->recv, (size_t)h->P * T0 * TILE * TILE));

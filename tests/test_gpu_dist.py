@@ -128,3 +128,24 @@ def test_rccl_single_rank():
     t = dc.times()
     assert t["total_ms"] > 0.0
     dc.close()
+
+
+@pytest.mark.parametrize("groups", ["4:0", "3:0", "2:0,1:0"])
+@pytest.mark.parametrize("P", [1, 3])
+def test_loopback_column_groups(ctx, monkeypatch, groups, P):
+    """Column groups (pending updates inside the group, one K = 128 W trailing update
+    per group; GPEMU_DIST_W forces widths on a small matrix): value and gradient equal
+    the single-GPU path, incl. the augmented [f H] row and a ragged last group."""
+    monkeypatch.setenv("GPEMU_DIST_W", groups)
+    n, d = 1000, 4
+    X, f, H = orc.synthetic_problem(n, d, seed=3)
+    hp = _hp(d)
+    ctx.set_data(X, f, H)
+    ref, gref, _ = ctx.objective(native.GP4ML, native.KERNEL_STD, hp)
+    dc = native.DistContext(0, P)
+    dc.set_data(X, f, H)
+    llh, g, _ = dc.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=True)
+    dc.close()
+    assert abs(llh - ref) <= 1e-10 * abs(ref), (llh, ref)
+    ok, err = _grad_ok(g, gref, 1e-8)
+    assert ok, err
