@@ -236,6 +236,8 @@ struct gpe_dist {
   // gradient (allocated on the first want_grad call after gpe_dist_set_data)
   bool grad_ready = false, grad_now = false;
   double* xrow = nullptr;    // 128 x n_pad: X(k, 0:k+1), broadcast per step
+  double* xgrp = nullptr;    // wmax*128 x n_pad (ld wmax*128): the current group's X rows, zero
+                             // right of each row's diagonal tile within the group
   double* dZ = nullptr;      // n_pad x Pc: L^-1 [f H]
   double* dR2 = nullptr;     // n_pad x Pc
   double* r2loc = nullptr;   // local rows of R2, 128 columns (zero beyond Pc)
@@ -245,7 +247,7 @@ struct gpe_dist {
   double* cpart = nullptr;   // contraction partials
   double* csum = nullptr;    // d+2 per local rank
   GemmProb* gprobs = nullptr;
-  std::vector<DLaunch> tri_x, tri_u, wa_l, lau_l;
+  std::vector<DLaunch> tri_p, tri_x, tri_u, wa_l, lau_l;
   double grad_ms = 0.0;
 };
 
@@ -479,6 +481,7 @@ int ensure_grad(gpe_dist* h) {
     maxld = std::max(maxld, R.ld);
   }
   DCHK(dalloc(h, &h->xrow, (size_t)TILE * np));
+  DCHK(dalloc(h, &h->xgrp, (size_t)h->wmax * TILE * np));
   DCHK(dalloc(h, &h->dZ, (size_t)np * Pc));
   DCHK(dalloc(h, &h->dR2, (size_t)np * Pc));
   DCHK(dalloc(h, &h->r2loc, (size_t)maxld * TILE));
@@ -489,16 +492,33 @@ int ensure_grad(gpe_dist* h) {
   DCHK(dalloc(h, &h->cpart, (size_t)NB * (NB + 1) / 2 * (d + 2)));
   DCHK(dalloc(h, &h->csum, h->ranks.size() * (size_t)(d + 2)));
 
+  // Rows of X = L^-1 in the Cholesky's column groups [gb, ge): the owner of row k first
+  // applies the pending rows gb..k-1 of its group, R(k, 0:k) -= L(k, gb:k) X(gb:k, 0:k)
+  // (K = 128 (k-gb), the group's broadcast rows held in xgrp), then finishes
+  // X(k, 0:k) = Dinv_k R(k, 0:k); the step closing a group updates every rank's rows
+  // i >= ge with the whole group, R(i, 0:ge) -= L(i, gb:ge) X(gb:ge, 0:ge), K = 128 W.
   std::vector<GemmProb> probs;
+  const long long ldx = (long long)h->wmax * TILE;
+  h->tri_p.assign(NB, DLaunch());
   h->tri_x.assign(NB, DLaunch());
   h->tri_u.assign(NB, DLaunch());
   for (int k = 0; k < NB; ++k) {
     const int owner = k % P, lk = k / P;
+    const int gb = h->gstart[k], ge = group_end(h, k), w = k - gb;
     for (Rank& R : h->ranks) {
       if (R.rank != owner || k == 0) continue;
+      double* row = R.X + (long long)lk * TILE;
+      if (w > 0) {
+        GemmProb p = dprob(R.A + (long long)lk * TILE + (long long)gb * TILE * R.ld, R.ld, h->xgrp, ldx,
+                           row, R.ld, 1, k, w * TILE, 0, -1.0, 1.0);
+        p.ntiles = k;
+        DLaunch L;
+        L.first = (int)probs.size(); L.count = 1; L.tiles = k; L.kind = 1;
+        h->tri_p[k] = L;
+        probs.push_back(p);
+      }
       // X(k, 0:k) = Dinv_k R(k, 0:k) with R(k, c) = -sum_{j<k} L(k,j) X(j,c), in place
       // (each output tile reads only itself)
-      double* row = R.X + (long long)lk * TILE;
       GemmProb p = dprob(row + (long long)k * TILE * R.ld, R.ld, row, R.ld, row, R.ld, 1, k, TILE, 0, 1.0, 0.0);
       p.ntiles = k;
       DLaunch L;
@@ -506,17 +526,17 @@ int ensure_grad(gpe_dist* h) {
       h->tri_x[k] = L;
       probs.push_back(p);
     }
+    if (k + 1 != ge) continue;
     DLaunch ul;
     ul.first = (int)probs.size();
     ul.kind = 1;
     for (Rank& R : h->ranks) {
-      const int a = li0_of(k, P, R.rank), c = R.nlx - a;
+      const int a = lstart_of(ge, P, R.rank), c = R.nlx - a;
       if (c <= 0) continue;
-      // R(i, 0:k+1) -= L(i,k) X(k, 0:k+1) over its rows i > k
-      GemmProb p = dprob(R.A + (long long)a * TILE + (long long)k * TILE * R.ld, R.ld, h->xrow, TILE,
-                         R.X + (long long)a * TILE, R.ld, c, k + 1, TILE, 0, -1.0, 1.0);
+      GemmProb p = dprob(R.A + (long long)a * TILE + (long long)gb * TILE * R.ld, R.ld, h->xgrp, ldx,
+                         R.X + (long long)a * TILE, R.ld, c, ge, (ge - gb) * TILE, 0, -1.0, 1.0);
       p.tile_begin = ul.tiles;
-      p.ntiles = c * (k + 1);
+      p.ntiles = c * ge;
       ul.tiles += p.ntiles;
       probs.push_back(p);
       ++ul.count;
@@ -566,9 +586,12 @@ int ensure_grad(gpe_dist* h) {
   return GPE_OK;
 }
 
-// TRTRI step k: owner finishes X(k, :), broadcast, every rank updates its rows > k
+// TRTRI step k: owner applies its group's pending rows and finishes X(k, :), broadcast
+// into the group's rows; the step closing a group updates every rank's rows below it
 int trtri_step(gpe_dist* h, int k, int& ev) {
   const int P = h->P, owner = k % P, lk = k / P;
+  const int gb = h->gstart[k], ge = group_end(h, k), w = k - gb;
+  DCHK(launch(h, h->tri_p[k], h->gprobs));
   DCHK(launch(h, h->tri_x[k], h->gprobs));
   if (k == h->NB - 1) return GPE_OK;   // no rows below
   for (Rank& R : h->ranks) {
@@ -582,6 +605,15 @@ int trtri_step(gpe_dist* h, int k, int& ev) {
                                h->stream));
     DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
   }
+  // X(k, 0:k+1) -> the group's row block w; zero its columns k+1 .. ge-1, which the
+  // group's later rows and the closing update read as X(k, c) = 0
+  const long long ldx = (long long)h->wmax * TILE;
+  double* blk = h->xgrp + (long long)w * TILE;
+  DCHK_HIP(h, hipMemcpy2DAsync(blk, ldx * sizeof(double), h->xrow, TILE * sizeof(double), TILE * sizeof(double),
+                               (size_t)(k + 1) * TILE, hipMemcpyDeviceToDevice, h->stream));
+  if (ge > k + 1)
+    DCHK_HIP(h, hipMemset2DAsync(blk + (long long)(k + 1) * TILE * ldx, ldx * sizeof(double), 0,
+                                 TILE * sizeof(double), (size_t)(ge - k - 1) * TILE, h->stream));
   DCHK(launch(h, h->tri_u[k], h->gprobs));
   return GPE_OK;
 }
@@ -748,7 +780,7 @@ void gpe_dist_destroy(gpe_dist* h) {
     if (R.X) (void)hipFree(R.X);
   }
   double* bufs[] = {h->dX,    h->dXw,   h->dF,   h->dr,    h->dinvdelta, h->dinv, h->panel,
-                    h->recv,  h->gram,  h->xrow, h->dZ,    h->dR2,       h->r2loc, h->wpart,
+                    h->recv,  h->gram,  h->xrow, h->xgrp, h->dZ,    h->dR2,       h->r2loc, h->wpart,
                     h->pbuf,  h->dT2,   h->cpart, h->csum};
   for (double* b : bufs)
     if (b) (void)hipFree(b);
