@@ -1,10 +1,11 @@
 """Row-block distributed objective on CPU: the partition map the
 library exports, the RCCL-id hand-off over gloo, and a NumPy model of the exact
-per-step schedule of gpemu_dist.hip (cyclic tile rows + augmented [f H] row,
-broadcast of the diagonal inverse, all-gather of the panel column, own-row trailing
-update) run on 2 and 3 gloo ranks against a dense factorisation, extended by the
-gradient schedule (rows of L^-1 finished by their owner and broadcast, own-row
-updates, per-rank partials X_r^T X_r whose sum is A^-1).  NumPy is only the test's
+per-step schedule of gpemu_dist.hip (cyclic tile rows + augmented [f H] row, column
+groups with pending updates inside the group, broadcast of the diagonal inverse,
+all-gather of the panel column, own-row trailing update per group) run on 2 and 3
+gloo ranks against a dense factorisation, extended by the gradient schedule (rows of
+L^-1 finished by their owner after its group's earlier rows, broadcast, own-row
+updates per group, per-rank partials X_r^T X_r whose sum is A^-1).  NumPy is only the test's
 stand-in for the HIP tile kernels."""
 import os
 import socket
@@ -73,13 +74,15 @@ def _problem(n, q, seed=3):
     return A, F
 
 
-def _sched_worker(rank, world, port, n, q, out):
+def _sched_worker(rank, world, port, n, q, W, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         A, F = _problem(n, q)
         nb = n // B
         Pc = q + 1
+        gstart = [k - k % W for k in range(nb)]                      # column groups of width W
+        gend = [min(gstart[k] + W, nb) for k in range(nb)]
         # augmented matrix: tile row nb holds F^T (zero padded to B rows), (nb, nb) = 0
         full = np.zeros(((nb + 1) * B, (nb + 1) * B))
         full[:n, :n] = A
@@ -87,8 +90,19 @@ def _sched_worker(rank, world, port, n, q, out):
         mine = [t for t in range(nb + 1) if t % world == rank]
         loc = {t: full[t * B:(t + 1) * B, :].copy() for t in mine}     # own tile rows
         logdet = np.zeros(nb + 1)
+        gpanel = {}   # the group's gathered panel columns: gpanel[c][t] = L(t, c)
         for k in range(nb):
             owner = k % world
+            gb, ge = gstart[k], gend[k]
+            if k == gb:
+                gpanel = {}
+            # pending update by the group's earlier columns: own diagonal and panel tiles
+            rows = [t for t in mine if t > k]
+            for c in range(gb, k):
+                if owner == rank:
+                    loc[k][:, k * B:(k + 1) * B] -= loc[k][:, c * B:(c + 1) * B] @ loc[k][:, c * B:(c + 1) * B].T
+                for t in rows:
+                    loc[t][:, k * B:(k + 1) * B] -= loc[t][:, c * B:(c + 1) * B] @ gpanel[c][k].T
             dinv = torch.zeros(B, B, dtype=torch.float64)
             if owner == rank:
                 L = np.linalg.cholesky(loc[k][:, k * B:(k + 1) * B])
@@ -97,7 +111,6 @@ def _sched_worker(rank, world, port, n, q, out):
                 dinv = torch.from_numpy(np.linalg.inv(L))
             dist.broadcast(dinv, src=owner)
             Dinv = dinv.numpy()
-            rows = [t for t in mine if t > k]
             for t in rows:                                            # panel
                 loc[t][:, k * B:(k + 1) * B] = loc[t][:, k * B:(k + 1) * B] @ Dinv.T
             maxT = max(len([t for t in range(nb + 1) if t % world == r and t > k]) for r in range(world))
@@ -111,9 +124,12 @@ def _sched_worker(rank, world, port, n, q, out):
                 rt = [t for t in range(nb + 1) if t % world == r and t > k]
                 for i, t in enumerate(rt):
                     panel[t] = recv[r][i].numpy()
-            for t in rows:                                            # own-row update
-                for j in range(k + 1, t + 1):
-                    loc[t][:, j * B:(j + 1) * B] -= loc[t][:, k * B:(k + 1) * B] @ panel[j].T
+            gpanel[k] = panel
+            if k + 1 == ge:                                           # group closes: own-row update
+                for t in [t for t in mine if t >= ge]:
+                    for j in range(ge, t + 1):
+                        for c in range(gb, ge):
+                            loc[t][:, j * B:(j + 1) * B] -= loc[t][:, c * B:(c + 1) * B] @ gpanel[c][j].T
         ld = torch.from_numpy(logdet)
         dist.all_reduce(ld)
         g = torch.zeros(Pc, Pc, dtype=torch.float64)
@@ -121,19 +137,30 @@ def _sched_worker(rank, world, port, n, q, out):
             g = torch.from_numpy(-loc[nb][:Pc, nb * B:nb * B + Pc].copy())
         dist.broadcast(g, src=nb % world)
         # gradient schedule: X = L^-1 by rows; R(t, :) accumulates -sum L(t,j) X(j, :)
+        # in the same column groups: the owner applies its group's earlier rows first, the
+        # step closing a group updates every rank's rows below it
         Xl = {t: np.zeros((B, nb * B)) for t in mine if t < nb}
+        xg = {}
         for k in range(nb):
             owner = k % world
+            gb, ge = gstart[k], gend[k]
+            if k == gb:
+                xg = {}
             xrow = torch.zeros(B, (k + 1) * B, dtype=torch.float64)
             if owner == rank:
+                for c in range(gb, k):
+                    Xl[k][:, :(c + 1) * B] -= loc[k][:, c * B:(c + 1) * B] @ xg[c]
                 Dinv = np.linalg.inv(loc[k][:, k * B:(k + 1) * B])
                 Xl[k][:, :k * B] = Dinv @ Xl[k][:, :k * B]
                 Xl[k][:, k * B:(k + 1) * B] = Dinv
                 xrow = torch.from_numpy(Xl[k][:, :(k + 1) * B].copy())
             dist.broadcast(xrow, src=owner)
-            for t in Xl:
-                if t > k:
-                    Xl[t][:, :(k + 1) * B] -= loc[t][:, k * B:(k + 1) * B] @ xrow.numpy()
+            xg[k] = xrow.numpy()
+            if k + 1 == ge:
+                for t in Xl:
+                    if t >= ge:
+                        for c in range(gb, ge):
+                            Xl[t][:, :(c + 1) * B] -= loc[t][:, c * B:(c + 1) * B] @ xg[c]
         part = np.zeros((nb * B, nb * B))
         for xr in Xl.values():
             part += xr.T @ xr
@@ -144,13 +171,15 @@ def _sched_worker(rank, world, port, n, q, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_schedule_model_matches_dense(world):
+@pytest.mark.parametrize("world,W", [(2, 1), (3, 1), (2, 3), (3, 4)])
+def test_schedule_model_matches_dense(world, W):
+    """W: column-group width (1 = a trailing update per column; 3 and 4 leave a ragged
+    last group of the 7 tile columns)."""
     n, q = 7 * B, 3
     port = _free_port()
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_sched_worker, args=(world, port, n, q, out), nprocs=world, join=True)
+        mp.spawn(_sched_worker, args=(world, port, n, q, W, out), nprocs=world, join=True)
         res = dict(out)
     A, F = _problem(n, q)
     L = np.linalg.cholesky(A)
