@@ -88,10 +88,21 @@ def cpu_baseline(d):
         times[n] = time.perf_counter() - t
     p = np.log(times[hi] / times[lo]) / np.log(hi / lo)
     t16k = times[hi] * (16384 / hi) ** 3
+    # best-effort CPU formulation (SURVEY 8d "fast-mode"): Cholesky, explicit inverse,
+    # Frobenius-contraction gradient, i.e. the GPU's algorithm on LAPACK
+    X, f, H = orc.synthetic_problem(hi, d, seed=0)
+    t = time.perf_counter()
+    orc.objective_fast(X, f, H, eval_point(d, 0), orc.GP4ML, orc.STD, True)
+    tf = time.perf_counter() - t
+    tf16k = tf * (16384 / hi) ** 3
     return {"value": 1.0 / t16k, "unit": "evals/s", "cores": int(threads), "kind": "port",
             "sample": (f"oracle ref-mode (reference op order, NumPy/OpenBLAS, {threads} threads), d={d}: "
                        f"n={lo} {times[lo]:.2f} s/eval, n={hi} {times[hi]:.2f} s/eval (fitted exponent "
-                       f"{p:.2f}); n=16384 = n={hi} x (16384/{hi})^3 -> {t16k:.0f} s/eval")}
+                       f"{p:.2f}); n=16384 = n={hi} x (16384/{hi})^3 -> {t16k:.0f} s/eval"),
+            "fast_mode": {"value": 1.0 / tf16k, "unit": "evals/s",
+                          "sample": (f"oracle fast-mode (Cholesky + inverse + contraction, the GPU's "
+                                     f"algorithm on LAPACK), n={hi} {tf:.2f} s/eval; n=16384 = "
+                                     f"x (16384/{hi})^3 -> {tf16k:.0f} s/eval")}}
 
 
 def other_configs(native, synthetic, ctx, args):
