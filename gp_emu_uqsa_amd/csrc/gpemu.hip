@@ -584,8 +584,10 @@ int ensure_fact(gpe_ctx* c, Fact& F, long long n_pad) {
 int scale_training(gpe_ctx* c, const double* delta) {
   CHK(ensure_pinned(c, 64));
   for (int k = 0; k < c->d; ++k) {
+    // zero or NaN length scale: the reference's covariance is NaN there and its Cholesky
+    // raises LinAlgError (-> `return None`, _emulatoroptimise.py:374-376, :489-491)
     if (!(delta[k] > 0.0) && !(delta[k] < 0.0))
-      return fail(c, GPE_ERR_ARG, "delta must be non-zero");
+      return fail(c, GPE_NOT_PD, "length scale delta[" + std::to_string(k) + "] is zero or NaN");
     c->hpin[k] = 1.0 / delta[k];
   }
   HIPCHK(c, hipMemcpyAsync(c->dinvdelta, c->hpin, c->d * sizeof(double), hipMemcpyHostToDevice,

@@ -894,7 +894,8 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
 
   DCHK(pinned(h, nslot * (NB + 1) + (size_t)Pc * Pc + nslot * (d + 2) + 64));
   for (int k = 0; k < d; ++k) {
-    if (!(hp[k] > 0.0) && !(hp[k] < 0.0)) return dfail(h, GPE_ERR_ARG, "delta must be non-zero");
+    if (!(hp[k] > 0.0) && !(hp[k] < 0.0))   // as the single-GPU path: not positive definite
+      return dfail(h, GPE_NOT_PD, "length scale delta[" + std::to_string(k) + "] is zero or NaN");
     h->hpin[k] = 1.0 / hp[k];
   }
   DCHK_HIP(h, hipEventRecord(h->e0, h->stream));

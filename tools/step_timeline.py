@@ -1,3 +1,6 @@
+"""Per-launch timeline of the last objective evaluation in a rocprofv3 kernel trace (dev tool):
+every launch after the last K-build with its grid and start/duration in us.
+usage: python tools/step_timeline.py kernel_trace.csv"""
 import csv, sys
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Start_Timestamp']))
 NB = 128
