@@ -14,7 +14,8 @@
  *  - Calls are synchronous: the context's HIP stream is drained before return.
  *  - One context per host thread, one GPU per context.  No callbacks.
  *  - Return codes: GPE_OK (0); GPE_NOT_PD (1) = Cholesky met a non-positive or
- *    NaN pivot -- the host maps it to the reference's `return None`
+ *    NaN pivot, or a length scale is zero / NaN (the reference's covariance is NaN
+ *    there) -- the host maps it to the reference's `return None`
  *    (_emulatoroptimise.py:374-376, :489-491); negative = error, text in
  *    gpe_last_error().
  *  - Hyperparameters are UNtransformed (delta, nu, sigma); transform /
