@@ -82,3 +82,29 @@ def test_final_beliefs_roundtrip(toysim_dir):
     assert b2.delta == [0.2, 0.16] and b2.beta == [0.5, 2.8] and b2.sigma == 0.61
     assert b2.input_minmax == [[0.01, 0.98], [0.013, 0.99]]
     assert b2.active_index == [0, 1] and b2.output_index == 0
+
+
+def test_concurrent_tries_policy(monkeypatch):
+    """Two tries in flight for 4096 <= n <= 32768 and >= 2 tries; GPEMU_CONCURRENT_TRIES
+    forces k (capped by the tries); never with a collective objective (host logic only)."""
+    from gp_emu_uqsa_amd import distributed, optimize
+
+    class D:
+        def __init__(self, n):
+            self.inputs = np.zeros((n, 2))
+
+    def conc(n, tries):
+        o = optimize.Optimize.__new__(optimize.Optimize)
+        o.data = D(n)
+        return o._concurrency(tries)
+
+    monkeypatch.delenv("GPEMU_CONCURRENT_TRIES", raising=False)
+    assert conc(16384, 4) == 2 and conc(4096, 2) == 2
+    assert conc(2048, 4) == 1 and conc(65536, 4) == 1 and conc(16384, 1) == 1
+    monkeypatch.setenv("GPEMU_CONCURRENT_TRIES", "3")
+    assert conc(100, 5) == 3 and conc(100, 2) == 2
+    monkeypatch.setenv("GPEMU_CONCURRENT_TRIES", "1")
+    assert conc(16384, 4) == 1
+    monkeypatch.setattr(distributed, "_OBJECTIVE", object())
+    monkeypatch.setenv("GPEMU_CONCURRENT_TRIES", "4")
+    assert conc(16384, 4) == 1
