@@ -1732,6 +1732,66 @@ int gpe_kernel_grad(gpe_ctx* c, const double* delta, int32_t d, int64_t m, const
   return rc;
 }
 
+int gpe_lhc_maximin(gpe_ctx* c, int32_t N, int64_t n, int32_t dim, const double* designs, int64_t ne,
+                    const double* fextra, int64_t* idx_out) {
+  if (!c) return GPE_ERR_ARG;
+  if (!designs || !idx_out || N <= 0 || n <= 0 || dim <= 0 || dim > 512 || ne < 0 || (ne > 0 && !fextra) ||
+      n + ne < 2 || n + ne > 0x7fffffffLL)
+    return fail(c, GPE_ERR_ARG, "bad lhc_maximin args");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const int m = (int)(n + ne);
+  // designs per launch: grid.y <= 65535 and <= 1 GiB of design points on the device
+  const long long per = std::max(1LL, (1LL << 27) / (n * (long long)dim));
+  const int K = (int)std::min<long long>({(long long)N, 65535LL, per});
+  const int tiles = (int)((n + LHC_R - 1) / LHC_R);
+  const int ftiles = ne > 1 ? (int)((ne - 1 + LHC_R - 1) / LHC_R) : 0;
+  const size_t lds = (size_t)LHC_R * dim * sizeof(double);
+  const size_t nbuf = std::max((size_t)K * tiles, (size_t)ftiles);
+  double *dD = nullptr, *dE = nullptr, *bd = nullptr;
+  long long *bi = nullptr, *oi = nullptr;
+  int rc = dalloc(c, &dD, (size_t)K * n * dim);
+  if (rc == GPE_OK && ne > 0) rc = dalloc(c, &dE, (size_t)ne * dim);
+  if (rc == GPE_OK) rc = dalloc(c, &bd, nbuf + 1);  // slot nbuf: the fextra-fextra minimum
+  if (rc == GPE_OK) rc = dalloc(c, &bi, nbuf + 1);
+  if (rc == GPE_OK) rc = dalloc(c, &oi, (size_t)K);
+  if (ne > 0) copy_checked(c, rc, dE, fextra, (size_t)ne * dim * sizeof(double), hipMemcpyHostToDevice);
+  const bool ff = ftiles > 0;
+  if (rc == GPE_OK && ff) {
+    // pairs among the fextra points (rows n .. m-2) are the same for every design
+    hipLaunchKernelGGL(k_lhc_rowmin, dim3(ftiles, 1), dim3(256), lds, c->stream, dD, 0LL, (int)n, dE,
+                       (int)ne, dim, (int)n, m - 1, bd, bi);
+    hipLaunchKernelGGL(k_lhc_reduce, dim3(1), dim3(256), 0, c->stream, bd, bi, ftiles,
+                       (const double*)nullptr, (const long long*)nullptr, bd + nbuf, bi + nbuf);
+  }
+  for (int k0 = 0; rc == GPE_OK && k0 < N; k0 += K) {
+    const int kb = std::min(K, N - k0);
+    copy_checked(c, rc, dD, designs + (size_t)k0 * n * dim, (size_t)kb * n * dim * sizeof(double),
+                 hipMemcpyHostToDevice);
+    if (rc != GPE_OK) break;
+    // rows 0 .. n-1 of each design (a design's last row has pairs only with fextra)
+    const int row_end = (int)std::min<long long>(n, m - 1);
+    const int tl = (row_end + LHC_R - 1) / LHC_R;
+    hipLaunchKernelGGL(k_lhc_rowmin, dim3(tl, kb), dim3(256), lds, c->stream, dD, n * (long long)dim, (int)n,
+                       dE, (int)ne, dim, 0, row_end, bd, bi);
+    hipLaunchKernelGGL(k_lhc_reduce, dim3(kb), dim3(256), 0, c->stream, bd, bi, tl,
+                       ff ? (const double*)(bd + nbuf) : nullptr, ff ? (const long long*)(bi + nbuf) : nullptr,
+                       (double*)nullptr, oi);
+    // the copies are synchronous on the null stream, which does not order with c->stream
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) rc = fail(c, GPE_ERR_HIP, std::string("lhc_maximin: ") + hipGetErrorString(e));
+    copy_checked(c, rc, idx_out + k0, oi, (size_t)kb * sizeof(long long), hipMemcpyDeviceToHost);
+  }
+  if (rc != GPE_OK) (void)hipStreamSynchronize(c->stream);
+  if (dD) hipFree(dD);
+  if (dE) hipFree(dE);
+  if (bd) hipFree(bd);
+  if (bi) hipFree(bi);
+  if (oi) hipFree(oi);
+  return rc;
+}
+
 int gpe_kernel_covar(gpe_ctx* c, int32_t kernel, const double* delta, int32_t d, double nu,
                      int64_t n, const double* XT, int64_t m, const double* XV, double* C_out) {
   if (!c) return GPE_ERR_ARG;

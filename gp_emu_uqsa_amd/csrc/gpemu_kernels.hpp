@@ -1675,4 +1675,107 @@ static __global__ void __launch_bounds__(256) k_noise_sq(const double* Y, long l
   z[i] = acc;
 }
 
+// ---- oLHC "maximin" selection (design_inputs.py:54-67): np.argmin(pdist(xt, 'sqeuclidean'))
+// per candidate design, xt = [x_k; fextra] (m = n + ne points).  Ordering key of a pair is
+// (distance, condensed index), NaN distances first -- np.argmin's first occurrence of the
+// minimum, with NaN as the minimum.
+__device__ __forceinline__ bool lhc_less(double a, long long ia, double b, long long ib) {
+  return a < b || (a == b && ia < ib);
+}
+
+__device__ __forceinline__ void lhc_block_min(double& bd, long long& bi, double* sd, long long* si) {
+  for (int off = 32; off > 0; off >>= 1) {
+    const double od = __shfl_down(bd, off, 64);
+    const long long oi = __shfl_down(bi, off, 64);
+    if (lhc_less(od, oi, bd, bi)) { bd = od; bi = oi; }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) { sd[w] = bd; si[w] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
+      if (lhc_less(sd[k], si[k], bd, bi)) { bd = sd[k]; bi = si[k]; }
+  }
+}
+
+// One block per (tile of LHC_R consecutive rows i, design k): rows [row0 + x R, +R) against
+// every j > i.  Each thread walks j = i0+1+tid, +256, ..., loads point j once and forms the
+// distances of all R rows from it (row points staged in LDS, read as broadcasts).  Point j
+// is row j of design k for j < n, else row j-n of E.  The squared distance is summed over
+// dimensions in order with separate multiply and add (no FMA), as scipy's pdist does, so
+// every distance is bit-identical to the host's.  Writes the tile's (min, index).
+constexpr int LHC_R = 8;
+static __global__ void __launch_bounds__(256) k_lhc_rowmin(const double* __restrict__ D, long long dstride,
+                                                           int n, const double* __restrict__ E, int ne,
+                                                           int dim, int row0, int row_end,
+                                                           double* __restrict__ out_d,
+                                                           long long* __restrict__ out_i) {
+#pragma clang fp contract(off)
+  extern __shared__ double lhc_sm[];  // LHC_R * dim row points
+  __shared__ double sd[4];
+  __shared__ long long si[4];
+  const int m = n + ne;
+  const double* Dk = D + (long long)blockIdx.y * dstride;
+  const int i0 = row0 + (int)blockIdx.x * LHC_R;
+  const int nr = min(LHC_R, row_end - i0);
+  for (int t = threadIdx.x; t < nr * dim; t += blockDim.x) {
+    const int r = t / dim, k = t - r * dim, i = i0 + r;
+    lhc_sm[t] = i < n ? Dk[(long long)i * dim + k] : E[(long long)(i - n) * dim + k];
+  }
+  __syncthreads();
+  double bd = __builtin_inf();
+  long long bi = 0x7fffffffffffffffLL;
+  double s[LHC_R];
+  for (int j = i0 + 1 + (int)threadIdx.x; j < m; j += blockDim.x) {
+    const double* pj = j < n ? Dk + (long long)j * dim : E + (long long)(j - n) * dim;
+#pragma unroll
+    for (int r = 0; r < LHC_R; ++r) s[r] = 0.0;
+    for (int k = 0; k < dim; ++k) {
+      const double xj = pj[k];
+#pragma unroll
+      for (int r = 0; r < LHC_R; ++r) {
+        const double t = lhc_sm[r * dim + k] - xj;
+        s[r] = s[r] + t * t;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < LHC_R; ++r) {
+      const int i = i0 + r;
+      if (r < nr && j > i) {
+        const double v = (s[r] != s[r]) ? -__builtin_inf() : s[r];
+        const long long idx = (long long)m * i - (long long)i * (i + 1) / 2 + (j - i - 1);
+        if (lhc_less(v, idx, bd, bi)) { bd = v; bi = idx; }
+      }
+    }
+  }
+  lhc_block_min(bd, bi, sd, si);
+  if (threadIdx.x == 0) {
+    const long long o = (long long)blockIdx.y * gridDim.x + blockIdx.x;
+    out_d[o] = bd;
+    out_i[o] = bi;
+  }
+}
+
+// One block per design: the minimum over its nb tile results, and over the (design
+// independent) fextra-fextra minimum (fd, fi) when given.  Writes the condensed index
+// (and the distance key, when out_d is given).
+static __global__ void __launch_bounds__(256) k_lhc_reduce(const double* __restrict__ in_d,
+                                                           const long long* __restrict__ in_i, int nb,
+                                                           const double* fd, const long long* fi,
+                                                           double* out_d, long long* __restrict__ out_i) {
+  __shared__ double sd[4];
+  __shared__ long long si[4];
+  double bd = __builtin_inf();
+  long long bi = 0x7fffffffffffffffLL;
+  const long long base = (long long)blockIdx.x * nb;
+  for (int t = threadIdx.x; t < nb; t += blockDim.x)
+    if (lhc_less(in_d[base + t], in_i[base + t], bd, bi)) { bd = in_d[base + t]; bi = in_i[base + t]; }
+  lhc_block_min(bd, bi, sd, si);
+  if (threadIdx.x == 0) {
+    if (fd && lhc_less(*fd, *fi, bd, bi)) { bd = *fd; bi = *fi; }
+    if (out_d) out_d[blockIdx.x] = bd;
+    out_i[blockIdx.x] = bi;
+  }
+}
+
 }  // namespace gpe

@@ -52,6 +52,8 @@ SIGNATURES = {
     "gpe_kernel_covar": (_ct.c_int, [_VP, _ct.c_int32, _D, _ct.c_int32, _ct.c_double, _ct.c_int64,
                                      _D, _ct.c_int64, _D, _D]),
     "gpe_kernel_grad": (_ct.c_int, [_VP, _D, _ct.c_int32, _ct.c_int64, _D, _D, _ct.c_double, _ct.c_double, _D]),
+    "gpe_lhc_maximin": (_ct.c_int, [_VP, _ct.c_int32, _ct.c_int64, _ct.c_int32, _D, _ct.c_int64, _D,
+                                    _ct.POINTER(_ct.c_int64)]),
     "gpe_cholesky": (_ct.c_int, [_VP, _ct.c_int64, _D, _D, _D, _D, _D]),
     "gpe_test_gemm": (_ct.c_int, [_VP, _ct.c_int32, _ct.c_int32, _ct.c_int64, _ct.c_int64,
                                   _ct.c_int64, _D, _D, _D, _ct.c_double, _ct.c_double]),
@@ -349,6 +351,18 @@ class Context:
         out = _np.zeros((m, m))
         self._check(self.lib.gpe_kernel_grad(self._h, _ptr(delta), d, m, _ptr(X), _ptr(cc),
                                              float(col_scale), float(pre), _ptr(out)), "gpe_kernel_grad")
+        return out
+
+    def lhc_maximin(self, designs, fextra=None):
+        """np.argmin(pdist([designs[k]; fextra], 'sqeuclidean')) for every candidate
+        design k (designs: N x n x dim) -> int64 array of N condensed indices."""
+        designs = _f64(designs)
+        N, n, dim = designs.shape
+        fe = None if fextra is None else _f64(fextra).reshape(-1, dim)
+        ne = 0 if fe is None else fe.shape[0]
+        out = _np.zeros(N, dtype=_np.int64)
+        self._check(self.lib.gpe_lhc_maximin(self._h, N, n, dim, _ptr(designs), ne, _ptr(fe),
+                                             out.ctypes.data_as(_ct.POINTER(_ct.c_int64))), "gpe_lhc_maximin")
         return out
 
     def cholesky(self, A, want=("L",)):

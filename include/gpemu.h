@@ -30,8 +30,9 @@
 extern "C" {
 #endif
 
-#define GPE_ABI_VERSION 6   /* 3: gpe_dist_objective gained want_grad / grad_out; 4: sensitivity;
-                                5: gpe_noise_sample (noise_fit); 6: gpe_kernel_grad */
+#define GPE_ABI_VERSION 7   /* 3: gpe_dist_objective gained want_grad / grad_out; 4: sensitivity;
+                                5: gpe_noise_sample (noise_fit); 6: gpe_kernel_grad;
+                                7: gpe_lhc_maximin */
 
 enum gpe_status {
     GPE_OK = 0,
@@ -136,6 +137,16 @@ int gpe_kernel_var(gpe_ctx* ctx, int32_t kernel, const double* delta, int32_t d,
  * form, s2 nu^2 I, is diagonal and built by the host.) */
 int gpe_kernel_grad(gpe_ctx* ctx, const double* delta, int32_t d, int64_t m, const double* X,
                     const double* col, double col_scale, double pre, double* G_out);
+
+/* The oLHC generator's selection statistic (design_inputs.py:54-64): for each of the N
+ * candidate designs (designs: N x n x dim row-major, design k at k*n*dim),
+ * idx_out[k] = np.argmin(scipy pdist(xt, 'sqeuclidean')) with xt = [design k; fextra]
+ * (fextra: ne x dim row-major, ne may be 0 / NULL): the condensed index of the closest
+ * pair, first occurrence on ties, NaN distances count as the minimum.  Distances are
+ * summed over dimensions in order without FMA, bit-identical to pdist's.  The caller
+ * keeps the reference's rule (largest index wins, :62-67).  n + ne >= 2, dim <= 512. */
+int gpe_lhc_maximin(gpe_ctx* ctx, int32_t N, int64_t n, int32_t dim, const double* designs,
+                    int64_t ne, const double* fextra, int64_t* idx_out);
 
 /* K.covar(XT, XV) -> n x m row-major: _emulatorkernels.py:75-79 / :148-152. */
 int gpe_kernel_covar(gpe_ctx* ctx, int32_t kernel, const double* delta, int32_t d,
