@@ -1735,7 +1735,7 @@ int gpe_kernel_grad(gpe_ctx* c, const double* delta, int32_t d, int64_t m, const
 int gpe_lhc_maximin(gpe_ctx* c, int32_t N, int64_t n, int32_t dim, const double* designs, int64_t ne,
                     const double* fextra, int64_t* idx_out) {
   if (!c) return GPE_ERR_ARG;
-  if (!designs || !idx_out || N <= 0 || n <= 0 || dim <= 0 || dim > 512 || ne < 0 || (ne > 0 && !fextra) ||
+  if (!designs || !idx_out || N <= 0 || n <= 0 || dim <= 0 || ne < 0 || (ne > 0 && !fextra) ||
       n + ne < 2 || n + ne > 0x7fffffffLL)
     return fail(c, GPE_ERR_ARG, "bad lhc_maximin args");
   HIPCHK(c, hipSetDevice(c->device));
@@ -1746,7 +1746,9 @@ int gpe_lhc_maximin(gpe_ctx* c, int32_t N, int64_t n, int32_t dim, const double*
   const int K = (int)std::min<long long>({(long long)N, 65535LL, per});
   const int tiles = (int)((n + LHC_R - 1) / LHC_R);
   const int ftiles = ne > 1 ? (int)((ne - 1 + LHC_R - 1) / LHC_R) : 0;
-  const size_t lds = (size_t)LHC_R * dim * sizeof(double);
+  const bool use_lds = dim <= LHC_LDS_DIM;
+  const size_t lds = use_lds ? (size_t)LHC_R * dim * sizeof(double) : 0;
+  auto rowmin = use_lds ? k_lhc_rowmin<true> : k_lhc_rowmin<false>;
   const size_t nbuf = std::max((size_t)K * tiles, (size_t)ftiles);
   double *dD = nullptr, *dE = nullptr, *bd = nullptr;
   long long *bi = nullptr, *oi = nullptr;
@@ -1759,7 +1761,7 @@ int gpe_lhc_maximin(gpe_ctx* c, int32_t N, int64_t n, int32_t dim, const double*
   const bool ff = ftiles > 0;
   if (rc == GPE_OK && ff) {
     // pairs among the fextra points (rows n .. m-2) are the same for every design
-    hipLaunchKernelGGL(k_lhc_rowmin, dim3(ftiles, 1), dim3(256), lds, c->stream, dD, 0LL, (int)n, dE,
+    hipLaunchKernelGGL(rowmin, dim3(ftiles, 1), dim3(256), lds, c->stream, dD, 0LL, (int)n, dE,
                        (int)ne, dim, (int)n, m - 1, bd, bi);
     hipLaunchKernelGGL(k_lhc_reduce, dim3(1), dim3(256), 0, c->stream, bd, bi, ftiles,
                        (const double*)nullptr, (const long long*)nullptr, bd + nbuf, bi + nbuf);
@@ -1772,7 +1774,7 @@ int gpe_lhc_maximin(gpe_ctx* c, int32_t N, int64_t n, int32_t dim, const double*
     // rows 0 .. n-1 of each design (a design's last row has pairs only with fextra)
     const int row_end = (int)std::min<long long>(n, m - 1);
     const int tl = (row_end + LHC_R - 1) / LHC_R;
-    hipLaunchKernelGGL(k_lhc_rowmin, dim3(tl, kb), dim3(256), lds, c->stream, dD, n * (long long)dim, (int)n,
+    hipLaunchKernelGGL(rowmin, dim3(tl, kb), dim3(256), lds, c->stream, dD, n * (long long)dim, (int)n,
                        dE, (int)ne, dim, 0, row_end, bd, bi);
     hipLaunchKernelGGL(k_lhc_reduce, dim3(kb), dim3(256), 0, c->stream, bd, bi, tl,
                        ff ? (const double*)(bd + nbuf) : nullptr, ff ? (const long long*)(bi + nbuf) : nullptr,

@@ -1704,7 +1704,10 @@ __device__ __forceinline__ void lhc_block_min(double& bd, long long& bi, double*
 // is row j of design k for j < n, else row j-n of E.  The squared distance is summed over
 // dimensions in order with separate multiply and add (no FMA), as scipy's pdist does, so
 // every distance is bit-identical to the host's.  Writes the tile's (min, index).
+// kLds = false (dim above LHC_LDS_DIM): the row points are read from global memory instead.
 constexpr int LHC_R = 8;
+constexpr int LHC_LDS_DIM = 512;
+template <bool kLds>
 static __global__ void __launch_bounds__(256) k_lhc_rowmin(const double* __restrict__ D, long long dstride,
                                                            int n, const double* __restrict__ E, int ne,
                                                            int dim, int row0, int row_end,
@@ -1718,11 +1721,19 @@ static __global__ void __launch_bounds__(256) k_lhc_rowmin(const double* __restr
   const double* Dk = D + (long long)blockIdx.y * dstride;
   const int i0 = row0 + (int)blockIdx.x * LHC_R;
   const int nr = min(LHC_R, row_end - i0);
-  for (int t = threadIdx.x; t < nr * dim; t += blockDim.x) {
-    const int r = t / dim, k = t - r * dim, i = i0 + r;
-    lhc_sm[t] = i < n ? Dk[(long long)i * dim + k] : E[(long long)(i - n) * dim + k];
+  const double* prow[LHC_R];
+#pragma unroll
+  for (int r = 0; r < LHC_R; ++r) {
+    const int i = min(i0 + r, m - 1);
+    prow[r] = i < n ? Dk + (long long)i * dim : E + (long long)(i - n) * dim;
   }
-  __syncthreads();
+  if (kLds) {
+    for (int t = threadIdx.x; t < nr * dim; t += blockDim.x) {
+      const int r = t / dim, k = t - r * dim, i = i0 + r;
+      lhc_sm[t] = i < n ? Dk[(long long)i * dim + k] : E[(long long)(i - n) * dim + k];
+    }
+    __syncthreads();
+  }
   double bd = __builtin_inf();
   long long bi = 0x7fffffffffffffffLL;
   double s[LHC_R];
@@ -1734,7 +1745,7 @@ static __global__ void __launch_bounds__(256) k_lhc_rowmin(const double* __restr
       const double xj = pj[k];
 #pragma unroll
       for (int r = 0; r < LHC_R; ++r) {
-        const double t = lhc_sm[r * dim + k] - xj;
+        const double t = (kLds ? lhc_sm[r * dim + k] : prow[r][k]) - xj;
         s[r] = s[r] + t * t;
       }
     }

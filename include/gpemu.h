@@ -144,7 +144,7 @@ int gpe_kernel_grad(gpe_ctx* ctx, const double* delta, int32_t d, int64_t m, con
  * (fextra: ne x dim row-major, ne may be 0 / NULL): the condensed index of the closest
  * pair, first occurrence on ties, NaN distances count as the minimum.  Distances are
  * summed over dimensions in order without FMA, bit-identical to pdist's.  The caller
- * keeps the reference's rule (largest index wins, :62-67).  n + ne >= 2, dim <= 512. */
+ * keeps the reference's rule (largest index wins, :62-67).  n + ne >= 2. */
 int gpe_lhc_maximin(gpe_ctx* ctx, int32_t N, int64_t n, int32_t dim, const double* designs,
                     int64_t ne, const double* fextra, int64_t* idx_out);
 

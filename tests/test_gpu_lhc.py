@@ -76,8 +76,14 @@ def test_lhc_maximin_history_matching_size(ctx):
 def test_lhc_maximin_bad_args(ctx):
     with pytest.raises(RuntimeError):
         ctx.lhc_maximin(np.zeros((2, 1, 3)))       # one point: no pairs
-    with pytest.raises(RuntimeError):
-        ctx.lhc_maximin(np.zeros((1, 4, 600)))     # dim above 512
+
+
+def test_lhc_maximin_wide_points(ctx):
+    """dim above the LDS staging limit (512): row points read from global memory."""
+    rng = np.random.RandomState(6)
+    xs = _designs(rng, 3, 40, 600)
+    fe = rng.uniform(0, 1, (20, 600))
+    assert np.array_equal(ctx.lhc_maximin(xs, fe), lhc_maximin_ref(xs, fe))
 
 
 def test_olhc_reference_designs_on_gpu(tmp_path, capsys):
