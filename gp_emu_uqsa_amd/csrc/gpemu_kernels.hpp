@@ -628,6 +628,49 @@ __device__ __forceinline__ void gemm_sstore(double* lds, int buf, int tid, const
   }
 }
 
+// Direct global -> LDS staging (global_load_lds_dwordx4, no VGPR round trip; the
+// default unless GEMM_REGSTAGE).  One wave-instruction writes 64 x 16 B contiguous
+// from a wave-uniform LDS base, so:
+// - M-contiguous operand: one instruction = one k-row of 128 doubles, into the same
+//   [k][m] image (pitch GP) as the register path;
+// - K-contiguous operand: one instruction = 8 rows m of 16 doubles, into a [m][16]
+//   image whose 16-byte granules are XOR-swizzled (granule kp of row m at slot
+//   kp ^ ((m >> 1) & 7)); the swizzle is applied to the per-lane SOURCE address and
+//   undone by the fragment reads (kc_idx), which keeps ds_read_b64 conflict-free.
+__device__ __forceinline__ int kc_idx(int m, int k) {
+  return m * GK + (((((k >> 1) ^ (m >> 1)) & 7)) << 1) + (k & 1);
+}
+
+__device__ __forceinline__ void glds16(const double* src, double* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+template <bool AK, bool BK>
+__device__ __forceinline__ void gemm_glds(const double* __restrict__ Ab, const double* __restrict__ Bb,
+                                          long long lda, long long ldb, int k0, int tid, double* lds,
+                                          int buf) {
+  double* As = lds + buf * (2 * G_OPND);
+  double* Bs = As + G_OPND;
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int w = wave + 4 * s;   // wave-instruction index 0..15
+    if (!AK) {
+      glds16(Ab + 2 * lane + (long long)(k0 + w) * lda, As + w * GP);
+    } else {
+      const int m = 8 * w + (lane >> 3), kp = (lane & 7) ^ ((m >> 1) & 7);
+      glds16(Ab + (long long)m * lda + k0 + 2 * kp, As + 8 * w * GK);
+    }
+    if (!BK) {
+      glds16(Bb + 2 * lane + (long long)(k0 + w) * ldb, Bs + w * GP);
+    } else {
+      const int n = 8 * w + (lane >> 3), kp = (lane & 7) ^ ((n >> 1) & 7);
+      glds16(Bb + (long long)n * ldb + k0 + 2 * kp, Bs + 8 * w * GK);
+    }
+  }
+}
+
 // Optional tile list: entry = problem (8 bits) | ti (12 bits) | tj (12 bits), one per
 // workgroup, in the order the host chose (longest-first, rows grouped per XCD under
 // round-robin dispatch).  Speed only: any order gives the same result.
@@ -645,12 +688,20 @@ __device__ __forceinline__ void gemm_frags(const double* As, const double* Bs, i
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = wm + i * 16 + (lane & 15);
+#ifdef GEMM_REGSTAGE
     af[i] = AK ? As[m * GQ + krow] : As[krow * GP + m];
+#else
+    af[i] = AK ? As[kc_idx(m, krow)] : As[krow * GP + m];
+#endif
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int n = wn + j * 16 + (lane & 15);
+#ifdef GEMM_REGSTAGE
     bf[j] = BK ? Bs[n * GQ + krow] : Bs[krow * GP + n];
+#else
+    bf[j] = BK ? Bs[kc_idx(n, krow)] : Bs[krow * GP + n];
+#endif
   }
 }
 
@@ -673,15 +724,24 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
                                            d4 (&acc)[4][4]) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  double ra[8], rb[8];
   double fa0[4], fb0[4], fa1[4], fb1[4];
+#ifdef GEMM_REGSTAGE
+  double ra[8], rb[8];
   gemm_gload<AK, BK>(Ab, Bb, lda, ldb, kbeg, tid, ra, rb);
   gemm_sstore<AK, BK>(lds, 0, tid, ra, rb);
+#else
+  gemm_glds<AK, BK>(Ab, Bb, lda, ldb, kbeg, tid, lds, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
   __syncthreads();
   gemm_frags<AK, BK>(lds, lds + G_OPND, 0, lane, wm, wn, fa0, fb0);
   for (int s = 0; s < nk; ++s) {
     const bool more = s + 1 < nk;
+#ifdef GEMM_REGSTAGE
     if (more) gemm_gload<AK, BK>(Ab, Bb, lda, ldb, kbeg + (s + 1) * GK, tid, ra, rb);
+#else
+    if (more) gemm_glds<AK, BK>(Ab, Bb, lda, ldb, kbeg + (s + 1) * GK, tid, lds, (s + 1) & 1);
+#endif
     const double* As = lds + (s & 1) * (2 * G_OPND);
     const double* Bs = As + G_OPND;
     gemm_frags<AK, BK>(As, Bs, 1, lane, wm, wn, fa1, fb1);
@@ -696,7 +756,11 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
     gemm_mfmas<0, 12>(acc, fa1, fb1);
     __builtin_amdgcn_sched_barrier(0);
     if (more) {
+#ifdef GEMM_REGSTAGE
       gemm_sstore<AK, BK>(lds, (s + 1) & 1, tid, ra, rb);
+#else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stage s+1 pieces landed
+#endif
       __syncthreads();
       const double* An = lds + ((s + 1) & 1) * (2 * G_OPND);
       gemm_frags<AK, BK>(An, An + G_OPND, 0, lane, wm, wn, fa0, fb0);
