@@ -15,7 +15,6 @@ import numpy as np
 import pytest
 
 import gp_emu_uqsa_amd as g
-from gp_emu_uqsa_amd import native
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
