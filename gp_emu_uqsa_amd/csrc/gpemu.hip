@@ -232,12 +232,23 @@ inline int pmax_bucket(int P) { return P <= 8 ? 8 : (P <= 16 ? 16 : 32); }
 
 // ------------------------------------------------------------------ launches
 int launch_pairs(gpe_ctx* c, const PairArgs& a, int nblocks) {
-  const int dm = a.d <= 4 ? 4 : a.d <= 8 ? 8 : a.d <= 16 ? 16 : 32;
+  // the smallest padded width >= d (zero-padded dimensions cost one FMA each)
+  static constexpr int widths[] = {2, 4, 6, 8, 10, 12, 16, 20, 24, 32};
+  int dm = 32;
+  for (int w : widths)
+    if (a.d <= w) { dm = w; break; }
+  const dim3 g(nblocks), b(256);
   switch (dm) {
-    case 4: hipLaunchKernelGGL(k_pairs<4>, dim3(nblocks), dim3(256), 0, c->stream, a); break;
-    case 8: hipLaunchKernelGGL(k_pairs<8>, dim3(nblocks), dim3(256), 0, c->stream, a); break;
-    case 16: hipLaunchKernelGGL(k_pairs<16>, dim3(nblocks), dim3(256), 0, c->stream, a); break;
-    default: hipLaunchKernelGGL(k_pairs<32>, dim3(nblocks), dim3(256), 0, c->stream, a); break;
+    case 2: hipLaunchKernelGGL(k_pairs<2>, g, b, 0, c->stream, a); break;
+    case 4: hipLaunchKernelGGL(k_pairs<4>, g, b, 0, c->stream, a); break;
+    case 6: hipLaunchKernelGGL(k_pairs<6>, g, b, 0, c->stream, a); break;
+    case 8: hipLaunchKernelGGL(k_pairs<8>, g, b, 0, c->stream, a); break;
+    case 10: hipLaunchKernelGGL(k_pairs<10>, g, b, 0, c->stream, a); break;
+    case 12: hipLaunchKernelGGL(k_pairs<12>, g, b, 0, c->stream, a); break;
+    case 16: hipLaunchKernelGGL(k_pairs<16>, g, b, 0, c->stream, a); break;
+    case 20: hipLaunchKernelGGL(k_pairs<20>, g, b, 0, c->stream, a); break;
+    case 24: hipLaunchKernelGGL(k_pairs<24>, g, b, 0, c->stream, a); break;
+    default: hipLaunchKernelGGL(k_pairs<32>, g, b, 0, c->stream, a); break;
   }
   HIPCHK(c, hipGetLastError());
   return GPE_OK;

@@ -58,6 +58,10 @@ __device__ inline void tri_decode(int e, int& ti, int& tj) {
   tj = e - r * (r + 1) / 2;
 }
 
+// Coordinates are zero-padded to DMAX in registers and LDS, so the distance loop has
+// no per-dimension branch; the padded terms are fma(0, 0, s) = s, so the sum over
+// k = 0..d-1 is bit-identical to the unpadded one.  Padding, diagonal and zeroed
+// entries are selected after the general formula (no divergent paths per entry).
 template <int DMAX>
 static __global__ void __launch_bounds__(256) k_pairs(PairArgs a) {
   __shared__ double xs_col[TILE * DMAX];
@@ -66,9 +70,9 @@ static __global__ void __launch_bounds__(256) k_pairs(PairArgs a) {
   else { ti = blockIdx.x % a.mt; tj = blockIdx.x / a.mt; }
   const int tid = threadIdx.x;
   const int d = a.d;
-  for (int e = tid; e < TILE * d; e += 256) {
-    int c = e / d, k = e - c * d;
-    xs_col[e] = a.xc[(long long)(tj * TILE + c) * d + k];
+  for (int e = tid; e < TILE * DMAX; e += 256) {
+    const int c = e / DMAX, k = e - c * DMAX;
+    xs_col[e] = k < d ? a.xc[(long long)(tj * TILE + c) * d + k] : 0.0;
   }
   const int r = tid & (TILE - 1);
   const int gi = ti * TILE + r;
@@ -78,32 +82,31 @@ static __global__ void __launch_bounds__(256) k_pairs(PairArgs a) {
   __syncthreads();
   const double pre = a.s2 * a.coff;
   const bool train = (a.mode & 2) != 0;
+  const bool zero_diag = (a.mode & 8) != 0;
+  const bool row_pad = gi >= a.nr_valid;
+  double vdiag = a.s2 * a.cdiag;
+  if (train && a.r && ti == tj && !row_pad) vdiag += a.rscale * a.r[gi];
+  const double fi = a.fcol ? a.fcol[gi] : 0.0;
+  double* out = a.out + gi;
   for (int c = (tid >> 7); c < TILE; c += 2) {
     const int gj = tj * TILE + c;
-    double v;
-    if (train && (gi >= a.nr_valid || gj >= a.nc_valid)) {
-      v = (gi == gj) ? 1.0 : 0.0;
-    } else if (!train && (gi >= a.nr_valid || gj >= a.nc_valid)) {
-      v = 0.0;
-    } else if (train && gi == gj) {
-      v = a.s2 * a.cdiag + (a.r ? a.rscale * a.r[gi] : 0.0);
-    } else {
-      double s = 0.0;
+    double s = 0.0;
 #pragma unroll
-      for (int k = 0; k < DMAX; ++k) {
-        if (k < d) {
-          double df = xi[k] - xs_col[c * d + k];
-          s = fma(df, df, s);
-        }
-      }
-      v = pre * exp(-s);
-      if (a.fcol) {
-        const double df = (a.fcol[gi] - a.fcol[gj]) * a.fscale;
-        v *= df * df;
-      }
+    for (int k = 0; k < DMAX; ++k) {
+      const double df = xi[k] - xs_col[c * DMAX + k];
+      s = fma(df, df, s);
     }
-    if ((a.mode & 8) && gi == gj) v = 0.0;
-    a.out[(long long)gi + (long long)gj * a.ld] = v;
+    double v = pre * exp(-s);
+    if (a.fcol) {
+      const double df = (fi - a.fcol[gj]) * a.fscale;
+      v *= df * df;
+    }
+    const bool pad = row_pad || gj >= a.nc_valid;
+    const bool diag = gi == gj;
+    if (train) v = pad ? (diag ? 1.0 : 0.0) : (diag ? vdiag : v);
+    else v = pad ? 0.0 : v;
+    if (zero_diag && diag) v = 0.0;
+    out[(long long)gj * a.ld] = v;
     if ((a.mode & 4) && ti != tj) a.out[(long long)gj + (long long)gi * a.ld] = v;
   }
 }
