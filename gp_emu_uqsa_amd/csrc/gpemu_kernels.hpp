@@ -1491,13 +1491,15 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
   int ti, tj;
   tri_decode(blockIdx.x, ti, tj);
   const int tid = threadIdx.x;
-  for (int e = tid; e < TILE * d; e += 256) {
-    int c = e / d, k = e - c * d;
-    xs[c * DMAX + k] = xw[(long long)(tj * TILE + c) * d + k];
+  // zero-padded to DMAX / QMAX: the padded terms are exact no-ops (fma(-0, 0, m) = m,
+  // s + 0 = s), so the inner loops carry no per-dimension branch
+  for (int e = tid; e < TILE * DMAX; e += 256) {
+    const int c = e / DMAX, k = e - c * DMAX;
+    xs[e] = k < d ? xw[(long long)(tj * TILE + c) * d + k] : 0.0;
   }
-  for (int e = tid; e < TILE * q1; e += 256) {
-    int c = e / q1, k = e - c * q1;
-    ws[c * QMAX + k] = Wa[(long long)(tj * TILE + c) + (long long)k * ldw];
+  for (int e = tid; e < TILE * QMAX; e += 256) {
+    const int c = e / QMAX, k = e - c * QMAX;
+    ws[e] = k < q1 ? Wa[(long long)(tj * TILE + c) + (long long)k * ldw] : 0.0;
   }
   const int r = tid & (TILE - 1);
   const int gi = ti * TILE + r;
@@ -1529,29 +1531,22 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
         const int gj = tj * TILE + c;
         double mij = mv[u];
 #pragma unroll
-        for (int k = 0; k < QMAX; ++k)
-          if (k < q1) mij = fma(-wi[k], ws[c * QMAX + k], mij);
-        if (gj == gi) {
-          accT += mij;
-        } else {
-          double df2[DMAX];
-          double s = 0.0;
+        for (int k = 0; k < QMAX; ++k) mij = fma(-wi[k], ws[c * QMAX + k], mij);
+        double df2[DMAX];
+        double s = 0.0;
 #pragma unroll
-          for (int k = 0; k < DMAX; ++k) {
-            if (k < d) {
-              double df = xi[k] - xs[c * DMAX + k];
-              df2[k] = df * df;
-              s += df2[k];
-            } else {
-              df2[k] = 0.0;
-            }
-          }
-          const double me = mij * exp(-s);
-          accE += me;
-#pragma unroll
-          for (int k = 0; k < DMAX; ++k)
-            if (k < d) acc[k] = fma(me, df2[k], acc[k]);
+        for (int k = 0; k < DMAX; ++k) {
+          const double df = xi[k] - xs[c * DMAX + k];
+          df2[k] = df * df;
+          s += df2[k];
         }
+        // the diagonal entry goes to accT; adding the zeros the selects leave is exact
+        const bool dg = gj == gi;
+        accT += dg ? mij : 0.0;
+        const double me = dg ? 0.0 : mij * exp(-s);
+        accE += me;
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) acc[k] = fma(me, df2[k], acc[k]);
       }
     }
   }
