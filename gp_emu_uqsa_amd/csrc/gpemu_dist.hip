@@ -76,10 +76,12 @@ __global__ void __launch_bounds__(256) k_dist_kbuild(DistPairArgs a) {
     }
     return;
   }
+  // coordinates zero-padded to DMAX (exact no-op terms), entries selected, not branched:
+  // the same sums and values as the single-GPU k_pairs
   const int d = a.d;
-  for (int e = tid; e < TILE * d; e += 256) {
-    const int c = e / d, k = e - c * d;
-    xs_col[e] = a.xw[(long long)(tj * TILE + c) * d + k];
+  for (int e = tid; e < TILE * DMAX; e += 256) {
+    const int c = e / DMAX, k = e - c * DMAX;
+    xs_col[e] = k < d ? a.xw[(long long)(tj * TILE + c) * d + k] : 0.0;
   }
   const int gi = gt * TILE + r;
   double xi[DMAX];
@@ -87,24 +89,20 @@ __global__ void __launch_bounds__(256) k_dist_kbuild(DistPairArgs a) {
   for (int k = 0; k < DMAX; ++k) xi[k] = (k < d) ? a.xw[(long long)gi * d + k] : 0.0;
   __syncthreads();
   const double pre = a.s2 * a.coff;
+  const bool row_pad = gi >= a.n_valid;
+  double vdiag = a.s2 * a.cdiag;
+  if (a.r && gt == tj && !row_pad) vdiag += a.rscale * a.r[gi];
   for (int c = tid >> 7; c < TILE; c += 2) {
     const int gj = tj * TILE + c;
-    double v;
-    if (gi >= a.n_valid || gj >= a.n_valid) {
-      v = (gi == gj) ? 1.0 : 0.0;
-    } else if (gi == gj) {
-      v = a.s2 * a.cdiag + (a.r ? a.rscale * a.r[gi] : 0.0);
-    } else {
-      double s = 0.0;
+    double s = 0.0;
 #pragma unroll
-      for (int k = 0; k < DMAX; ++k) {
-        if (k < d) {
-          const double df = xi[k] - xs_col[c * d + k];
-          s = fma(df, df, s);
-        }
-      }
-      v = pre * exp(-s);
+    for (int k = 0; k < DMAX; ++k) {
+      const double df = xi[k] - xs_col[c * DMAX + k];
+      s = fma(df, df, s);
     }
+    double v = pre * exp(-s);
+    const bool diag = gi == gj;
+    v = (row_pad || gj >= a.n_valid) ? (diag ? 1.0 : 0.0) : (diag ? vdiag : v);
     out[r + (long long)c * a.ld] = v;
   }
 }
@@ -637,7 +635,9 @@ int kbuild(gpe_dist* h, int kernel, double nu, double s2, double rscale) {
     const dim3 grid((unsigned)(R.nloc * (h->NB + 1)));
     if (h->d <= 4) hipLaunchKernelGGL(k_dist_kbuild<4>, grid, dim3(256), 0, h->stream, a);
     else if (h->d <= 8) hipLaunchKernelGGL(k_dist_kbuild<8>, grid, dim3(256), 0, h->stream, a);
+    else if (h->d <= 10) hipLaunchKernelGGL(k_dist_kbuild<10>, grid, dim3(256), 0, h->stream, a);
     else if (h->d <= 16) hipLaunchKernelGGL(k_dist_kbuild<16>, grid, dim3(256), 0, h->stream, a);
+    else if (h->d <= 20) hipLaunchKernelGGL(k_dist_kbuild<20>, grid, dim3(256), 0, h->stream, a);
     else hipLaunchKernelGGL(k_dist_kbuild<32>, grid, dim3(256), 0, h->stream, a);
     DCHK_HIP(h, hipGetLastError());
   }

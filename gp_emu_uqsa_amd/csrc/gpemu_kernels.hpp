@@ -1608,13 +1608,14 @@ static __global__ void __launch_bounds__(256) k_sense_pairs(const double* Ainv, 
   const int cbeg = blockIdx.z * cslice, cfin = min(n_valid, cbeg + cslice);
   for (int c0 = cbeg; c0 < cfin; c0 += SP_CT) {
     __syncthreads();
-    for (int e = tid; e < SP_CT * d; e += 256) {
-      const int c = e / d, k = e - c * d, g = c0 + c;
-      xs[c * DMAX + k] = g < n_valid ? x[(long long)g * d + k] : 0.0;
+    // zero-padded to DMAX / PMAX, so the loops below carry no per-dimension branch
+    for (int e = tid; e < SP_CT * DMAX; e += 256) {
+      const int c = e / DMAX, k = e - c * DMAX, g = c0 + c;
+      xs[e] = (k < d && g < n_valid) ? x[(long long)g * d + k] : 0.0;
     }
-    for (int e = tid; e < SP_CT * p; e += 256) {
+    for (int e = tid; e < SP_CT * PMAX; e += 256) {
       const int c = e % SP_CT, k = e / SP_CT, g = c0 + c;
-      zs[c * PMAX + k] = g < n_valid ? Z[g + (long long)k * ldz] : 0.0;
+      zs[c * PMAX + k] = (k < p && g < n_valid) ? Z[g + (long long)k * ldz] : 0.0;
     }
     if (tid < SP_CT) us[tid] = (c0 + tid < n_valid) ? u[j * ldu + c0 + tid] : 0.0;
     __syncthreads();
@@ -1625,16 +1626,16 @@ static __global__ void __launch_bounds__(256) k_sense_pairs(const double* Ainv, 
         double s = 0.0;
 #pragma unroll
         for (int k = 0; k < DMAX; ++k) {
-          if (k < d) {
-            const double df = xi[k] - xs[c * DMAX + k];
-            s = fma(wj[k] * df, df, s);
-          }
+          const double df = xi[k] - xs[c * DMAX + k];
+          s = fma(wj[k] * df, df, s);
         }
         const double K = ui * us[c] * exp(-s);
 #pragma unroll
-        for (int q = 0; q < PMAX; ++q)
-          if (q < p) v[q] = fma(K, zs[c * PMAX + q], v[q]);
-        if (gj <= gi) acc = fma(gj == gi ? K : 2.0 * K, Ainv[gi + (long long)gj * lda], acc);
+        for (int q = 0; q < PMAX; ++q) v[q] = fma(K, zs[c * PMAX + q], v[q]);
+        // lower triangle only (the upper one is not stored): a masked load, then an
+        // exact no-op fma(0, 0, acc) above the diagonal
+        const double av = gj <= gi ? Ainv[gi + (long long)gj * lda] : 0.0;
+        acc = fma(gj < gi ? 2.0 * K : (gj == gi ? K : 0.0), av, acc);
       }
     }
   }
