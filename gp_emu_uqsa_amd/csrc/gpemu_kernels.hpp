@@ -717,10 +717,17 @@ __device__ __forceinline__ void gemm_mfmas(d4 (&acc)[4][4], const double (&af)[4
 }
 
 // K loop of one 128x128 output tile: acc += opA(Ab) opB(Bb) over nk stages of GK.
-// Software pipeline: the fragments of the next k-step are read while the 16 MFMAs
-// of the current one issue; at a stage boundary the last 4 MFMAs are held back
-// until the next stage's first fragments are in flight (sched_barrier keeps the
-// compiler from regrouping).
+// Software pipeline (source order): the fragments of the next k-step are read while
+// the 16 MFMAs of the current one issue; at a stage boundary the last 4 MFMAs are
+// held back until the next stage's first fragments are in flight.
+// Order pins between the MFMA clusters: needed by the register-staging path, whose
+// fragment reads the compiler otherwise sinks behind the MFMAs; with direct global->LDS
+// staging the compiler's own schedule is ~1% faster, so no pins.
+#ifdef GEMM_REGSTAGE
+#define GEMM_SB() __builtin_amdgcn_sched_barrier(0)
+#else
+#define GEMM_SB() do {} while (0)
+#endif
 template <bool AK, bool BK>
 __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
                                            long long lda, long long ldb, int kbeg, int nk, double* lds,
@@ -749,15 +756,15 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
     const double* Bs = As + G_OPND;
     gemm_frags<AK, BK>(As, Bs, 1, lane, wm, wn, fa1, fb1);
     gemm_mfmas<0, 16>(acc, fa0, fb0);
-    __builtin_amdgcn_sched_barrier(0);
+    GEMM_SB();
     gemm_frags<AK, BK>(As, Bs, 2, lane, wm, wn, fa0, fb0);
     gemm_mfmas<0, 16>(acc, fa1, fb1);
-    __builtin_amdgcn_sched_barrier(0);
+    GEMM_SB();
     gemm_frags<AK, BK>(As, Bs, 3, lane, wm, wn, fa1, fb1);
     gemm_mfmas<0, 16>(acc, fa0, fb0);
-    __builtin_amdgcn_sched_barrier(0);
+    GEMM_SB();
     gemm_mfmas<0, 12>(acc, fa1, fb1);
-    __builtin_amdgcn_sched_barrier(0);
+    GEMM_SB();
     if (more) {
 #ifdef GEMM_REGSTAGE
       gemm_sstore<AK, BK>(lds, (s + 1) & 1, tid, ra, rb);
@@ -768,9 +775,9 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
       const double* An = lds + ((s + 1) & 1) * (2 * G_OPND);
       gemm_frags<AK, BK>(An, An + G_OPND, 0, lane, wm, wn, fa0, fb0);
     }
-    __builtin_amdgcn_sched_barrier(0);
+    GEMM_SB();
     gemm_mfmas<12, 16>(acc, fa1, fb1);
-    __builtin_amdgcn_sched_barrier(0);
+    GEMM_SB();
   }
   __syncthreads();   // callers reuse the staging LDS
 }
