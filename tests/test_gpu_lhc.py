@@ -92,3 +92,14 @@ def test_olhc_reference_designs_on_gpu(tmp_path, capsys):
         f = str(tmp_path / ("imp_input_" + tag))
         design_inputs.optLatinHyperCube(1, 20, 10, [[0.0, 1.0]], f)
         assert np.array_equal(np.loadtxt(f), G["design_" + tag]), tag
+
+
+def test_lhc_maximin_more_designs_than_one_launch(ctx):
+    """N above the 65535 designs of one launch: the native loop runs two batches."""
+    rng = np.random.RandomState(8)
+    xs = rng.uniform(0, 1, (70000, 3, 2))
+    fe = rng.uniform(0, 1, (2, 2))
+    got = ctx.lhc_maximin(xs, fe)
+    ref = lhc_maximin_ref(xs[::997], fe)
+    assert np.array_equal(got[::997], ref)
+    assert np.array_equal(got[65530:65540], lhc_maximin_ref(xs[65530:65540], fe))
