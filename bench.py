@@ -62,6 +62,28 @@ def eval_point(d, rank):
     return np.concatenate([delta, [1e-3, 1.0]])
 
 
+def _host_info():
+    """The CPU the baseline ran on: model, logical CPUs, BLAS build."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    blas = None
+    try:
+        from threadpoolctl import threadpool_info
+        libs = [i for i in threadpool_info() if i.get("user_api") == "blas"]
+        if libs:
+            blas = f"{libs[0].get('internal_api')} {libs[0].get('version')} ({libs[0].get('architecture')})"
+    except Exception:
+        pass
+    return {"cpu_model": model, "logical_cpus": os.cpu_count(), "blas": blas}
+
+
 def cpu_baseline(d):
     """Op-for-op NumPy/SciPy restatement of the reference objective (oracle
     ref-mode: pdist/squareform, np.linalg.cholesky, LU-based np.linalg.solve for
@@ -96,6 +118,7 @@ def cpu_baseline(d):
     tf = time.perf_counter() - t
     tf16k = tf * (16384 / hi) ** 3
     return {"value": 1.0 / t16k, "unit": "evals/s", "cores": int(threads), "kind": "port",
+            "host": _host_info(),
             "sample": (f"oracle ref-mode (reference op order, NumPy/OpenBLAS, {threads} threads), d={d}: "
                        f"n={lo} {times[lo]:.2f} s/eval, n={hi} {times[hi]:.2f} s/eval (fitted exponent "
                        f"{p:.2f}); n=16384 = n={hi} x (16384/{hi})^3 -> {t16k:.0f} s/eval"),
