@@ -8,16 +8,25 @@ sigma=1.  Each GPU keeps --concurrent (default 2) multistart tries in flight, as
 g.train() does at this size: one context (HIP stream, workspaces) and one host
 thread per try, each at its own point.  One step = one evaluation of every try.
 
-Multi-GPU: `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`
-runs one replica per GPU (independent multistart evaluations, no data-path
-collective; gloo is used only for the barrier and the max-over-ranks timing).
-value = evaluations completed by all ranks / the slowest rank's time.
+Processes: one per GPU.  `python bench.py --gpus N` starts its N ranks itself
+(before anything touches a GPU); under `python -m torch.distributed.run
+--nproc-per-node N bench.py --gpus N` the launcher has set RANK / WORLD_SIZE /
+LOCAL_RANK and --gpus must equal WORLD_SIZE.  No PyTorch in any rank: barriers
+and the max over ranks go through gp_emu_uqsa_amd/rendezvous.py, device
+synchronisation through libgpemu.so.  The headline runs one replica per GPU
+(independent multistart evaluations, no data-path collective; value =
+evaluations by all ranks / the slowest rank's time).  With N > 1 the line also
+carries `extra.rowblock`: BASELINE configs[3] (n=65536, d=20) LLH + gradient as
+ONE evaluation spread over the N GPUs by the row-block distributed objective
+over RCCL (include/gpemu_dist.h), its collective time, and a rank-0 parity check
+against the single-GPU objective.
 
 Also reported: the roofline of the dominant kernel (the MFMA GEMM: algorithmic
 flops per launch / mean launch time from HIP events on its own stream, recorded
-live on the last timed step -- events on every step would add ~1.5 ms per eval), HBM traffic per GEMM launch from the committed rocprofv3 PMC
-summary (profiles/), and a CPU baseline (the op-for-op NumPy restatement of the
-reference, oracle/gp_oracle.py, on this host's cores; rank 0, N=1 only).
+live on the last timed step), its HBM traffic per launch from the committed
+rocprofv3 PMC pass (profiles/, labelled), and a CPU baseline (the op-for-op
+NumPy restatement of the reference, oracle/gp_oracle.py, on this host's cores;
+rank 0, N=1 only).
 """
 from __future__ import annotations
 
@@ -25,7 +34,9 @@ import argparse
 import glob
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import threading
 import time
 
@@ -36,9 +47,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "log-marginal-likelihood evals/sec at n=16384 d=10 fp64; 1/2/4/8 GPU"
 FP64_MFMA_PEAK_TFLOPS = 78.6       # MI355X dense fp64 matrix peak (spec)
+C4 = (65536, 20)                   # BASELINE.json configs[3]
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -46,6 +58,8 @@ def parse():
     ap.add_argument("--n", type=int, default=16384)
     ap.add_argument("--d", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-full", action="store_true",
+                    help="also time the CPU fast-mode objective at the full n (~2-3 min)")
     ap.add_argument("--no-profile", action="store_true",
                     help="time without per-launch HIP events (roofline omitted)")
     ap.add_argument("--no-other-configs", dest="other_configs", action="store_false",
@@ -53,7 +67,53 @@ def parse():
     ap.add_argument("--concurrent", type=int, default=2,
                     help="multistart tries in flight per GPU (own context and HIP stream each), "
                          "as g.train() runs them at this size (optimize.Optimize._concurrency)")
-    return ap.parse_args()
+    ap.add_argument("--no-rowblock", dest="rowblock", action="store_false",
+                    help="N > 1: skip the row-block distributed configs[3] leg")
+    ap.add_argument("--rowblock-n", type=int, default=C4[0])
+    ap.add_argument("--rowblock-d", type=int, default=C4[1])
+    ap.add_argument("--rowblock-steps", type=int, default=2)
+    ap.add_argument("--rowblock-timeout", type=float, default=300.0)
+    ap.add_argument("--rendezvous-check", action="store_true",
+                    help="(test hook) spawn / rendezvous only: no GPU, rank 0 prints the ranks it saw")
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# launcher: N rank processes, started before anything touches a GPU
+# ---------------------------------------------------------------------------
+def spawn_ranks(nprocs: int, argv: list[str]) -> int:
+    """Run this script as `nprocs` rank processes on this node (RANK = LOCAL_RANK =
+    0..N-1, WORLD_SIZE = N, a fresh rendezvous directory) and return the first
+    non-zero exit status, or 0.  If a rank fails the others are stopped."""
+    rdzv = tempfile.mkdtemp(prefix="gpemu-bench-")
+    procs = []
+    try:
+        for r in range(nprocs):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs),
+                       LOCAL_WORLD_SIZE=str(nprocs), MASTER_ADDR="127.0.0.1",
+                       GPEMU_RDZV_DIR=rdzv)
+            env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+        rc = 0
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in pending:      # the exact PIDs this launcher started
+                        q.terminate()
+            time.sleep(0.05)
+        return rc
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        import shutil
+        shutil.rmtree(rdzv, ignore_errors=True)
 
 
 def eval_point(d, rank):
@@ -62,77 +122,115 @@ def eval_point(d, rank):
     return np.concatenate([delta, [1e-3, 1.0]])
 
 
+# ---------------------------------------------------------------------------
+# CPU baseline (rank 0, N=1 only)
+# ---------------------------------------------------------------------------
 def _host_info():
-    """The CPU the baseline ran on: model, logical CPUs, BLAS build."""
-    model = None
+    """The CPU the baseline ran on: model, logical and physical CPUs,
+    this process's affinity, the cgroup CPU quota, BLAS build."""
+    info = {"cpu_model": None, "logical_cpus": os.cpu_count()}
     try:
+        cores = set()
+        phys = core = None
         with open("/proc/cpuinfo") as fh:
             for line in fh:
-                if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
+                if line.startswith("model name") and info["cpu_model"] is None:
+                    info["cpu_model"] = line.split(":", 1)[1].strip()
+                elif line.startswith("physical id"):
+                    phys = line.split(":", 1)[1].strip()
+                elif line.startswith("core id"):
+                    core = line.split(":", 1)[1].strip()
+                    cores.add((phys, core))
+        info["physical_cores"] = len(cores) or None
     except OSError:
         pass
-    blas = None
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity_cpus"] = None
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_cpu_quota"] = quota
     try:
         from threadpoolctl import threadpool_info
         libs = [i for i in threadpool_info() if i.get("user_api") == "blas"]
         if libs:
-            blas = f"{libs[0].get('internal_api')} {libs[0].get('version')} ({libs[0].get('architecture')})"
+            info["blas"] = f"{libs[0].get('internal_api')} {libs[0].get('version')} ({libs[0].get('architecture')})"
     except Exception:
         pass
-    return {"cpu_model": model, "logical_cpus": os.cpu_count(), "blas": blas}
+    return info
 
 
-def cpu_baseline(d):
-    """Op-for-op NumPy/SciPy restatement of the reference objective (oracle
-    ref-mode: pdist/squareform, np.linalg.cholesky, LU-based np.linalg.solve for
-    every triangular solve, one dense dA per hyperparameter) timed once at
-    n=1536 and once at n=3072 on this host (~10 s of CPU work in all).  The
-    n=16384 time is the n=3072 time scaled by (16384/3072)^3: the reference's
-    evaluation is ~68 n^3 flops of LAPACK LU solves, and an
-    exponent fitted between two small sizes is not stable (BLAS efficiency still
-    grows with n there).  (In the survey container the reference itself measured
-    1230.7 s at n=16384 on 8 cores.)"""
+def cpu_baseline(d, n_full, full=False):
+    """The oracle's ref-mode (op-for-op restatement of the reference: pdist /
+    squareform, np.linalg.cholesky, LU-based np.linalg.solve for every triangular
+    solve, one dense dA per hyperparameter) MEASURED at n=4096 (BASELINE configs[1]),
+    3 repetitions, median, with the BLAS on every CPU this process may use (the
+    affinity mask, capped by the cgroup quota).  The n=16384 value is that time
+    scaled by (16384/4096)^3 -- the reference's evaluation is ~68 n^3 flops of
+    LAPACK LU solves -- and is labelled an estimate; the reference
+    itself measured 1230.7 s at n=16384 on 8 cores in the survey container.
+    fast_mode: the GPU's formulation on LAPACK (Cholesky, explicit inverse,
+    contraction), measured at n=4096, and with full=True at n=16384 itself."""
     from oracle import gp_oracle as orc
+    host = _host_info()
+    threads = host.get("affinity_cpus") or os.cpu_count() or 1
+    if host.get("cgroup_cpu_quota"):
+        threads = max(1, min(threads, int(host["cgroup_cpu_quota"])))
     try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()
-                       if i.get("user_api") == "blas"] or [1])
+        from threadpoolctl import threadpool_limits
+        limiter = threadpool_limits(limits=threads, user_api="blas")
     except Exception:
-        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    times = {}
-    lo, hi = 1536, 3072
-    for n in (lo, hi):
-        X, f, H = orc.synthetic_problem(n, d, seed=0)
+        limiter = None
+    try:
+        n2 = 4096
+        X, f, H = orc.synthetic_problem(n2, d, seed=0)
+        hp = eval_point(d, 0)
+        reps = []
+        for _ in range(3):
+            t = time.perf_counter()
+            orc.objective_ref(X, f, H, hp, orc.GP4ML, orc.STD, True)
+            reps.append(time.perf_counter() - t)
+        t2 = float(np.median(reps))
+        scale = (n_full / n2) ** 3
         t = time.perf_counter()
-        orc.objective_ref(X, f, H, eval_point(d, 0), orc.GP4ML, orc.STD, True)
-        times[n] = time.perf_counter() - t
-    p = np.log(times[hi] / times[lo]) / np.log(hi / lo)
-    t16k = times[hi] * (16384 / hi) ** 3
-    # best-effort CPU formulation (SURVEY 8d "fast-mode"): Cholesky, explicit inverse,
-    # Frobenius-contraction gradient, i.e. the GPU's algorithm on LAPACK
-    X, f, H = orc.synthetic_problem(hi, d, seed=0)
-    t = time.perf_counter()
-    orc.objective_fast(X, f, H, eval_point(d, 0), orc.GP4ML, orc.STD, True)
-    tf = time.perf_counter() - t
-    tf16k = tf * (16384 / hi) ** 3
-    return {"value": 1.0 / t16k, "unit": "evals/s", "cores": int(threads), "kind": "port",
-            "host": _host_info(),
-            "sample": (f"oracle ref-mode (reference op order, NumPy/OpenBLAS, {threads} threads), d={d}: "
-                       f"n={lo} {times[lo]:.2f} s/eval, n={hi} {times[hi]:.2f} s/eval (fitted exponent "
-                       f"{p:.2f}); n=16384 = n={hi} x (16384/{hi})^3 -> {t16k:.0f} s/eval"),
-            "fast_mode": {"value": 1.0 / tf16k, "unit": "evals/s",
-                          "sample": (f"oracle fast-mode (Cholesky + inverse + contraction, the GPU's "
-                                     f"algorithm on LAPACK), n={hi} {tf:.2f} s/eval; n=16384 = "
-                                     f"x (16384/{hi})^3 -> {tf16k:.0f} s/eval")}}
+        orc.objective_fast(X, f, H, hp, orc.GP4ML, orc.STD, True)
+        tf2 = time.perf_counter() - t
+        fast = {"n4096_s_per_eval": tf2, "value_estimate": 1.0 / (tf2 * scale), "unit": "evals/s",
+                "sample": f"oracle fast-mode at n={n2}, {tf2:.2f} s/eval; n={n_full} estimate = x (n/{n2})^3"}
+        if full:
+            Xf, ff, Hf = orc.synthetic_problem(n_full, d, seed=0)
+            t = time.perf_counter()
+            orc.objective_fast(Xf, ff, Hf, hp, orc.GP4ML, orc.STD, True)
+            tff = time.perf_counter() - t
+            fast.update({"value": 1.0 / tff, "measured_s_per_eval": tff,
+                         "sample": f"oracle fast-mode measured at n={n_full}: {tff:.1f} s/eval"})
+    finally:
+        if limiter is not None:
+            limiter.unregister()
+    return {"value": 1.0 / (t2 * scale), "unit": "evals/s", "cores": int(threads), "kind": "port",
+            "host": host,
+            "c2_n4096": {"s_per_eval_median": t2, "reps_s": reps, "evals_per_s": 1.0 / t2},
+            "sample": (f"oracle ref-mode (reference op order, NumPy/OpenBLAS, {threads} threads) measured at "
+                       f"n={n2} d={d} (BASELINE configs[1]): 3 reps, median {t2:.2f} s/eval; n={n_full} value is "
+                       f"an ESTIMATE = x ({n_full}/{n2})^3 -> {t2 * scale:.0f} s/eval"),
+            "fast_mode": fast}
 
 
+# ---------------------------------------------------------------------------
+# informational legs (rank 0, after the timed region)
+# ---------------------------------------------------------------------------
 def other_configs(native, synthetic, ctx, args):
-    """Informational, after the timed region (rank 0): BASELINE.json configs[1]
-    (n=4096, d=10: one LLH+grad and one value-only evaluation, single stream) and
-    configs[4] (n=16384, d=10 emulator, posterior mean + diagonal variance at m=1e6
-    points, precision 32).  The headline metric stays configs[2]."""
+    """BASELINE.json configs[1] (n=4096, d=10: one LLH+grad and one value-only
+    evaluation, single stream) and configs[4] (n=16384, d=10 emulator, posterior
+    mean + diagonal variance at m=1e6 points, precision 32).  The headline metric
+    stays configs[2]."""
     out = {}
     X, f, H = synthetic.problem(4096, 10, seed=0)
     c = native.Context(ctx.device)
@@ -160,6 +258,101 @@ def other_configs(native, synthetic, ctx, args):
     return out
 
 
+def rowblock_leg(native, synthetic, group, rank, world, local, args, sync_all):
+    """configs[3]: one LLH+gradient (and one value-only evaluation) of n x n spread
+    over the `world` GPUs by the row-block distributed objective over RCCL; time =
+    max over ranks; rank 0 then checks value and gradient against the single-GPU
+    objective (tolerances as tests/test_gpu_fullsize.py)."""
+    from gp_emu_uqsa_amd import distributed
+    n, d = args.rowblock_n, args.rowblock_d
+    X, f, H = synthetic.problem(n, d, seed=0)
+    hp = eval_point(d, 0)
+    dc = distributed.dist_context(local, group)
+    dc.set_data(X, f, H)
+    llh, g, _ = dc.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=True)   # allocates
+    sync_all()
+    t0 = time.perf_counter()
+    comm = []
+    for _ in range(args.rowblock_steps):
+        llh, g, _ = dc.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=True)
+        comm.append(dc.times()["comm_ms"])
+    sync_all()
+    t_grad = group.all_reduce_max((time.perf_counter() - t0) / args.rowblock_steps)
+    t0 = time.perf_counter()
+    dc.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=False)
+    sync_all()
+    t_val = group.all_reduce_max(time.perf_counter() - t0)
+    comm_val = dc.times()["comm_ms"]
+    rank_gb = group.all_gather(dc.rank_bytes() / 1e9)
+    dc.close()
+    out = None
+    if rank == 0:
+        c = native.Context(local)
+        c.set_data(X, f, H)
+        ref, gref, _ = c.objective(native.GP4ML, native.KERNEL_STD, hp)
+        c.close()
+        rel_llh = abs(llh - ref) / abs(ref)
+        rel_g = float(np.max(np.abs(np.asarray(g) - gref)) / np.max(np.abs(gref)))
+        flops = float(n) ** 3   # algorithmic: n^3/3 each for POTRF, TRTRI and the A^-1 partials
+        out = {"config": f"BASELINE configs[3]: gp4ml LLH+grad n={n} d={d}, one evaluation over {world} GPUs "
+                         f"(row-block cyclic tile rows, RCCL)",
+               "n": n, "d": d, "ranks": world,
+               "llh_grad_ms": 1000.0 * t_grad, "value_only_ms": 1000.0 * t_val,
+               "comm_ms_llh_grad": float(np.mean(comm)), "comm_ms_value_only": comm_val,
+               "algorithmic_tflops": flops / t_grad / 1e12,
+               "per_rank_device_gb": rank_gb,
+               "parity_vs_single_gpu": {"llh_rel": rel_llh, "grad_max_rel": rel_g,
+                                        "ok": bool(rel_llh <= 1e-10 and rel_g <= 1e-8)}}
+    return out
+
+
+_EMIT = threading.Lock()
+_EMITTED = [False]
+
+
+def emit(out):
+    """Rank 0's one JSON line, at most once (the row-block watchdog may print it)."""
+    with _EMIT:
+        if not _EMITTED[0]:
+            _EMITTED[0] = True
+            print(json.dumps(out), flush=True)
+
+
+def guarded_rowblock(native, synthetic, group, rank, world, local, args, sync_all, out):
+    """rowblock_leg behind a pre-flight check and a watchdog, so that the headline
+    line survives a row-block failure: every rank first reports whether its GPU is
+    visible; a failure on any rank makes all skip; an exception is recorded; and if
+    the leg outlives --rowblock-timeout (a rank stuck in a collective), rank 0
+    prints the line with the error and every rank exits."""
+    if os.environ.get("GPEMU_BENCH_ONE_DEVICE") == "1":
+        return {"skipped": "one-device rehearsal: RCCL refuses two ranks on one GPU"}
+    ok = native.load_library().gpe_device_count() > local
+    if not all(group.all_gather(bool(ok))):
+        return {"skipped": "a rank does not see its GPU"}
+    done = threading.Event()
+
+    def watchdog():
+        if done.wait(args.rowblock_timeout):
+            return
+        if rank == 0:
+            out.setdefault("extra", {})["rowblock"] = {"error": f"timed out after {args.rowblock_timeout:.0f} s"}
+            emit(out)
+        sys.stdout.flush()
+        os._exit(0 if rank == 0 else 3)
+
+    threading.Thread(target=watchdog, daemon=True).start()
+    try:
+        res = rowblock_leg(native, synthetic, group, rank, world, local, args, sync_all)
+        err = None
+    except Exception as e:   # recorded in the line; the headline stands
+        res, err = None, f"{type(e).__name__}: {e}"
+    errs = [e for e in group.all_gather(err) if e]
+    done.set()
+    if errs:
+        return {"error": errs[0]}
+    return res
+
+
 def pmc_traffic(n, d):
     """HBM bytes per GEMM launch from the committed rocprofv3 PMC summary."""
     best = None
@@ -169,28 +362,46 @@ def pmc_traffic(n, d):
         except Exception:
             continue
         if rec.get("n") == n and rec.get("d") == d:
-            best = rec
-    return None if best is None else best.get("bytes_per_gemm_launch")
+            best = (os.path.relpath(path, ROOT), rec)
+    if best is None:
+        return None, None
+    return best[1].get("bytes_per_gemm_launch"), best[0]
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, argv))
+    world = int(world_env or 1)
+    if args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
     if os.environ.get("GPEMU_BENCH_ONE_DEVICE") == "1":
         local = 0   # rehearsal of the N-rank path with every rank on GPU 0 (one-GPU box)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    import torch
-    have_torch_gpu = torch.cuda.is_available()
-    if have_torch_gpu:
-        torch.cuda.set_device(local)
 
-    from gp_emu_uqsa_amd import native
-    from gp_emu_uqsa_amd import synthetic
+    from gp_emu_uqsa_amd import rendezvous
+    group = rendezvous.init_from_env() if world > 1 else None
+
+    if args.rendezvous_check:   # spawn / rendezvous test hook: no GPU
+        seen = group.all_gather([rank, local, world]) if group else [[rank, local, world]]
+        mx = group.all_reduce_max(float(rank)) if group else 0.0
+        if group:
+            group.barrier()
+        if rank == 0:
+            print(json.dumps({"ranks": seen, "max_rank": mx}), flush=True)
+        if group:
+            group.close()
+        return
+
+    from gp_emu_uqsa_amd import native, synthetic
+
+    def sync_all():
+        native.device_synchronize(local)
+        if group is not None:
+            group.barrier()
 
     K = max(1, args.concurrent)
     X, f, H = synthetic.problem(args.n, args.d, seed=0)
@@ -203,12 +414,6 @@ def main():
     hps = [eval_point(args.d, rank * K + k) for k in range(K)]   # one multistart point per try
     prof = not args.no_profile
     last = [None] * K
-
-    def sync_all():
-        if have_torch_gpu:
-            torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
 
     def run_tries(count):
         """Each of the K contexts evaluates `count` times, all K in flight at once
@@ -251,10 +456,8 @@ def main():
     sync_all()
     elapsed = time.perf_counter() - t0
     llh = last[0][0]
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    if group is not None:
+        elapsed = group.all_reduce_max(elapsed)
     # informational, outside the timed region: one eval alone (latency) and value-only
     t1 = time.perf_counter()
     ctx.objective(native.GP4ML, native.KERNEL_STD, hps[0])
@@ -263,7 +466,9 @@ def main():
     ctx.objective(native.GP4ML, native.KERNEL_STD, hps[0], want_grad=False)
     value_only_s = time.perf_counter() - t1
     other = other_configs(native, synthetic, ctx, args) if (rank == 0 and args.other_configs) else None
-
+    if group is not None:
+        group.barrier()
+    out = None
     if rank == 0:
         n_units = world * args.steps * K
         out = {
@@ -287,29 +492,42 @@ def main():
         }
         if prof and gemm_ms > 0:
             achieved = gemm_fl / (gemm_ms * 1e-3) / 1e12
+            traffic, tsrc = pmc_traffic(args.n, args.d)
             out["roofline"] = {"bound": "mfma", "achieved": achieved,
                                "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                                "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
-                               "traffic": pmc_traffic(args.n, args.d),
+                               "traffic": traffic,
+                               "traffic_source": (f"{tsrc}: rocprofv3 --pmc passes of this bench command "
+                                                  f"(committed, not measured in this run)") if tsrc else None,
                                "kernel": "k_gemm (fp64 v_mfma_f64_16x16x4_f64)",
                                "flops_per_launch": gemm_fl / gemm_n,
                                "ms_per_launch": gemm_ms / gemm_n}
             whole = K * 4398e9 * (args.n / 16384) ** 3 / 1e12   # ~n^3 algorithmic flops per eval
+            step_tflops = whole / (elapsed / args.steps)
             out["extra"] = {"phase_ms": {k: v / max(prof_steps, 1) for k, v in phase_acc.items()},
                             "roofline_sample": f"HIP events around every GEMM launch of timed step "
                                                f"{args.steps} (its {K} evals run one at a time)",
-                            "eval_tflops_algorithmic": whole / (elapsed / args.steps),
+                            "eval_tflops_algorithmic": step_tflops,
+                            "step_level_frac": step_tflops / FP64_MFMA_PEAK_TFLOPS,
                             "single_eval_ms": 1000.0 * single_s,
                             "value_only_ms": 1000.0 * value_only_s,
                             "other_configs": other,
                             "llh": llh}
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.d)
-        print(json.dumps(out), flush=True)
+            out["cpu_baseline"] = cpu_baseline(args.d, args.n, full=args.cpu_full)
+    if world > 1 and args.rowblock:
+        for c in ctxs:          # the replica workspaces are not needed by the row-block leg
+            c.close()
+        ctxs = []
+        rb = guarded_rowblock(native, synthetic, group, rank, world, local, args, sync_all, out)
+        if rank == 0:
+            out.setdefault("extra", {})["rowblock"] = rb
+    if rank == 0:
+        emit(out)
     for c in ctxs:
         c.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    if group is not None:
+        group.close()
 
 
 if __name__ == "__main__":

@@ -841,6 +841,11 @@ int gpe_device_count(void) {
   return n;
 }
 
+int gpe_device_synchronize(int32_t device) {
+  if (hipSetDevice(device) != hipSuccess) return GPE_ERR_HIP;
+  return hipDeviceSynchronize() == hipSuccess ? GPE_OK : GPE_ERR_HIP;
+}
+
 gpe_ctx* gpe_create(int32_t device) {
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);

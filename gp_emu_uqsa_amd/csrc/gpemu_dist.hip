@@ -11,23 +11,30 @@
 //   owner(k): A(k,k) -= L(k,gb:k) L(k,gb:k)^T, -> L_kk (in place), Dinv = L_kk^-1
 //             (k_gemm G_DIAG, 1 workgroup); every rank: its panel tiles
 //             A(i,k) -= L(i,gb:k) L(k,gb:k)^T (same launch; row k from the gathered panels)
-//   RCCL broadcast of Dinv from owner(k)                    (128 KB)
+//   broadcast of Dinv from owner(k)                          (128 KB)
 //   panel:   L(i,k) = A(i,k) Dinv^T for its rows i > k      (k_gemm)
-//   pack its panel tiles, RCCL all-gather, unpermute into the group's panel block k-gb
+//   pack its panel tiles, all-gather, unpermute into the group's panel block k-gb
 //   k = ge-1: A(i,j) -= L(i,gb:ge) L(j,gb:ge)^T, its rows, ge <= j <= i
 //             (k_gemm, tile list, K = 128 (ge-gb))
 //
-// Gradient (want_grad), same partition, no n x n collective:
+// Gradient (want_grad), same partition, no n x n collective, O(n^2 / P) memory:
 //   X = L^-1 by rows, right-looking: step k, owner(k) finishes its row
 //     X(k, 0:k) = Dinv_k R(k, 0:k)  (X(k,k) = Dinv_k kept from the sweep),
-//     RCCL broadcasts X(k, 0:k+1), every rank updates its rows i > k:
+//     broadcasts X(k, 0:k+1), every rank updates its rows i > k:
 //     R(i, 0:k+1) -= L(i,k) X(k, 0:k+1)                      (k_gemm)
-//   A^-1 = X^T X = sum_r X_r^T X_r over each rank's rows: rank r forms its partial
-//   P_r (lower tiles, K = its rows) and W_r = X_r^T R2_r; W is all-reduced (n x (q+1))
-//   the contraction <M, dA/dtheta> is linear in A^-1, so each rank contracts its own
-//   P_r (rank 0 also carries the -W W^T term) and only d+2 sums are all-reduced.
-// Loopback transport: all P ranks in this process on one GPU (separate local
-// buffers, one shared Dinv and panel column), copies instead of RCCL.
+//   A^-1 = X^T X = sum_r X_r^T X_r over each rank's rows.  The contraction
+//   <M, dA/dtheta> is linear in A^-1, so rank r contracts its own partial X_r^T X_r,
+//   formed slab by slab (a few tile rows of the lower triangle at a time, never the
+//   whole n x n), and rank 0 also carries the -W W^T term; W = [sqrt(c) alpha, W] is
+//   all-reduced (n x (q+1)) and then only the d+2 sums.
+//
+// Every logical rank owns all of its buffers (tile rows, Dinv, panel, all-gather
+// buffer, Gram, log-det, X rows, broadcast row, W, slab, sums).  The two transports
+// differ only in the collective call (coll_* below): RCCL on this process's one
+// rank, or loopback -- all P logical ranks in this process on one GPU, each
+// collective a set of device copies (and an add kernel for the all-reduce) between
+// the ranks' buffers.  The replicated inputs (points, [f H], r) and the abort flag
+// are shared by the loopback ranks.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -136,20 +143,6 @@ __global__ void __launch_bounds__(256) k_dist_unpermute(const double* recv, long
   }
 }
 
-// loopback: panel tiles of one logical rank straight into the panel column
-__global__ void __launch_bounds__(256) k_dist_to_panel(const double* Aloc, long long ld, int li0, int k,
-                                                       int P, int rank, double* panel, long long ldp) {
-  const int t = blockIdx.x;
-  const int gt = (li0 + t) * P + rank;
-  const double* src = Aloc + (long long)(li0 + t) * TILE + (long long)k * TILE * ld;
-  double* o = panel + (long long)gt * TILE;
-  for (int e = threadIdx.x; e < TILE * TILE / 2; e += 256) {
-    const int i = (e & 63) * 2, c = e >> 6;
-    *reinterpret_cast<double2*>(o + i + (long long)c * ldp) =
-        *reinterpret_cast<const double2*>(src + i + (long long)c * ld);
-  }
-}
-
 // Z = L^-1 [f H] (n_pad x Pc, column-major) out of the augmented tile row (local row li)
 __global__ void __launch_bounds__(256) k_dist_take_z(const double* Aloc, long long ld, int li, long long np,
                                                      int Pc, double* Z) {
@@ -169,13 +162,35 @@ __global__ void __launch_bounds__(256) k_dist_rows(const double* R2, long long l
   for (int p = 0; p < Pc; ++p) out[e + p * ldo] = R2[g + p * ldr];
 }
 
-struct Rank {              // one rank's stored tile rows
+// loopback all-reduce: dst += src
+__global__ void __launch_bounds__(256) k_dist_add(double* dst, const double* src, long long count) {
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < count; e += (long long)gridDim.x * 256)
+    dst[e] += src[e];
+}
+
+struct Rank {              // one rank's buffers (one per process over RCCL, P in loopback)
   int rank = 0, nloc = 0;
   long long ld = 0;
-  double* A = nullptr;     // nloc*128 x (NB+1)*128, column-major
-  double* logdet = nullptr;
   int nlx = 0;             // tile rows of the matrix proper (without the [f H] row)
-  double* X = nullptr;     // L^-1 rows, ld as A, NB*128 columns (gradient only)
+  // sweep
+  double* A = nullptr;     // nloc*128 x (NB+1)*128, column-major
+  double* logdet = nullptr;   // NB+1 (own steps; all-reduced)
+  double* dinv = nullptr;  // 128 x 128
+  double* panel = nullptr; // (NB+1)*128 x wmax*128: the current column group's gathered panels
+  double* recv = nullptr;  // all-gather buffer, P segments of the largest panel
+  double* gram = nullptr;  // Pc x Pc
+  // gradient
+  double* X = nullptr;     // L^-1 rows, ld as A, NB*128 columns
+  double* xrow = nullptr;  // 128 x n_pad: X(k, 0:k+1), broadcast per step
+  double* xgrp = nullptr;  // wmax*128 x n_pad (ld wmax*128): the current group's X rows, zero
+                           // right of each row's diagonal tile within the group
+  double* dZ = nullptr;    // n_pad x Pc: L^-1 [f H] (broadcast)
+  double* dR2 = nullptr;   // n_pad x Pc
+  double* r2loc = nullptr; // local rows of R2, 128 columns (zero beyond Pc)
+  double* wpart = nullptr; // n_pad x 128: [sqrt(c) alpha, W] (all-reduced)
+  double* slab = nullptr;  // slab*128 x n_pad: tile rows of this rank's partial X_r^T X_r
+  double* csum = nullptr;  // d+2 contraction sums (all-reduced)
+  size_t bytes = 0;        // device bytes held for this rank
 };
 
 struct DLaunch {           // one grouped k_gemm launch
@@ -184,7 +199,13 @@ struct DLaunch {           // one grouped k_gemm launch
   int kind = 0;            // 0 <false,false>, 1 <false,true>, 2 <true,true>
 };
 
+struct SlabLaunch {        // one slab of a rank's partial of A^-1: GEMM + contraction
+  DLaunch gemm;
+  int a0 = 0, a1 = 0;      // tile rows [a0, a1)
+};
+
 constexpr int DIST_DESC_MAX = 1 << 20;
+constexpr size_t SLAB_DOUBLES = (size_t)1 << 27;   // 1 GiB per rank for the A^-1 slab
 
 int nloc_of(int NB, int P, int r) { return r <= NB ? (NB - r) / P + 1 : 0; }
 // first local row of rank r whose global tile row exceeds k
@@ -202,51 +223,43 @@ struct gpe_dist {
   long long n = 0, n_pad = 0;
   int d = 0, q = 0, NB = 0;
   bool has_r = false;
+  // replicated inputs (one copy shared by the loopback ranks)
   double* dX = nullptr;    // n_pad x d raw
   double* dXw = nullptr;   // scaled
   double* dF = nullptr;    // n_pad x (q+1)
   double* dr = nullptr;
   double* dinvdelta = nullptr;
+  int* dinfo = nullptr;    // abort flag / failed pivot (all-reduced with max over RCCL)
+  double* cpart = nullptr; // contraction partials (scratch, stream-ordered)
   std::vector<Rank> ranks;   // local ranks (all P in loopback, one otherwise)
 
-  double* dinv = nullptr;    // 128 x 128
-  double* panel = nullptr;   // (NB+1)*128 x wmax*128: the current column group's gathered panels
   // column groups (as the single-GPU fused Cholesky): {width, min remaining tile
   // columns}, first match wins, else 1 (GPEMU_DIST_W="8:160,4:80,2:40" style)
   std::vector<std::pair<int, int>> groups = {{8, 160}, {4, 80}, {2, 40}};
   std::vector<int> gstart;   // per step: first column of its group
   int wmax = 1;
-  double* recv = nullptr;    // RCCL all-gather buffer
-  double* gram = nullptr;    // Pc x Pc
-  int* dinfo = nullptr;
   int* dli0 = nullptr;       // [NB][P] first local row with global row > k
   int* dcnt = nullptr;       // [NB][P] panel tiles of rank r at step k
   GemmProb* dprobs = nullptr;
   unsigned* dtiles = nullptr;
   std::vector<DLaunch> diag, panel_l, upd;   // per step
   std::vector<int> maxT;                       // per step: max panel tiles over ranks
+  int T0 = 0;                                  // the most panel tiles any rank contributes
   double* hpin = nullptr;
   size_t hpin_cap = 0;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   std::vector<hipEvent_t> cev;
+  int ev = 0;                                  // event pairs used by this objective call
   double total_ms = 0.0, comm_ms = 0.0;
+  size_t shared_bytes = 0;
 
   // gradient (allocated on the first want_grad call after gpe_dist_set_data)
   bool grad_ready = false, grad_now = false;
-  double* xrow = nullptr;    // 128 x n_pad: X(k, 0:k+1), broadcast per step
-  double* xgrp = nullptr;    // wmax*128 x n_pad (ld wmax*128): the current group's X rows, zero
-                             // right of each row's diagonal tile within the group
-  double* dZ = nullptr;      // n_pad x Pc: L^-1 [f H]
-  double* dR2 = nullptr;     // n_pad x Pc
-  double* r2loc = nullptr;   // local rows of R2, 128 columns (zero beyond Pc)
-  double* wpart = nullptr;   // n_pad x 128: [sqrt(c) alpha, W] (sum over ranks)
-  double* pbuf = nullptr;    // n_pad x n_pad: this rank's partial of A^-1 (lower tiles)
+  int slab_rows = 1;                           // tile rows per slab of A^-1
   double* dT2 = nullptr;
-  double* cpart = nullptr;   // contraction partials
-  double* csum = nullptr;    // d+2 per local rank
   GemmProb* gprobs = nullptr;
-  std::vector<DLaunch> tri_p, tri_x, tri_u, wa_l, lau_l;
-  double grad_ms = 0.0;
+  std::vector<DLaunch> tri_p, tri_x, tri_u, wa_l;
+  std::vector<std::vector<SlabLaunch>> slabs;  // per local rank
 };
 
 namespace {
@@ -281,17 +294,28 @@ int dfail(gpe_dist* h, int code, const std::string& m) {
 }
 
 template <typename T>
-int dalloc(gpe_dist* h, T** p, size_t count) {
-  if (*p) {
-    (void)hipFree(*p);
-    *p = nullptr;
-  }
+void dfree(T** p) {
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+}
+
+template <typename T>
+int dalloc(gpe_dist* h, T** p, size_t count, size_t* acct = nullptr) {
+  dfree(p);
   if (count == 0) return GPE_OK;
   if (hipMalloc((void**)p, count * sizeof(T)) != hipSuccess) {
     *p = nullptr;
     return dfail(h, GPE_ERR_ALLOC, "hipMalloc failed (" + std::to_string(count * sizeof(T)) + " bytes)");
   }
+  if (acct) *acct += count * sizeof(T);
   return GPE_OK;
+}
+
+void free_rank(Rank& R) {
+  double** bufs[] = {&R.A, &R.logdet, &R.dinv, &R.panel, &R.recv, &R.gram, &R.X, &R.xrow, &R.xgrp,
+                     &R.dZ, &R.dR2, &R.r2loc, &R.wpart, &R.slab, &R.csum};
+  for (double** b : bufs) dfree(b);
+  R.bytes = 0;
 }
 
 int pinned(gpe_dist* h, size_t doubles) {
@@ -313,6 +337,102 @@ GemmProb dprob(const double* A, long long lda, const double* B, long long ldb, d
   p.mt = mt; p.nt = nt; p.K = K; p.flags = flags;
   p.alpha = alpha; p.beta = beta;
   return p;
+}
+
+Rank* rank_slot(gpe_dist* h, int r) {   // the local slot of rank r, or null (another process)
+  for (Rank& R : h->ranks)
+    if (R.rank == r) return &R;
+  return nullptr;
+}
+
+// ---------------------------------------------------------------------------
+// Collectives.  Arguments name a buffer member of Rank plus an element offset;
+// over RCCL they act on this process's one rank, in loopback on the P logical
+// ranks' buffers.  Each is bracketed by an event pair (comm time).
+// ---------------------------------------------------------------------------
+int ensure_events(gpe_dist* h, size_t n) {
+  while (h->cev.size() < n) {
+    hipEvent_t e;
+    DCHK_HIP(h, hipEventCreate(&e));
+    h->cev.push_back(e);
+  }
+  return GPE_OK;
+}
+
+int comm_begin(gpe_dist* h) {
+  DCHK(ensure_events(h, (size_t)h->ev + 2));
+  DCHK_HIP(h, hipEventRecord(h->cev[h->ev], h->stream));
+  return GPE_OK;
+}
+
+int comm_end(gpe_dist* h) {
+  DCHK_HIP(h, hipEventRecord(h->cev[h->ev + 1], h->stream));
+  h->ev += 2;
+  return GPE_OK;
+}
+
+// broadcast count doubles at (Rank::*buf + off) from rank root
+int coll_bcast(gpe_dist* h, double* Rank::*buf, long long off, size_t count, int root) {
+  DCHK(comm_begin(h));
+  if (!h->loop) {
+    double* p = h->ranks[0].*buf + off;
+    DCHK_NCCL(h, ncclBroadcast(p, p, count, ncclDouble, root, h->comm, h->stream));
+  } else {
+    const double* src = rank_slot(h, root)->*buf + off;
+    for (Rank& R : h->ranks) {
+      if (R.rank == root) continue;
+      DCHK_HIP(h, hipMemcpyAsync(R.*buf + off, src, count * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    }
+  }
+  return comm_end(h);
+}
+
+// in-place all-gather: rank r's segment of seg doubles at offset r*seg
+int coll_allgather(gpe_dist* h, double* Rank::*buf, size_t seg) {
+  DCHK(comm_begin(h));
+  if (!h->loop) {
+    double* p = h->ranks[0].*buf;
+    DCHK_NCCL(h, ncclAllGather(p + (size_t)h->rank * seg, p, seg, ncclDouble, h->comm, h->stream));
+  } else {
+    for (Rank& D : h->ranks)
+      for (const Rank& S : h->ranks) {
+        if (S.rank == D.rank) continue;
+        const size_t o = (size_t)S.rank * seg;
+        DCHK_HIP(h, hipMemcpyAsync(D.*buf + o, S.*buf + o, seg * sizeof(double), hipMemcpyDeviceToDevice,
+                                   h->stream));
+      }
+  }
+  return comm_end(h);
+}
+
+// all-reduce (sum) of count doubles at (Rank::*buf + off)
+int coll_allreduce_sum(gpe_dist* h, double* Rank::*buf, long long off, size_t count) {
+  DCHK(comm_begin(h));
+  if (!h->loop) {
+    double* p = h->ranks[0].*buf + off;
+    DCHK_NCCL(h, ncclAllReduce(p, p, count, ncclDouble, ncclSum, h->comm, h->stream));
+  } else if (h->ranks.size() > 1) {
+    double* acc = h->ranks[0].*buf + off;
+    const unsigned g = (unsigned)std::min<size_t>((count + 255) / 256, 2048);
+    for (size_t s = 1; s < h->ranks.size(); ++s) {
+      hipLaunchKernelGGL(k_dist_add, dim3(g), dim3(256), 0, h->stream, acc, h->ranks[s].*buf + off,
+                         (long long)count);
+      DCHK_HIP(h, hipGetLastError());
+    }
+    for (size_t s = 1; s < h->ranks.size(); ++s)
+      DCHK_HIP(h, hipMemcpyAsync(h->ranks[s].*buf + off, acc, count * sizeof(double), hipMemcpyDeviceToDevice,
+                                 h->stream));
+  }
+  return comm_end(h);
+}
+
+// all-reduce (max) of the abort flag: over RCCL each process has its own; the
+// loopback ranks share one (their launches are batched), so it is already reduced
+int coll_info_max(gpe_dist* h) {
+  if (h->loop) return GPE_OK;
+  DCHK(comm_begin(h));
+  DCHK_NCCL(h, ncclAllReduce(h->dinfo, h->dinfo, 1, ncclInt32, ncclMax, h->comm, h->stream));
+  return comm_end(h);
 }
 
 // Column groups [gb, ge): step k = gb + w applies the pending update by the group's
@@ -360,19 +480,17 @@ int build_schedule(gpe_dist* h) {
       h->maxT[k] = std::max(h->maxT[k], cnt[(size_t)k * P + r]);
     }
     // diagonal tile: owner's local row k / P, column k, less the pending update
-    // L(k, gb:k) L(k, gb:k)^T from its own row; then factored and inverted
+    // L(k, gb:k) L(k, gb:k)^T from its own row; then factored and inverted into its Dinv
     DLaunch dl;
     dl.first = (int)probs.size();
-    const int owner = k % P;
-    for (Rank& R : h->ranks) {
-      if (R.rank != owner) continue;
-      double* Ckk = R.A + (long long)(k / P) * TILE + (long long)k * TILE * R.ld;
-      const double* Lk = R.A + (long long)(k / P) * TILE + (long long)gb * TILE * R.ld;
-      GemmProb p = dprob(Kp ? Lk : nullptr, R.ld, Kp ? Lk : nullptr, R.ld, Ckk, R.ld, 1, 1, Kp, G_DIAG,
+    if (Rank* R = rank_slot(h, k % P)) {
+      double* Ckk = R->A + (long long)(k / P) * TILE + (long long)k * TILE * R->ld;
+      const double* Lk = R->A + (long long)(k / P) * TILE + (long long)gb * TILE * R->ld;
+      GemmProb p = dprob(Kp ? Lk : nullptr, R->ld, Kp ? Lk : nullptr, R->ld, Ckk, R->ld, 1, 1, Kp, G_DIAG,
                          Kp ? -1.0 : 1.0, 1.0);
-      p.X = h->dinv;
+      p.X = R->dinv;
       p.ldx = TILE;
-      p.logdet = R.logdet + k;
+      p.logdet = R->logdet + k;
       p.diag_col0 = k * TILE;
       p.tile_begin = dl.tiles;
       p.ntiles = 1;
@@ -381,13 +499,13 @@ int build_schedule(gpe_dist* h) {
       ++dl.count;
     }
     // pending update of the panel tiles: A(i,k) -= L(i, gb:k) L(k, gb:k)^T over each
-    // local rank's rows i > k; L(k, gb:k) is row k of the group's gathered panels
+    // local rank's rows i > k; L(k, gb:k) is row k of the rank's gathered panels
     if (Kp > 0) {
       for (Rank& R : h->ranks) {
         const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
         if (c == 0) continue;
         GemmProb p = dprob(R.A + (long long)a * TILE + (long long)gb * TILE * R.ld, R.ld,
-                           h->panel + (long long)k * TILE, ldp,
+                           R.panel + (long long)k * TILE, ldp,
                            R.A + (long long)a * TILE + (long long)k * TILE * R.ld, R.ld, c, 1, Kp, 0, -1.0, 1.0);
         p.tile_begin = dl.tiles;
         p.ntiles = c;
@@ -404,7 +522,7 @@ int build_schedule(gpe_dist* h) {
       const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
       if (c == 0) continue;
       double* Aik = R.A + (long long)a * TILE + (long long)k * TILE * R.ld;
-      GemmProb p = dprob(Aik, R.ld, h->dinv, TILE, Aik, R.ld, c, 1, TILE, 0, 1.0, 0.0);
+      GemmProb p = dprob(Aik, R.ld, R.dinv, TILE, Aik, R.ld, c, 1, TILE, 0, 1.0, 0.0);
       p.tile_begin = pl.tiles;
       p.ntiles = c;
       pl.tiles += c;
@@ -422,7 +540,7 @@ int build_schedule(gpe_dist* h) {
     for (Rank& R : h->ranks) {
       const int a = li0_of(k, P, R.rank);
       if (a >= R.nloc) continue;
-      GemmProb p = dprob(R.A + (long long)gb * TILE * R.ld, R.ld, h->panel, ldp, R.A, R.ld,
+      GemmProb p = dprob(R.A + (long long)gb * TILE * R.ld, R.ld, R.panel, ldp, R.A, R.ld,
                          R.nloc, NB + 1, (ge - gb) * TILE, 0, -1.0, 1.0);
       for (int li = a; li < R.nloc; ++li) {
         const int gt = li * P + R.rank;
@@ -467,28 +585,29 @@ int launch(gpe_dist* h, const DLaunch& L, const GemmProb* base = nullptr) {
 // first local tile row of rank r whose global row is >= a
 int lstart_of(int a, int P, int r) { return a <= r ? 0 : (a - r + P - 1) / P; }
 
-// gradient buffers and GEMM descriptors (TRTRI steps, W partial, A^-1 partial)
+// gradient buffers and GEMM descriptors (TRTRI steps, W partial, A^-1 slabs)
 int ensure_grad(gpe_dist* h) {
   if (h->grad_ready) return GPE_OK;
   const int NB = h->NB, P = h->P, Pc = h->q + 1, d = h->d;
   const long long np = h->n_pad;
-  long long maxld = TILE;
+  // slab of the A^-1 partial: as many tile rows as fit SLAB_DOUBLES
+  h->slab_rows = (int)std::max<long long>(1, std::min<long long>(NB, (long long)SLAB_DOUBLES / (TILE * np)));
+  const long long lds = (long long)h->slab_rows * TILE;
   for (Rank& R : h->ranks) {
     R.nlx = R.rank <= NB - 1 ? (NB - 1 - R.rank) / P + 1 : 0;
-    DCHK(dalloc(h, &R.X, (size_t)R.ld * NB * TILE));
-    maxld = std::max(maxld, R.ld);
+    DCHK(dalloc(h, &R.X, (size_t)R.ld * NB * TILE, &R.bytes));
+    DCHK(dalloc(h, &R.xrow, (size_t)TILE * np, &R.bytes));
+    DCHK(dalloc(h, &R.xgrp, (size_t)h->wmax * TILE * np, &R.bytes));
+    DCHK(dalloc(h, &R.dZ, (size_t)np * Pc, &R.bytes));
+    DCHK(dalloc(h, &R.dR2, (size_t)np * Pc, &R.bytes));
+    DCHK(dalloc(h, &R.r2loc, (size_t)R.ld * TILE, &R.bytes));
+    DCHK_HIP(h, hipMemset(R.r2loc, 0, (size_t)R.ld * TILE * sizeof(double)));
+    DCHK(dalloc(h, &R.wpart, (size_t)np * TILE, &R.bytes));
+    DCHK(dalloc(h, &R.slab, (size_t)lds * np, &R.bytes));
+    DCHK(dalloc(h, &R.csum, (size_t)d + 2, &R.bytes));
   }
-  DCHK(dalloc(h, &h->xrow, (size_t)TILE * np));
-  DCHK(dalloc(h, &h->xgrp, (size_t)h->wmax * TILE * np));
-  DCHK(dalloc(h, &h->dZ, (size_t)np * Pc));
-  DCHK(dalloc(h, &h->dR2, (size_t)np * Pc));
-  DCHK(dalloc(h, &h->r2loc, (size_t)maxld * TILE));
-  DCHK_HIP(h, hipMemset(h->r2loc, 0, (size_t)maxld * TILE * sizeof(double)));
-  DCHK(dalloc(h, &h->wpart, (size_t)np * TILE));
-  DCHK(dalloc(h, &h->pbuf, (size_t)np * np));
-  DCHK(dalloc(h, &h->dT2, (size_t)Pc * Pc));
-  DCHK(dalloc(h, &h->cpart, (size_t)NB * (NB + 1) / 2 * (d + 2)));
-  DCHK(dalloc(h, &h->csum, h->ranks.size() * (size_t)(d + 2)));
+  DCHK(dalloc(h, &h->dT2, (size_t)Pc * Pc, &h->shared_bytes));
+  DCHK(dalloc(h, &h->cpart, (size_t)NB * (NB + 1) / 2 * (d + 2), &h->shared_bytes));
 
   // Rows of X = L^-1 in the Cholesky's column groups [gb, ge): the owner of row k first
   // applies the pending rows gb..k-1 of its group, R(k, 0:k) -= L(k, gb:k) X(gb:k, 0:k)
@@ -501,14 +620,14 @@ int ensure_grad(gpe_dist* h) {
   h->tri_x.assign(NB, DLaunch());
   h->tri_u.assign(NB, DLaunch());
   for (int k = 0; k < NB; ++k) {
-    const int owner = k % P, lk = k / P;
+    const int lk = k / P;
     const int gb = h->gstart[k], ge = group_end(h, k), w = k - gb;
-    for (Rank& R : h->ranks) {
-      if (R.rank != owner || k == 0) continue;
-      double* row = R.X + (long long)lk * TILE;
+    Rank* O = rank_slot(h, k % P);
+    if (O && k > 0) {
+      double* row = O->X + (long long)lk * TILE;
       if (w > 0) {
-        GemmProb p = dprob(R.A + (long long)lk * TILE + (long long)gb * TILE * R.ld, R.ld, h->xgrp, ldx,
-                           row, R.ld, 1, k, w * TILE, 0, -1.0, 1.0);
+        GemmProb p = dprob(O->A + (long long)lk * TILE + (long long)gb * TILE * O->ld, O->ld, O->xgrp, ldx,
+                           row, O->ld, 1, k, w * TILE, 0, -1.0, 1.0);
         p.ntiles = k;
         DLaunch L;
         L.first = (int)probs.size(); L.count = 1; L.tiles = k; L.kind = 1;
@@ -517,7 +636,7 @@ int ensure_grad(gpe_dist* h) {
       }
       // X(k, 0:k) = Dinv_k R(k, 0:k) with R(k, c) = -sum_{j<k} L(k,j) X(j,c), in place
       // (each output tile reads only itself)
-      GemmProb p = dprob(row + (long long)k * TILE * R.ld, R.ld, row, R.ld, row, R.ld, 1, k, TILE, 0, 1.0, 0.0);
+      GemmProb p = dprob(row + (long long)k * TILE * O->ld, O->ld, row, O->ld, row, O->ld, 1, k, TILE, 0, 1.0, 0.0);
       p.ntiles = k;
       DLaunch L;
       L.first = (int)probs.size(); L.count = 1; L.tiles = k; L.kind = 1;
@@ -531,7 +650,7 @@ int ensure_grad(gpe_dist* h) {
     for (Rank& R : h->ranks) {
       const int a = lstart_of(ge, P, R.rank), c = R.nlx - a;
       if (c <= 0) continue;
-      GemmProb p = dprob(R.A + (long long)a * TILE + (long long)gb * TILE * R.ld, R.ld, h->xgrp, ldx,
+      GemmProb p = dprob(R.A + (long long)a * TILE + (long long)gb * TILE * R.ld, R.ld, R.xgrp, ldx,
                          R.X + (long long)a * TILE, R.ld, c, ge, (ge - gb) * TILE, 0, -1.0, 1.0);
       p.tile_begin = ul.tiles;
       p.ntiles = c * ge;
@@ -542,18 +661,18 @@ int ensure_grad(gpe_dist* h) {
     h->tri_u[k] = ul;
   }
   h->wa_l.assign(h->ranks.size(), DLaunch());
-  h->lau_l.assign(h->ranks.size(), DLaunch());
+  h->slabs.assign(h->ranks.size(), std::vector<SlabLaunch>());
   for (size_t s = 0; s < h->ranks.size(); ++s) {
     Rank& R = h->ranks[s];
-    DLaunch wl, ll;
-    wl.kind = ll.kind = 2;
+    DLaunch wl;
+    wl.kind = 2;
     wl.first = (int)probs.size();
     for (int a = 0; a < NB; ++a) {
       const int ls = lstart_of(a, P, R.rank), K = (R.nlx - ls) * TILE;
       if (K <= 0) continue;
       // W(a) += X_r(:, a)^T R2_r over its rows >= a
       GemmProb p = dprob(R.X + (long long)ls * TILE + (long long)a * TILE * R.ld, R.ld,
-                         h->r2loc + (long long)ls * TILE, R.ld, h->wpart + (long long)a * TILE, np,
+                         R.r2loc + (long long)ls * TILE, R.ld, R.wpart + (long long)a * TILE, np,
                          1, 1, K, 0, 1.0, 1.0);
       p.tile_begin = wl.tiles;
       p.ntiles = 1;
@@ -561,57 +680,59 @@ int ensure_grad(gpe_dist* h) {
       ++wl.count;
       probs.push_back(p);
     }
-    ll.first = (int)probs.size();
-    for (int a = 0; a < NB; ++a) {
-      const int ls = lstart_of(a, P, R.rank), K = std::max(0, (R.nlx - ls) * TILE);
-      // P_r(a, 0:a+1) = X_r(:, a)^T X_r(:, 0:a+1) over its rows >= a (K = 0 writes zeros)
-      GemmProb p = dprob(R.X + (long long)ls * TILE + (long long)a * TILE * R.ld, R.ld,
-                         R.X + (long long)ls * TILE, R.ld, h->pbuf + (long long)a * TILE, np,
-                         1, a + 1, K, 0, 1.0, 0.0);
-      p.tile_begin = ll.tiles;
-      p.ntiles = a + 1;
-      ll.tiles += a + 1;
-      ++ll.count;
-      probs.push_back(p);
-    }
     h->wa_l[s] = wl;
-    h->lau_l[s] = ll;
+    // partial of A^-1 by slabs of tile rows [a0, a1): P_r(a, 0:a+1) = X_r(:, a)^T X_r(:, 0:a+1)
+    // over its rows >= a (K = 0 writes zeros), into slab row a - a0
+    for (int a0 = 0; a0 < NB; a0 += h->slab_rows) {
+      SlabLaunch sl;
+      sl.a0 = a0;
+      sl.a1 = std::min(NB, a0 + h->slab_rows);
+      sl.gemm.kind = 2;
+      sl.gemm.first = (int)probs.size();
+      for (int a = sl.a0; a < sl.a1; ++a) {
+        const int ls = lstart_of(a, P, R.rank), K = std::max(0, (R.nlx - ls) * TILE);
+        GemmProb p = dprob(R.X + (long long)ls * TILE + (long long)a * TILE * R.ld, R.ld,
+                           R.X + (long long)ls * TILE, R.ld, R.slab + (long long)(a - a0) * TILE, lds,
+                           1, a + 1, K, 0, 1.0, 0.0);
+        p.tile_begin = sl.gemm.tiles;
+        p.ntiles = a + 1;
+        sl.gemm.tiles += a + 1;
+        ++sl.gemm.count;
+        probs.push_back(p);
+      }
+      h->slabs[s].push_back(sl);
+    }
   }
   if ((int)probs.size() > DIST_DESC_MAX) return dfail(h, GPE_ERR_UNSUPPORTED, "distributed gradient schedule too large");
-  DCHK(dalloc(h, &h->gprobs, probs.size()));
+  DCHK(dalloc(h, &h->gprobs, probs.size(), &h->shared_bytes));
   DCHK_HIP(h, hipMemcpy(h->gprobs, probs.data(), probs.size() * sizeof(GemmProb), hipMemcpyHostToDevice));
   h->grad_ready = true;
   return GPE_OK;
 }
 
 // TRTRI step k: owner applies its group's pending rows and finishes X(k, :), broadcast
-// into the group's rows; the step closing a group updates every rank's rows below it
-int trtri_step(gpe_dist* h, int k, int& ev) {
+// into every rank's group rows; the step closing a group updates every rank's rows below it
+int trtri_step(gpe_dist* h, int k) {
   const int P = h->P, owner = k % P, lk = k / P;
   const int gb = h->gstart[k], ge = group_end(h, k), w = k - gb;
   DCHK(launch(h, h->tri_p[k], h->gprobs));
   DCHK(launch(h, h->tri_x[k], h->gprobs));
   if (k == h->NB - 1) return GPE_OK;   // no rows below
-  for (Rank& R : h->ranks) {
-    if (R.rank != owner) continue;
-    DCHK_HIP(h, hipMemcpy2DAsync(h->xrow, TILE * sizeof(double), R.X + (long long)lk * TILE, R.ld * sizeof(double),
+  if (Rank* O = rank_slot(h, owner))
+    DCHK_HIP(h, hipMemcpy2DAsync(O->xrow, TILE * sizeof(double), O->X + (long long)lk * TILE, O->ld * sizeof(double),
                                  TILE * sizeof(double), (size_t)(k + 1) * TILE, hipMemcpyDeviceToDevice, h->stream));
-  }
-  if (!h->loop) {
-    DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
-    DCHK_NCCL(h, ncclBroadcast(h->xrow, h->xrow, (size_t)(k + 1) * TILE * TILE, ncclDouble, owner, h->comm,
-                               h->stream));
-    DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
-  }
+  DCHK(coll_bcast(h, &Rank::xrow, 0, (size_t)(k + 1) * TILE * TILE, owner));
   // X(k, 0:k+1) -> the group's row block w; zero its columns k+1 .. ge-1, which the
   // group's later rows and the closing update read as X(k, c) = 0
   const long long ldx = (long long)h->wmax * TILE;
-  double* blk = h->xgrp + (long long)w * TILE;
-  DCHK_HIP(h, hipMemcpy2DAsync(blk, ldx * sizeof(double), h->xrow, TILE * sizeof(double), TILE * sizeof(double),
-                               (size_t)(k + 1) * TILE, hipMemcpyDeviceToDevice, h->stream));
-  if (ge > k + 1)
-    DCHK_HIP(h, hipMemset2DAsync(blk + (long long)(k + 1) * TILE * ldx, ldx * sizeof(double), 0,
-                                 TILE * sizeof(double), (size_t)(ge - k - 1) * TILE, h->stream));
+  for (Rank& R : h->ranks) {
+    double* blk = R.xgrp + (long long)w * TILE;
+    DCHK_HIP(h, hipMemcpy2DAsync(blk, ldx * sizeof(double), R.xrow, TILE * sizeof(double), TILE * sizeof(double),
+                                 (size_t)(k + 1) * TILE, hipMemcpyDeviceToDevice, h->stream));
+    if (ge > k + 1)
+      DCHK_HIP(h, hipMemset2DAsync(blk + (long long)(k + 1) * TILE * ldx, ldx * sizeof(double), 0,
+                                   TILE * sizeof(double), (size_t)(ge - k - 1) * TILE, h->stream));
+  }
   DCHK(launch(h, h->tri_u[k], h->gprobs));
   return GPE_OK;
 }
@@ -644,53 +765,34 @@ int kbuild(gpe_dist* h, int kernel, double nu, double s2, double rscale) {
   return GPE_OK;
 }
 
-// one column step: diag, Dinv broadcast, panel, panel all-gather, trailing update
-int step(gpe_dist* h, int k, int& ev) {
+// one column step: diag, Dinv broadcast, panel, pack + all-gather + unpermute, trailing update
+int step(gpe_dist* h, int k) {
   const int P = h->P, owner = k % P;
   DCHK(launch(h, h->diag[k]));
-  if (!h->loop) {
-    DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
-    DCHK_NCCL(h, ncclBroadcast(h->dinv, h->dinv, (size_t)TILE * TILE, ncclDouble, owner, h->comm, h->stream));
-    DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
-  }
+  DCHK(coll_bcast(h, &Rank::dinv, 0, (size_t)TILE * TILE, owner));
   if (h->grad_now) {
-    for (Rank& R : h->ranks) {
-      if (R.rank != owner) continue;
-      DCHK_HIP(h, hipMemcpy2DAsync(R.X + (long long)(k / P) * TILE + (long long)k * TILE * R.ld,
-                                   R.ld * sizeof(double), h->dinv, TILE * sizeof(double), TILE * sizeof(double),
+    if (Rank* O = rank_slot(h, owner))
+      DCHK_HIP(h, hipMemcpy2DAsync(O->X + (long long)(k / P) * TILE + (long long)k * TILE * O->ld,
+                                   O->ld * sizeof(double), O->dinv, TILE * sizeof(double), TILE * sizeof(double),
                                    TILE, hipMemcpyDeviceToDevice, h->stream));
-    }
   }
   DCHK(launch(h, h->panel_l[k]));
   const long long ldp = (long long)(h->NB + 1) * TILE;
-  double* pcol = h->panel + (long long)(k - h->gstart[k]) * TILE * ldp;   // the group's panel block
-  if (h->loop) {
-    if (h->cev.size() > (size_t)ev + 1) DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
+  const long long pcol = (long long)(k - h->gstart[k]) * TILE * ldp;   // the group's panel block
+  const int T = h->maxT[k];
+  if (T > 0) {
+    const size_t seg = (size_t)T * TILE * TILE;
     for (Rank& R : h->ranks) {
       const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
       if (c == 0) continue;
-      hipLaunchKernelGGL(k_dist_to_panel, dim3(c), dim3(256), 0, h->stream, R.A, R.ld, a, k, P, R.rank,
-                         pcol, ldp);
+      hipLaunchKernelGGL(k_dist_pack, dim3(c), dim3(256), 0, h->stream, R.A, R.ld, a, k,
+                         R.recv + (size_t)R.rank * seg);
       DCHK_HIP(h, hipGetLastError());
     }
-    if (h->cev.size() > (size_t)ev) DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
-  } else {
-    const Rank& R = h->ranks[0];
-    const int T = h->maxT[k];
-    const long long seg = (long long)T * TILE * TILE;
-    if (T > 0) {
-      const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
-      if (c > 0) {
-        hipLaunchKernelGGL(k_dist_pack, dim3(c), dim3(256), 0, h->stream, R.A, R.ld, a, k,
-                           h->recv + (long long)h->rank * seg);
-        DCHK_HIP(h, hipGetLastError());
-      }
-      DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
-      DCHK_NCCL(h, ncclAllGather(h->recv + (long long)h->rank * seg, h->recv, (size_t)seg, ncclDouble, h->comm,
-                                 h->stream));
-      DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
-      hipLaunchKernelGGL(k_dist_unpermute, dim3(T, P), dim3(256), 0, h->stream, h->recv, seg,
-                         h->dli0 + (size_t)k * P, h->dcnt + (size_t)k * P, P, pcol, ldp);
+    DCHK(coll_allgather(h, &Rank::recv, seg));
+    for (Rank& R : h->ranks) {
+      hipLaunchKernelGGL(k_dist_unpermute, dim3(T, P), dim3(256), 0, h->stream, R.recv, (long long)seg,
+                         h->dli0 + (size_t)k * P, h->dcnt + (size_t)k * P, P, R.panel + pcol, ldp);
       DCHK_HIP(h, hipGetLastError());
     }
   }
@@ -698,13 +800,22 @@ int step(gpe_dist* h, int k, int& ev) {
   return GPE_OK;
 }
 
-int ensure_events(gpe_dist* h, size_t n) {
-  while (h->cev.size() < n) {
-    hipEvent_t e;
-    DCHK_HIP(h, hipEventCreate(&e));
-    h->cev.push_back(e);
-  }
-  return GPE_OK;
+void contract_launch(gpe_dist* h, const double* slab, long long lds, long long row0, int blk0, int nblk,
+                     const double* wpart, int q1) {
+  const int d = h->d, Pc = h->q + 1, bucket = std::max(d, Pc);
+  const long long np = h->n_pad;
+  const dim3 g(nblk);
+  const int nv = (int)h->n;
+  if (d == 10 && Pc <= 13)
+    hipLaunchKernelGGL((k_contract<10, 13>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0);
+  else if (d == 20 && Pc <= 21)   // BASELINE configs[3]
+    hipLaunchKernelGGL((k_contract<20, 21>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0);
+  else if (bucket <= 8)
+    hipLaunchKernelGGL((k_contract<8, 9>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0);
+  else if (bucket <= 16)
+    hipLaunchKernelGGL((k_contract<16, 17>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0);
+  else
+    hipLaunchKernelGGL((k_contract<32, 33>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0);
 }
 
 }  // namespace
@@ -755,8 +866,7 @@ gpe_dist* gpe_dist_create(int32_t device, int32_t nranks, int32_t rank, const ui
   }
   bool ok = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess &&
             hipEventCreate(&h->e0) == hipSuccess && hipEventCreate(&h->e1) == hipSuccess &&
-            hipMalloc((void**)&h->dinfo, sizeof(int)) == hipSuccess &&
-            hipMalloc((void**)&h->dinv, (size_t)TILE * TILE * sizeof(double)) == hipSuccess;
+            hipMalloc((void**)&h->dinfo, sizeof(int)) == hipSuccess;
   if (ok && !h->loop) {
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof(id));
@@ -774,22 +884,15 @@ void gpe_dist_destroy(gpe_dist* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->comm) (void)ncclCommDestroy(h->comm);
-  for (Rank& R : h->ranks) {
-    if (R.A) (void)hipFree(R.A);
-    if (R.logdet) (void)hipFree(R.logdet);
-    if (R.X) (void)hipFree(R.X);
-  }
-  double* bufs[] = {h->dX,    h->dXw,   h->dF,   h->dr,    h->dinvdelta, h->dinv, h->panel,
-                    h->recv,  h->gram,  h->xrow, h->xgrp, h->dZ,    h->dR2,       h->r2loc, h->wpart,
-                    h->pbuf,  h->dT2,   h->cpart, h->csum};
-  for (double* b : bufs)
-    if (b) (void)hipFree(b);
-  if (h->dinfo) (void)hipFree(h->dinfo);
-  if (h->dli0) (void)hipFree(h->dli0);
-  if (h->dcnt) (void)hipFree(h->dcnt);
-  if (h->dprobs) (void)hipFree(h->dprobs);
-  if (h->dtiles) (void)hipFree(h->dtiles);
-  if (h->gprobs) (void)hipFree(h->gprobs);
+  for (Rank& R : h->ranks) free_rank(R);
+  double** bufs[] = {&h->dX, &h->dXw, &h->dF, &h->dr, &h->dinvdelta, &h->cpart, &h->dT2};
+  for (double** b : bufs) dfree(b);
+  dfree(&h->dinfo);
+  dfree(&h->dli0);
+  dfree(&h->dcnt);
+  dfree(&h->dprobs);
+  dfree(&h->dtiles);
+  dfree(&h->gprobs);
   if (h->hpin) (void)hipHostFree(h->hpin);
   for (hipEvent_t e : h->cev) (void)hipEventDestroy(e);
   if (h->e0) (void)hipEventDestroy(h->e0);
@@ -806,6 +909,7 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
   if (n <= 0 || d <= 0 || d > 32 || q < 0 || q + 1 > 128 || !X || !f || (q > 0 && !H))
     return dfail(h, GPE_ERR_ARG, "bad shapes");
   DCHK_HIP(h, hipSetDevice(h->device));
+  DCHK_HIP(h, hipStreamSynchronize(h->stream));
   h->n = n;
   h->d = d;
   h->q = q;
@@ -814,15 +918,22 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
   if (h->NB + 1 > 4095) return dfail(h, GPE_ERR_UNSUPPORTED, "n too large for the tile list");
   const long long np = h->n_pad;
   const int Pc = q + 1;
+  for (Rank& R : h->ranks) free_rank(R);
+  h->ranks.clear();
+  h->grad_ready = false;
+  h->shared_bytes = 0;
+  dfree(&h->cpart);
+  dfree(&h->dT2);
+  dfree(&h->gprobs);
   DCHK(pinned(h, (size_t)np * std::max(d, Pc) + 16));
   // X (row-major, zero padded)
-  DCHK(dalloc(h, &h->dX, (size_t)np * d));
-  DCHK(dalloc(h, &h->dXw, (size_t)np * d));
+  DCHK(dalloc(h, &h->dX, (size_t)np * d, &h->shared_bytes));
+  DCHK(dalloc(h, &h->dXw, (size_t)np * d, &h->shared_bytes));
   std::memset(h->hpin, 0, (size_t)np * d * sizeof(double));
   std::memcpy(h->hpin, X, (size_t)n * d * sizeof(double));
   DCHK_HIP(h, hipMemcpy(h->dX, h->hpin, (size_t)np * d * sizeof(double), hipMemcpyHostToDevice));
   // [f H] column-major, zero padded
-  DCHK(dalloc(h, &h->dF, (size_t)np * Pc));
+  DCHK(dalloc(h, &h->dF, (size_t)np * Pc, &h->shared_bytes));
   std::memset(h->hpin, 0, (size_t)np * Pc * sizeof(double));
   for (long long i = 0; i < n; ++i) {
     h->hpin[i] = f[i];
@@ -830,21 +941,17 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
   }
   DCHK_HIP(h, hipMemcpy(h->dF, h->hpin, (size_t)np * Pc * sizeof(double), hipMemcpyHostToDevice));
   h->has_r = r != nullptr;
+  dfree(&h->dr);
   if (r) {
-    DCHK(dalloc(h, &h->dr, (size_t)np));
+    DCHK(dalloc(h, &h->dr, (size_t)np, &h->shared_bytes));
     std::memset(h->hpin, 0, (size_t)np * sizeof(double));
     std::memcpy(h->hpin, r, (size_t)n * sizeof(double));
     DCHK_HIP(h, hipMemcpy(h->dr, h->hpin, (size_t)np * sizeof(double), hipMemcpyHostToDevice));
   }
-  DCHK(dalloc(h, &h->dinvdelta, 32));
-  // local tile rows
-  for (Rank& R : h->ranks) {
-    if (R.A) (void)hipFree(R.A);
-    if (R.logdet) (void)hipFree(R.logdet);
-    if (R.X) (void)hipFree(R.X);
-  }
-  h->ranks.clear();
-  h->grad_ready = false;
+  DCHK(dalloc(h, &h->dinvdelta, 32, &h->shared_bytes));
+  // local ranks and their sweep buffers
+  build_groups(h);
+  h->T0 = nloc_of(h->NB, h->P, 0);
   for (int rr = 0; rr < h->P; ++rr) {
     if (!h->loop && rr != h->rank) continue;
     Rank R;
@@ -853,18 +960,15 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
     R.ld = (long long)std::max(R.nloc, 1) * TILE;
     h->ranks.push_back(R);
     Rank& B = h->ranks.back();
-    DCHK(dalloc(h, &B.A, (size_t)B.ld * (size_t)(h->NB + 1) * TILE));
-    DCHK(dalloc(h, &B.logdet, (size_t)h->NB + 1));
+    DCHK(dalloc(h, &B.A, (size_t)B.ld * (size_t)(h->NB + 1) * TILE, &B.bytes));
+    DCHK(dalloc(h, &B.logdet, (size_t)h->NB + 1, &B.bytes));
+    DCHK(dalloc(h, &B.dinv, (size_t)TILE * TILE, &B.bytes));
+    DCHK(dalloc(h, &B.panel, (size_t)(h->NB + 1) * TILE * TILE * h->wmax, &B.bytes));
+    DCHK(dalloc(h, &B.recv, (size_t)h->P * h->T0 * TILE * TILE, &B.bytes));
+    DCHK(dalloc(h, &B.gram, (size_t)Pc * Pc, &B.bytes));
   }
-  build_groups(h);
-  DCHK(dalloc(h, &h->panel, (size_t)(h->NB + 1) * TILE * TILE * h->wmax));
-  if (!h->loop) {
-    const int T0 = nloc_of(h->NB, h->P, 0);   // the most tiles any rank contributes
-    DCHK(dalloc(h, &h->recv, (size_t)h->P * T0 * TILE * TILE));
-  }
-  DCHK(dalloc(h, &h->gram, (size_t)Pc * Pc));
   DCHK(build_schedule(h));
-  DCHK(ensure_events(h, (size_t)6 * h->NB + 16));
+  DCHK(ensure_events(h, (size_t)8 * h->NB + 32));
   return GPE_OK;
 }
 
@@ -890,9 +994,10 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
   const double rscale = (gp4ml && kernel == GPE_KERNEL_ALT_NUG) ? 1.0 : 0.0;
   if (want_grad) DCHK(ensure_grad(h));
   h->grad_now = want_grad != 0;
-  const size_t nslot = h->ranks.size();
+  h->ev = 0;
+  Rank& R0 = h->ranks[0];   // every rank holds the reduced results; read this process's first
 
-  DCHK(pinned(h, nslot * (NB + 1) + (size_t)Pc * Pc + nslot * (d + 2) + 64));
+  DCHK(pinned(h, (size_t)NB + 1 + (size_t)Pc * Pc + (size_t)(d + 2) + 64));
   for (int k = 0; k < d; ++k) {
     if (!(hp[k] > 0.0) && !(hp[k] < 0.0))   // as the single-GPU path: not positive definite
       return dfail(h, GPE_NOT_PD, "length scale delta[" + std::to_string(k) + "] is zero or NaN");
@@ -911,60 +1016,55 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
       DCHK_HIP(h, hipMemsetAsync(R.X, 0, (size_t)R.ld * NB * TILE * sizeof(double), h->stream));
   }
   DCHK(kbuild(h, kernel, nu, s2, rscale));
-  int ev = 0;
-  for (int k = 0; k < NB; ++k) DCHK(step(h, k, ev));
+  for (int k = 0; k < NB; ++k) DCHK(step(h, k));
 
   // Gram of L^-1 [f H] = -(tile (NB, NB)), and Z = L^-1 [f H], from the owner of tile row NB
   const int ra = NB % P;
-  for (Rank& R : h->ranks) {
-    if (R.rank != ra) continue;
-    const double* t = R.A + (long long)(NB / P) * TILE + (long long)NB * TILE * R.ld;
-    DCHK_HIP(h, hipMemcpy2DAsync(h->gram, Pc * sizeof(double), t, R.ld * sizeof(double), Pc * sizeof(double),
+  if (Rank* O = rank_slot(h, ra)) {
+    const double* t = O->A + (long long)(NB / P) * TILE + (long long)NB * TILE * O->ld;
+    DCHK_HIP(h, hipMemcpy2DAsync(O->gram, Pc * sizeof(double), t, O->ld * sizeof(double), Pc * sizeof(double),
                                  Pc, hipMemcpyDeviceToDevice, h->stream));
     if (h->grad_now) {
-      hipLaunchKernelGGL(k_dist_take_z, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, h->stream, R.A, R.ld,
-                         NB / P, np, Pc, h->dZ);
+      hipLaunchKernelGGL(k_dist_take_z, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, h->stream, O->A, O->ld,
+                         NB / P, np, Pc, O->dZ);
       DCHK_HIP(h, hipGetLastError());
     }
   }
-  if (!h->loop) {
-    const Rank& R = h->ranks[0];
-    DCHK_NCCL(h, ncclBroadcast(h->gram, h->gram, (size_t)Pc * Pc, ncclDouble, ra, h->comm, h->stream));
-    DCHK_NCCL(h, ncclAllReduce(R.logdet, R.logdet, (size_t)NB + 1, ncclDouble, ncclSum, h->comm, h->stream));
-    DCHK_NCCL(h, ncclAllReduce(h->dinfo, h->dinfo, 1, ncclInt32, ncclMax, h->comm, h->stream));
-    if (h->grad_now) DCHK_NCCL(h, ncclBroadcast(h->dZ, h->dZ, (size_t)np * Pc, ncclDouble, ra, h->comm, h->stream));
-  }
+  DCHK(coll_bcast(h, &Rank::gram, 0, (size_t)Pc * Pc, ra));
+  DCHK(coll_allreduce_sum(h, &Rank::logdet, 0, (size_t)NB + 1));
+  DCHK(coll_info_max(h));
+  if (h->grad_now) DCHK(coll_bcast(h, &Rank::dZ, 0, (size_t)np * Pc, ra));
   // host reads behind an event; the triangular inverse (independent of the host
   // algebra) is queued first so the GPU does not idle over the round trip
   double* hld = h->hpin;
-  double* hgram = h->hpin + nslot * (NB + 1);
-  for (size_t s = 0; s < nslot; ++s)
-    DCHK_HIP(h, hipMemcpyAsync(hld + s * (NB + 1), h->ranks[s].logdet, (NB + 1) * sizeof(double),
-                               hipMemcpyDeviceToHost, h->stream));
-  DCHK_HIP(h, hipMemcpyAsync(hgram, h->gram, (size_t)Pc * Pc * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  double* hgram = h->hpin + (NB + 1);
+  DCHK_HIP(h, hipMemcpyAsync(hld, R0.logdet, (NB + 1) * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  DCHK_HIP(h, hipMemcpyAsync(hgram, R0.gram, (size_t)Pc * Pc * sizeof(double), hipMemcpyDeviceToHost, h->stream));
   DCHK_HIP(h, hipMemcpyAsync(hgram + Pc * Pc, h->dinfo, sizeof(int), hipMemcpyDeviceToHost, h->stream));
   DCHK_HIP(h, hipEventRecord(h->e1, h->stream));
   if (h->grad_now)
-    for (int k = 0; k < NB; ++k) DCHK(trtri_step(h, k, ev));
+    for (int k = 0; k < NB; ++k) DCHK(trtri_step(h, k));
   DCHK_HIP(h, hipEventSynchronize(h->e1));
   int info = 0;
   std::memcpy(&info, hgram + Pc * Pc, sizeof(int));
-  if (info == GEMM_WAIT_TIMEOUT) return dfail(h, GPE_ERR_HIP, "internal error: flag wait timed out");
+  if (info == GEMM_WAIT_TIMEOUT) {
+    (void)hipStreamSynchronize(h->stream);
+    return dfail(h, GPE_ERR_HIP, "internal error: flag wait timed out");
+  }
   if (info != 0) {
+    (void)hipStreamSynchronize(h->stream);   // the queued inverse steps skip themselves (abort flag)
     h->err = "matrix not positive definite (pivot " + std::to_string(info) + ")";
     return GPE_NOT_PD;
   }
   double logdetA = 0.0;
-  for (int k = 0; k < NB; ++k) {
-    // loopback: step k's log-determinant part sits in its owner's slot; RCCL: summed
-    logdetA += h->loop ? hld[(size_t)(k % P) * (NB + 1) + k] : hld[k];
-  }
+  for (int k = 0; k < NB; ++k) logdetA += hld[k];
   logdetA *= 2.0;
   std::vector<double> G((size_t)Pc * Pc);
   for (int i = 0; i < Pc; ++i)
     for (int j = 0; j < Pc; ++j) G[(size_t)i * Pc + j] = -hgram[i + (size_t)j * Pc];
   SmallAlgebra sa = small_from_gram(G, Pc);
   if (!sa.ok) {
+    (void)hipStreamSynchronize(h->stream);
     h->err = "H^T A^-1 H not positive definite";
     return GPE_NOT_PD;
   }
@@ -989,62 +1089,45 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
     const std::vector<double> T2 = small_t2(sa, q, cfac);
     std::memcpy(h->hpin, T2.data(), T2.size() * sizeof(double));
     DCHK_HIP(h, hipMemcpyAsync(h->dT2, h->hpin, T2.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
-    hipLaunchKernelGGL(k_apply_small, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, h->stream, h->dZ, np, Pc,
-                       h->dT2, Pc, h->dR2, np, (int)np, h->dinfo);
-    DCHK_HIP(h, hipGetLastError());
-    DCHK_HIP(h, hipMemsetAsync(h->wpart, 0, (size_t)np * TILE * sizeof(double), h->stream));
-    for (size_t s = 0; s < nslot; ++s) {
-      const Rank& R = h->ranks[s];
+    for (size_t s = 0; s < h->ranks.size(); ++s) {
+      Rank& R = h->ranks[s];
+      DCHK_HIP(h, hipMemsetAsync(R.wpart, 0, (size_t)np * TILE * sizeof(double), h->stream));
       if (R.nlx == 0) continue;
+      hipLaunchKernelGGL(k_apply_small, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, h->stream, R.dZ, np, Pc,
+                         h->dT2, Pc, R.dR2, np, (int)np, h->dinfo);
+      DCHK_HIP(h, hipGetLastError());
       const long long e = (long long)R.nlx * TILE;
-      hipLaunchKernelGGL(k_dist_rows, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, h->stream, h->dR2, np, Pc,
-                         P, R.rank, R.nlx, h->r2loc, R.ld);
+      hipLaunchKernelGGL(k_dist_rows, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, h->stream, R.dR2, np, Pc,
+                         P, R.rank, R.nlx, R.r2loc, R.ld);
       DCHK_HIP(h, hipGetLastError());
       DCHK(launch(h, h->wa_l[s], h->gprobs));
     }
-    if (!h->loop) {
-      DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
-      DCHK_NCCL(h, ncclAllReduce(h->wpart, h->wpart, (size_t)np * Pc, ncclDouble, ncclSum, h->comm, h->stream));
-      DCHK_HIP(h, hipEventRecord(h->cev[ev++], h->stream));
-    }
-    // each rank: partial A^-1 over its rows, then its share of the contraction
-    DCHK_HIP(h, hipMemsetAsync(h->csum, 0, nslot * (d + 2) * sizeof(double), h->stream));
+    DCHK(coll_allreduce_sum(h, &Rank::wpart, 0, (size_t)np * Pc));
+    // each rank: its partial of A^-1 slab by slab, each slab contracted at once
     const int nblk = NB * (NB + 1) / 2;
-    const int bucket = std::max(d, Pc);
-    for (size_t s = 0; s < nslot; ++s) {
-      const Rank& R = h->ranks[s];
+    const long long lds = (long long)h->slab_rows * TILE;
+    for (size_t s = 0; s < h->ranks.size(); ++s) {
+      Rank& R = h->ranks[s];
+      DCHK_HIP(h, hipMemsetAsync(R.csum, 0, (size_t)(d + 2) * sizeof(double), h->stream));
       if (R.nlx == 0) continue;
-      DCHK(launch(h, h->lau_l[s], h->gprobs));
       const int q1 = R.rank == 0 ? Pc : 0;   // the -W W^T term once
-      const dim3 g(nblk);
-      if (d == 10 && Pc <= 13)
-        hipLaunchKernelGGL((k_contract<10, 13>), g, dim3(256), 0, h->stream, h->pbuf, np, h->dXw, d, h->wpart, np, q1, (int)h->n, h->cpart, h->dinfo);
-      else if (d == 20 && Pc <= 21)   // BASELINE configs[3]
-        hipLaunchKernelGGL((k_contract<20, 21>), g, dim3(256), 0, h->stream, h->pbuf, np, h->dXw, d, h->wpart, np, q1, (int)h->n, h->cpart, h->dinfo);
-      else if (bucket <= 8)
-        hipLaunchKernelGGL((k_contract<8, 9>), g, dim3(256), 0, h->stream, h->pbuf, np, h->dXw, d, h->wpart, np, q1, (int)h->n, h->cpart, h->dinfo);
-      else if (bucket <= 16)
-        hipLaunchKernelGGL((k_contract<16, 17>), g, dim3(256), 0, h->stream, h->pbuf, np, h->dXw, d, h->wpart, np, q1, (int)h->n, h->cpart, h->dinfo);
-      else
-        hipLaunchKernelGGL((k_contract<32, 33>), g, dim3(256), 0, h->stream, h->pbuf, np, h->dXw, d, h->wpart, np, q1, (int)h->n, h->cpart, h->dinfo);
-      DCHK_HIP(h, hipGetLastError());
-      hipLaunchKernelGGL(k_reduce_rows, dim3(d + 2), dim3(256), 0, h->stream, h->cpart, nblk, d + 2,
-                         h->csum + s * (d + 2));
+      for (const SlabLaunch& sl : h->slabs[s]) {
+        DCHK(launch(h, sl.gemm, h->gprobs));
+        const int b0 = sl.a0 * (sl.a0 + 1) / 2, b1 = sl.a1 * (sl.a1 + 1) / 2;
+        contract_launch(h, R.slab, lds, (long long)sl.a0 * TILE, b0, b1 - b0, R.wpart, q1);
+        DCHK_HIP(h, hipGetLastError());
+      }
+      hipLaunchKernelGGL(k_reduce_rows, dim3(d + 2), dim3(256), 0, h->stream, h->cpart, nblk, d + 2, R.csum);
       DCHK_HIP(h, hipGetLastError());
     }
-    if (!h->loop) {
-      DCHK_NCCL(h, ncclAllReduce(h->csum, h->csum, (size_t)d + 2, ncclDouble, ncclSum, h->comm, h->stream));
-    }
+    DCHK(coll_allreduce_sum(h, &Rank::csum, 0, (size_t)d + 2));
   }
   DCHK_HIP(h, hipEventRecord(h->e1, h->stream));
   if (h->grad_now)
-    DCHK_HIP(h, hipMemcpyAsync(h->hpin, h->csum, nslot * (d + 2) * sizeof(double), hipMemcpyDeviceToHost,
+    DCHK_HIP(h, hipMemcpyAsync(h->hpin, R0.csum, (size_t)(d + 2) * sizeof(double), hipMemcpyDeviceToHost,
                                h->stream));
   DCHK_HIP(h, hipStreamSynchronize(h->stream));
   if (h->grad_now) {
-    std::vector<double> red((size_t)d + 2, 0.0);
-    for (size_t s = 0; s < nslot; ++s)
-      for (int k = 0; k < d + 2; ++k) red[k] += h->hpin[s * (d + 2) + k];
     double coff, cdiag;
     if (kernel == GPE_KERNEL_ALT_NUG) {
       coff = 1.0;
@@ -1053,6 +1136,7 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
       coff = 1.0 - nu;
       cdiag = 1.0;
     }
+    std::vector<double> red(h->hpin, h->hpin + d + 2);
     small_grad(red.data(), d, kernel == GPE_KERNEL_ALT_NUG, nu, fitnug, gp4ml, gscale, s2, coff, cdiag, n_hp,
                grad_out);
   }
@@ -1061,7 +1145,7 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
     (void)hipEventElapsedTime(&ms, h->e0, h->e1);
     h->total_ms = ms;
     double c = 0.0;
-    for (int i = 0; i + 1 < ev; i += 2) {
+    for (int i = 0; i + 1 < h->ev; i += 2) {
       ms = 0.f;
       (void)hipEventElapsedTime(&ms, h->cev[i], h->cev[i + 1]);
       c += ms;
@@ -1076,6 +1160,16 @@ int gpe_dist_times(gpe_dist* h, double* total_ms, double* comm_ms) {
   if (total_ms) *total_ms = h->total_ms;
   if (comm_ms) *comm_ms = h->comm_ms;
   return GPE_OK;
+}
+
+int gpe_dist_rank_bytes(gpe_dist* h, int32_t rank, int64_t* bytes_out) {
+  if (!h || !bytes_out) return GPE_ERR_ARG;
+  for (const Rank& R : h->ranks)
+    if (R.rank == rank) {
+      *bytes_out = (int64_t)(R.bytes + h->shared_bytes);
+      return GPE_OK;
+    }
+  return dfail(h, GPE_ERR_ARG, "rank " + std::to_string(rank) + " is not held by this process");
 }
 
 }  // extern "C"

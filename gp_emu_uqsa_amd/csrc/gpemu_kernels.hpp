@@ -1484,19 +1484,23 @@ static __global__ void __launch_bounds__(256) k_colnorm2(const double* V, long l
 //   diagonal:            accT += M(i,i)
 // E recomputed from the scaled points (no n x n exp cache, no n x n dA).
 // part[blk][0:d] = acc_k, [d] = accE, [d+1] = accT
+// Slabs: the launch covers lower tiles blk0 .. blk0 + gridDim.x - 1 (row-major tile
+// order) and Ainv holds global rows row0 .. (A^-1 row gi at Ainv[gi - row0]).
 // ---------------------------------------------------------------------------
 template <int DMAX, int QMAX>
 static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, long long lda,
                                                   const double* xw, int d,
                                                   const double* Wa, long long ldw, int q1,
                                                   int n_valid, double* part,
-                                                  const int* abort_flag) {
+                                                  const int* abort_flag, int blk0 = 0,
+                                                  long long row0 = 0) {
   __shared__ double xs[TILE * DMAX];
   __shared__ double ws[TILE * QMAX];
   __shared__ double red[4 * (DMAX + 2)];
   if (abort_flag && *abort_flag) return;
   int ti, tj;
-  tri_decode(blockIdx.x, ti, tj);
+  const int blk = blk0 + (int)blockIdx.x;
+  tri_decode(blk, ti, tj);
   const int tid = threadIdx.x;
   // zero-padded to DMAX / QMAX: the padded terms are exact no-ops (fma(-0, 0, m) = m,
   // s + 0 = s), so the inner loops carry no per-dimension branch
@@ -1521,7 +1525,7 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
   double accE = 0.0, accT = 0.0;
   __syncthreads();
   if (gi < n_valid) {
-    const double* acol = Ainv + gi + (long long)tj * TILE * lda;
+    const double* acol = Ainv + (gi - row0) + (long long)tj * TILE * lda;
     const int cend = min((ti == tj) ? r + 1 : TILE, n_valid - tj * TILE);
     // columns c = (tid >> 7) + 2u, four loads in flight ahead of the arithmetic
     for (int c0 = (tid >> 7); c0 < cend; c0 += 8) {
@@ -1574,7 +1578,7 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
   if (tid < nv) {
     const double s = (red[tid] + red[(DMAX + 2) + tid]) +
                      (red[2 * (DMAX + 2) + tid] + red[3 * (DMAX + 2) + tid]);
-    part[(long long)blockIdx.x * nv + tid] = s;
+    part[(long long)blk * nv + tid] = s;
   }
 }
 

@@ -1,9 +1,11 @@
 """Row-block distributed objective across the GPUs of one node.
 
-One process per GPU (torchrun / torch.distributed.run sets RANK, WORLD_SIZE,
-LOCAL_RANK).  torch.distributed (gloo is enough: only 128 bytes travel) carries
-the RCCL unique id from rank 0 to the others; every data-path collective after
-that is RCCL on the GPU, issued by libgpemu.so itself (include/gpemu_dist.h):
+One process per GPU (bench.py's spawner or torch.distributed.run sets RANK,
+WORLD_SIZE, LOCAL_RANK).  The native rendezvous group (rendezvous.py: files on the
+node, no PyTorch; or a torch.distributed group the caller initialised) carries
+the 128-byte RCCL unique id from rank 0 to the others; every data-path
+collective after that is RCCL on the GPU, issued by libgpemu.so itself
+(include/gpemu_dist.h):
 a 128 KB broadcast of the diagonal-block inverse and an all-gather of the panel
 column per 128-column step; for the gradient a broadcast of one row of L^-1 per
 step, an all-reduce of [sqrt(c) alpha, W] (n x (q+1)) and of d+2 sums.
@@ -18,30 +20,44 @@ over ranks in that mode (replicas.py does that when the objective is local).
 from __future__ import annotations
 
 import os
+import sys
 
-from . import native
+from . import native, rendezvous
+
+
+def _resolve(group):
+    """(rank, world, broadcast(bytes or None) -> bytes) of `group`: a rendezvous
+    FileGroup, a torch.distributed group (or None = its default group when torch
+    initialised one), or None = the native default group."""
+    if group is None:
+        group = rendezvous.default_group()
+    if isinstance(group, rendezvous.FileGroup):
+        return group.rank, group.world_size, lambda b: group.broadcast_bytes(b, 0)
+    dist = sys.modules.get("torch.distributed")
+    if dist is not None and dist.is_available() and dist.is_initialized():
+        def bcast(b):
+            box = [b]
+            dist.broadcast_object_list(box, src=0, group=group)
+            return box[0]
+        return dist.get_rank(group), dist.get_world_size(group), bcast
+    raise RuntimeError("no process group: call rendezvous.init_from_env() in every rank first")
 
 
 def share_unique_id(make_id=None, group=None) -> bytes:
     """Rank 0 creates the communicator id, every rank returns the same 128 bytes.
 
     `make_id` (default: native.dist_unique_id) is only called on rank 0."""
-    import torch.distributed as dist
-    if not dist.is_initialized():
-        raise RuntimeError("torch.distributed is not initialised")
+    rank, _, bcast = _resolve(group)
     make_id = make_id or native.dist_unique_id
-    box = [make_id() if dist.get_rank(group) == 0 else None]
-    dist.broadcast_object_list(box, src=0, group=group)
-    uid = box[0]
+    uid = bcast(make_id() if rank == 0 else None)
     if not isinstance(uid, (bytes, bytearray)) or len(uid) != native.UNIQUE_ID_BYTES:
         raise RuntimeError("bad communicator id")
     return bytes(uid)
 
 
 def dist_context(device: int | None = None, group=None) -> native.DistContext:
-    """DistContext for this process's rank of the initialised process group."""
-    import torch.distributed as dist
-    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    """DistContext for this process's rank of the job's group."""
+    rank, world, _ = _resolve(group)
     if device is None:
         device = int(os.environ.get("LOCAL_RANK", rank))
     uid = share_unique_id(group=group)

@@ -31,6 +31,7 @@ _VP = _ct.c_void_p
 SIGNATURES = {
     "gpe_abi_version": (_ct.c_int, []),
     "gpe_device_count": (_ct.c_int, []),
+    "gpe_device_synchronize": (_ct.c_int, [_ct.c_int32]),
     "gpe_create": (_VP, [_ct.c_int32]),
     "gpe_destroy": (None, [_VP]),
     "gpe_last_error": (_ct.c_char_p, [_VP]),
@@ -73,6 +74,7 @@ SIGNATURES = {
     "gpe_dist_owner": (_ct.c_int32, [_ct.c_int32, _ct.c_int32]),
     "gpe_dist_local_rows": (_ct.c_int32, [_ct.c_int64, _ct.c_int32, _ct.c_int32]),
     "gpe_dist_times": (_ct.c_int, [_VP, _D, _D]),
+    "gpe_dist_rank_bytes": (_ct.c_int, [_VP, _ct.c_int32, _ct.POINTER(_ct.c_int64)]),
 }
 
 UNIQUE_ID_BYTES = 128
@@ -533,6 +535,21 @@ class DistContext:
         tot, comm = _ct.c_double(0.0), _ct.c_double(0.0)
         self._check(self.lib.gpe_dist_times(self._h, _ct.byref(tot), _ct.byref(comm)), "gpe_dist_times")
         return {"total_ms": tot.value, "comm_ms": comm.value}
+
+    def rank_bytes(self, rank: int | None = None) -> int:
+        """Device bytes held for `rank` (default: this process's rank; any logical
+        rank in loopback)."""
+        b = _ct.c_int64(0)
+        r = self.rank if rank is None else int(rank)
+        self._check(self.lib.gpe_dist_rank_bytes(self._h, r, _ct.byref(b)), "gpe_dist_rank_bytes")
+        return int(b.value)
+
+
+def device_synchronize(device: int) -> None:
+    """Wait for all work on GPU `device` (no PyTorch in the process)."""
+    rc = load_library().gpe_device_synchronize(int(device))
+    if rc != GPE_OK:
+        raise RuntimeError(f"gpe_device_synchronize({device}) failed ({rc})")
 
 
 def dist_unique_id() -> bytes:

@@ -30,9 +30,10 @@
 extern "C" {
 #endif
 
-#define GPE_ABI_VERSION 7   /* 3: gpe_dist_objective gained want_grad / grad_out; 4: sensitivity;
+#define GPE_ABI_VERSION 8   /* 3: gpe_dist_objective gained want_grad / grad_out; 4: sensitivity;
                                 5: gpe_noise_sample (noise_fit); 6: gpe_kernel_grad;
-                                7: gpe_lhc_maximin */
+                                7: gpe_lhc_maximin; 8: gpe_dist_rank_bytes,
+                                gpe_device_synchronize */
 
 enum gpe_status {
     GPE_OK = 0,
@@ -53,6 +54,8 @@ typedef struct gpe_ctx gpe_ctx;
 
 int gpe_abi_version(void);
 int gpe_device_count(void);
+/* Wait for all work on GPU `device` (the timed-region bracket of bench.py). */
+int gpe_device_synchronize(int32_t device);
 
 /* Create a context on one GPU (device index as HIP sees it). NULL on failure;
  * the reason is then available from gpe_last_error(NULL). */

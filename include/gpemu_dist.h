@@ -16,16 +16,19 @@
  *
  * Gradient: X = L^-1 is formed by rows with the same partition (per step the
  * owner finishes X(k, :) and RCCL broadcasts it; every rank updates its own rows);
- * each rank then forms its partial X_r^T X_r of A^-1 and contracts it locally, so
- * the only other collectives are an all-reduce of the n x (q+1) matrix
+ * each rank then forms its partial X_r^T X_r of A^-1 slab by slab (a few tile rows
+ * at a time, so per-rank memory stays O(n^2 / P)) and contracts it locally, so the
+ * only other collectives are an all-reduce of the n x (q+1) matrix
  * [sqrt(c) alpha, W] and of the d+2 contraction sums.
  *
  * Processes: one per GPU.  Rank 0 calls gpe_dist_unique_id, the host shares the
  * 128 bytes (torch.distributed / gloo in gp_emu_uqsa_amd/distributed.py), every
  * rank calls gpe_dist_create with it.  unique_id == NULL selects the in-process
- * loopback transport: all P logical ranks live in this process on one GPU, with
- * the same partition and schedule and device copies in place of RCCL (used to
- * test P = 2..8 on one GPU).
+ * loopback transport: all P logical ranks live in this process on one GPU, each
+ * with its own buffers, running the same partition, schedule and device code
+ * (pack, all-gather buffer, unpermute, broadcast rows, all-reduced partials);
+ * only the collective calls become device copies (used to test P = 2..8 on one
+ * GPU).
  *
  * Same conventions and status codes as gpemu.h.
  */
@@ -55,8 +58,9 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
 
 /* Objective (and gradient when want_grad != 0), arguments and outputs as
  * gpe_objective.  All ranks call it collectively and all receive the same llh,
- * gradient and sigma2.  The gradient buffers (this rank's rows of L^-1 and an
- * n_pad x n_pad partial of A^-1) are allocated on the first want_grad call. */
+ * gradient and sigma2.  The gradient buffers (this rank's rows of L^-1 and a slab
+ * of at most 1 GiB of its partial of A^-1) are allocated on the first want_grad
+ * call. */
 int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const double* hp,
                        int32_t n_hp, double nu_fixed, int32_t want_grad, double* llh_out,
                        double* grad_out, double* sigma2_out);
@@ -69,6 +73,10 @@ int32_t gpe_dist_local_rows(int64_t n, int32_t nranks, int32_t rank);
 /* Time of the last gpe_dist_objective: total and the part spent in collectives
  * (RCCL or loopback copies), ms, measured with HIP events on this rank. */
 int gpe_dist_times(gpe_dist* h, double* total_ms, double* comm_ms);
+
+/* Device bytes held for rank `rank` (this process's rank over RCCL, any logical
+ * rank in loopback): its own buffers plus the replicated inputs and schedules. */
+int gpe_dist_rank_bytes(gpe_dist* h, int32_t rank, int64_t* bytes_out);
 
 #ifdef __cplusplus
 }

@@ -1,7 +1,9 @@
 """Row-block distributed objective and gradient (include/gpemu_dist.h) on the GPU:
-the loopback transport (P logical ranks in one process, same partition and
-schedule as RCCL) for P = 1..8, and a 1-rank RCCL communicator, against the
-oracle (reference op order) and the single-GPU path.
+the loopback transport (P logical ranks in one process, each with its own
+buffers, running the device code of the RCCL path -- pack, all-gather buffer,
+unpermute, broadcast rows, all-reduced partials -- with copies for the
+collectives) for P = 1..8, and a 1-rank RCCL communicator, against the oracle
+(reference op order) and the single-GPU path.
 
 Gradient tolerance as tests/test_gpu_objective.py:
 |g - g_ref| <= 1e-7 (|g_ref| + max|g_ref|)."""
@@ -149,3 +151,27 @@ def test_loopback_column_groups(ctx, monkeypatch, groups, P):
     assert abs(llh - ref) <= 1e-10 * abs(ref), (llh, ref)
     ok, err = _grad_ok(g, gref, 1e-8)
     assert ok, err
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_loopback_rank_memory(P):
+    """Each logical rank holds its own tile rows (of A and, after a gradient call, of
+    L^-1): the per-rank bytes follow the partition, not n^2."""
+    n, d = 4000, 3
+    X, f, H = orc.synthetic_problem(n, d, seed=1)
+    dc = native.DistContext(0, P)
+    dc.set_data(X, f, H)
+    nb = (n + 127) // 128
+    val = [dc.rank_bytes(r) for r in range(P)]
+    for r in range(P):
+        rows = native.dist_local_rows(n, P, r)
+        assert val[r] >= rows * 128 * (nb + 1) * 128 * 8            # its tile rows of A
+        assert val[r] < (rows + 1) * 128 * (nb + 1) * 128 * 8 * 1.6   # plus panels and inputs
+    dc.objective(native.GP4ML, native.KERNEL_STD, _hp(d), want_grad=True)
+    grad = [dc.rank_bytes(r) for r in range(P)]
+    for r in range(P):
+        rows = native.dist_local_rows(n, P, r)
+        assert grad[r] - val[r] >= rows * 128 * nb * 128 * 8        # its rows of L^-1
+    with pytest.raises(RuntimeError):
+        dc.rank_bytes(P)
+    dc.close()
