@@ -6,9 +6,10 @@ one synchronous gpe_objective per evaluation.  NotPositiveDefinite is mapped to
 the reference's ``return None`` (:374-376, :489-491), which makes scipy raise
 TypeError and the multistart loop move on to the next guess (:248-251).
 
-Multistart tries are independent units: when torch.distributed is initialised
-with world_size > 1 the tries are sharded over ranks (one GPU per rank, no data
-exchange) and only the (fun, x) results are gathered -- the guess grid is drawn
+Multistart tries are independent units: in a job with world_size > 1 (the group
+of rendezvous.init_from_env(), or a torch.distributed group the caller set up)
+the tries are sharded over ranks (one GPU per rank, no data exchange) and only
+the (fun, x) results are gathered (replicas.py) -- the guess grid is drawn
 identically on every rank, so the chosen optimum equals the sequential one.
 With distributed.enable_objective() each evaluation is instead spread over all
 ranks (row-block partition) and every rank runs every try in lockstep.

@@ -33,14 +33,13 @@ def main():
     hp = np.concatenate([np.ones(args.dims), [1e-3, 1.0]])
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    dist = None
+    group = None
     if args.loopback:
         ctx = native.DistContext(int(os.environ.get("LOCAL_RANK", "0")), args.loopback)
         nranks = args.loopback
     else:
-        import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        from gp_emu_uqsa_amd import distributed
+        from gp_emu_uqsa_amd import distributed, rendezvous
+        group = rendezvous.init_from_env()
         ctx = distributed.dist_context()
         nranks = world
     ctx.set_data(X, f, H)
@@ -50,17 +49,14 @@ def main():
     llh, g = ev()   # warm-up (allocates the gradient buffers)
     ts = []
     for _ in range(args.reps):
-        if dist is not None:
-            dist.barrier()
+        if group is not None:
+            group.barrier()
         t = time.perf_counter()
         llh, g = ev()
         ts.append(time.perf_counter() - t)
     el = min(ts)
-    if dist is not None:
-        import torch
-        v = torch.tensor([el], dtype=torch.float64)
-        dist.all_reduce(v, op=dist.ReduceOp.MAX)
-        el = float(v.item())
+    if group is not None:
+        el = group.all_reduce_max(el)
     out = {"n": args.points, "d": args.dims, "ranks": nranks, "transport": "loopback" if args.loopback else "rccl",
            "grad": args.grad, "llh": llh, "ms_per_eval": 1e3 * el, **ctx.times()}
     if args.check and rank == 0:
@@ -75,8 +71,8 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    if group is not None:
+        group.close()
 
 
 if __name__ == "__main__":

@@ -59,9 +59,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     mode = "single"
+    group = None
     if world > 1:
-        import torch.distributed as tdist
-        tdist.init_process_group("gloo", rank=rank, world_size=world)
+        from gp_emu_uqsa_amd import rendezvous
+        group = rendezvous.init_from_env()
         distributed.enable_objective()
         mode = f"rowblock-rccl-{world}"
     elif args.loopback:
@@ -103,8 +104,8 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     distributed.disable_objective()
-    if world > 1:
-        tdist.destroy_process_group()
+    if group is not None:
+        group.close()
 
 
 if __name__ == "__main__":
