@@ -99,7 +99,7 @@ struct gpe_ctx {
   double* dT2 = nullptr;     // SK_PMAX^2
   double* dcpart = nullptr;  // contraction partials
   size_t cpart_cap = 0;
-  double* dcsum = nullptr;   // d+2
+  double* dcsum = nullptr;   // d+3
   GemmProb* dprobs = nullptr;
   unsigned* dtiles = nullptr;    // tile lists: training plan [0, cap/2), aux plan [cap/2, cap)
   size_t tiles_cap = 0;
@@ -977,7 +977,7 @@ int gpe_set_data(gpe_ctx* c, int64_t n, int32_t d, int32_t q, const double* X, c
     CHK(dalloc(c, &c->dZ, (size_t)n_pad * SK_PMAX));
     CHK(dalloc(c, &c->dR2, (size_t)n_pad * SK_PMAX));
     CHK(dalloc(c, &c->dWa, (size_t)n_pad * SK_PMAX));
-    const size_t cp = (size_t)c->NB * (c->NB + 1) / 2 * (d + 2);
+    const size_t cp = (size_t)c->NB * (c->NB + 1) / 2 * (d + 3);
     CHK(dalloc(c, &c->dcpart, cp));
     c->cpart_cap = cp;
   }
@@ -1110,29 +1110,30 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
     HIPCHK(c, hipGetLastError());
     CHK(skinny(c, true, c->tr.B, np, c->NB, c->NB, true, c->dR2, np, P, c->dWa, np));
     ev_rec(c, 6);
-    // contraction
+    // contraction; sum_i M_ii r_i for the std kernel's sigma gradient when r is set
+    const double* rdiag = (gp4ml && kernel == GPE_KERNEL_STD && c->has_r) ? c->dr : nullptr;
     const int nblk = c->NB * (c->NB + 1) / 2;
     const int bucket = std::max(d, P);
     if (d == 10 && P <= 13) {   // the headline configuration: no padded dimensions
-      hipLaunchKernelGGL((k_contract<10, 13>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo);
+      hipLaunchKernelGGL((k_contract<10, 13>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
     } else if (bucket <= 8) {
-      hipLaunchKernelGGL((k_contract<8, 9>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo);
+      hipLaunchKernelGGL((k_contract<8, 9>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
     } else if (bucket <= 16) {
-      hipLaunchKernelGGL((k_contract<16, 17>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo);
+      hipLaunchKernelGGL((k_contract<16, 17>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
     } else {
-      hipLaunchKernelGGL((k_contract<32, 33>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo);
+      hipLaunchKernelGGL((k_contract<32, 33>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
     }
     HIPCHK(c, hipGetLastError());
-    hipLaunchKernelGGL(k_reduce_rows, dim3(d + 2), dim3(256), 0, c->stream, c->dcpart, nblk, d + 2, c->dcsum);
+    hipLaunchKernelGGL(k_reduce_rows, dim3(d + 3), dim3(256), 0, c->stream, c->dcpart, nblk, d + 3, c->dcsum);
     HIPCHK(c, hipGetLastError());
     ev_rec(c, 7);
-    HIPCHK(c, hipMemcpyAsync(c->hpin, c->dcsum, (d + 2) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->hpin, c->dcsum, (d + 3) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const double* red = c->hpin;
     double coff, cdiag;
     kernel_consts(kernel, nu, true, &coff, &cdiag);
     small_grad(red, d, kernel == GPE_KERNEL_ALT_NUG, nu, fitnug, gp4ml, gscale, s2, coff, cdiag, n_hp,
-               grad_out);
+               grad_out, rdiag != nullptr);
   }
 done:
   if (c->prof) {

@@ -26,7 +26,7 @@
 //   <M, dA/dtheta> is linear in A^-1, so rank r contracts its own partial X_r^T X_r,
 //   formed slab by slab (a few tile rows of the lower triangle at a time, never the
 //   whole n x n), and rank 0 also carries the -W W^T term; W = [sqrt(c) alpha, W] is
-//   all-reduced (n x (q+1)) and then only the d+2 sums.
+//   all-reduced (n x (q+1)) and then only the d+3 sums.
 //
 // Every logical rank owns all of its buffers (tile rows, Dinv, panel, all-gather
 // buffer, Gram, log-det, X rows, broadcast row, W, slab, sums).  The two transports
@@ -189,7 +189,7 @@ struct Rank {              // one rank's buffers (one per process over RCCL, P i
   double* r2loc = nullptr; // local rows of R2, 128 columns (zero beyond Pc)
   double* wpart = nullptr; // n_pad x 128: [sqrt(c) alpha, W] (all-reduced)
   double* slab = nullptr;  // slab*128 x n_pad: tile rows of this rank's partial X_r^T X_r
-  double* csum = nullptr;  // d+2 contraction sums (all-reduced)
+  double* csum = nullptr;  // d+3 contraction sums (all-reduced)
   size_t bytes = 0;        // device bytes held for this rank
 };
 
@@ -604,10 +604,10 @@ int ensure_grad(gpe_dist* h) {
     DCHK_HIP(h, hipMemset(R.r2loc, 0, (size_t)R.ld * TILE * sizeof(double)));
     DCHK(dalloc(h, &R.wpart, (size_t)np * TILE, &R.bytes));
     DCHK(dalloc(h, &R.slab, (size_t)lds * np, &R.bytes));
-    DCHK(dalloc(h, &R.csum, (size_t)d + 2, &R.bytes));
+    DCHK(dalloc(h, &R.csum, (size_t)d + 3, &R.bytes));
   }
   DCHK(dalloc(h, &h->dT2, (size_t)Pc * Pc, &h->shared_bytes));
-  DCHK(dalloc(h, &h->cpart, (size_t)NB * (NB + 1) / 2 * (d + 2), &h->shared_bytes));
+  DCHK(dalloc(h, &h->cpart, (size_t)NB * (NB + 1) / 2 * (d + 3), &h->shared_bytes));
 
   // Rows of X = L^-1 in the Cholesky's column groups [gb, ge): the owner of row k first
   // applies the pending rows gb..k-1 of its group, R(k, 0:k) -= L(k, gb:k) X(gb:k, 0:k)
@@ -801,21 +801,21 @@ int step(gpe_dist* h, int k) {
 }
 
 void contract_launch(gpe_dist* h, const double* slab, long long lds, long long row0, int blk0, int nblk,
-                     const double* wpart, int q1) {
+                     const double* wpart, int q1, const double* rdiag) {
   const int d = h->d, Pc = h->q + 1, bucket = std::max(d, Pc);
   const long long np = h->n_pad;
   const dim3 g(nblk);
   const int nv = (int)h->n;
   if (d == 10 && Pc <= 13)
-    hipLaunchKernelGGL((k_contract<10, 13>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0);
+    hipLaunchKernelGGL((k_contract<10, 13>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0, rdiag);
   else if (d == 20 && Pc <= 21)   // BASELINE configs[3]
-    hipLaunchKernelGGL((k_contract<20, 21>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0);
+    hipLaunchKernelGGL((k_contract<20, 21>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0, rdiag);
   else if (bucket <= 8)
-    hipLaunchKernelGGL((k_contract<8, 9>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0);
+    hipLaunchKernelGGL((k_contract<8, 9>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0, rdiag);
   else if (bucket <= 16)
-    hipLaunchKernelGGL((k_contract<16, 17>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0);
+    hipLaunchKernelGGL((k_contract<16, 17>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0, rdiag);
   else
-    hipLaunchKernelGGL((k_contract<32, 33>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0);
+    hipLaunchKernelGGL((k_contract<32, 33>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0, rdiag);
 }
 
 }  // namespace
@@ -997,7 +997,7 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
   h->ev = 0;
   Rank& R0 = h->ranks[0];   // every rank holds the reduced results; read this process's first
 
-  DCHK(pinned(h, (size_t)NB + 1 + (size_t)Pc * Pc + (size_t)(d + 2) + 64));
+  DCHK(pinned(h, (size_t)NB + 1 + (size_t)Pc * Pc + (size_t)(d + 3) + 64));
   for (int k = 0; k < d; ++k) {
     if (!(hp[k] > 0.0) && !(hp[k] < 0.0))   // as the single-GPU path: not positive definite
       return dfail(h, GPE_NOT_PD, "length scale delta[" + std::to_string(k) + "] is zero or NaN");
@@ -1106,25 +1106,27 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
     // each rank: its partial of A^-1 slab by slab, each slab contracted at once
     const int nblk = NB * (NB + 1) / 2;
     const long long lds = (long long)h->slab_rows * TILE;
+    // sum_i M_ii r_i for the std kernel's sigma gradient when r is set (small_grad)
+    const double* rdiag = (gp4ml && kernel == GPE_KERNEL_STD && h->has_r) ? h->dr : nullptr;
     for (size_t s = 0; s < h->ranks.size(); ++s) {
       Rank& R = h->ranks[s];
-      DCHK_HIP(h, hipMemsetAsync(R.csum, 0, (size_t)(d + 2) * sizeof(double), h->stream));
+      DCHK_HIP(h, hipMemsetAsync(R.csum, 0, (size_t)(d + 3) * sizeof(double), h->stream));
       if (R.nlx == 0) continue;
       const int q1 = R.rank == 0 ? Pc : 0;   // the -W W^T term once
       for (const SlabLaunch& sl : h->slabs[s]) {
         DCHK(launch(h, sl.gemm, h->gprobs));
         const int b0 = sl.a0 * (sl.a0 + 1) / 2, b1 = sl.a1 * (sl.a1 + 1) / 2;
-        contract_launch(h, R.slab, lds, (long long)sl.a0 * TILE, b0, b1 - b0, R.wpart, q1);
+        contract_launch(h, R.slab, lds, (long long)sl.a0 * TILE, b0, b1 - b0, R.wpart, q1, rdiag);
         DCHK_HIP(h, hipGetLastError());
       }
-      hipLaunchKernelGGL(k_reduce_rows, dim3(d + 2), dim3(256), 0, h->stream, h->cpart, nblk, d + 2, R.csum);
+      hipLaunchKernelGGL(k_reduce_rows, dim3(d + 3), dim3(256), 0, h->stream, h->cpart, nblk, d + 3, R.csum);
       DCHK_HIP(h, hipGetLastError());
     }
-    DCHK(coll_allreduce_sum(h, &Rank::csum, 0, (size_t)d + 2));
+    DCHK(coll_allreduce_sum(h, &Rank::csum, 0, (size_t)d + 3));
   }
   DCHK_HIP(h, hipEventRecord(h->e1, h->stream));
   if (h->grad_now)
-    DCHK_HIP(h, hipMemcpyAsync(h->hpin, R0.csum, (size_t)(d + 2) * sizeof(double), hipMemcpyDeviceToHost,
+    DCHK_HIP(h, hipMemcpyAsync(h->hpin, R0.csum, (size_t)(d + 3) * sizeof(double), hipMemcpyDeviceToHost,
                                h->stream));
   DCHK_HIP(h, hipStreamSynchronize(h->stream));
   if (h->grad_now) {
@@ -1136,9 +1138,9 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
       coff = 1.0 - nu;
       cdiag = 1.0;
     }
-    std::vector<double> red(h->hpin, h->hpin + d + 2);
+    std::vector<double> red(h->hpin, h->hpin + d + 3);
     small_grad(red.data(), d, kernel == GPE_KERNEL_ALT_NUG, nu, fitnug, gp4ml, gscale, s2, coff, cdiag, n_hp,
-               grad_out);
+               grad_out, gp4ml && kernel == GPE_KERNEL_STD && h->has_r);
   }
   {
     float ms = 0.f;

@@ -1483,7 +1483,9 @@ static __global__ void __launch_bounds__(256) k_colnorm2(const double* V, long l
 //   off-diagonal (i>j):  accE += M E,  acc_k += M E (x_ik - x_jk)^2 / delta_k^2
 //   diagonal:            accT += M(i,i)
 // E recomputed from the scaled points (no n x n exp cache, no n x n dA).
-// part[blk][0:d] = acc_k, [d] = accE, [d+1] = accT
+// part[blk][0:d] = acc_k, [d] = accE, [d+1] = accT, [d+2] = accR = sum_i M(i,i) r_i
+// (rdiag non-null: the reference's sigma gradient subtracts diag(r) from A for every
+// kernel, _emulatoroptimise.py:476-478, while make_A adds r only for alt-nugget)
 // Slabs: the launch covers lower tiles blk0 .. blk0 + gridDim.x - 1 (row-major tile
 // order) and Ainv holds global rows row0 .. (A^-1 row gi at Ainv[gi - row0]).
 // ---------------------------------------------------------------------------
@@ -1493,10 +1495,10 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
                                                   const double* Wa, long long ldw, int q1,
                                                   int n_valid, double* part,
                                                   const int* abort_flag, int blk0 = 0,
-                                                  long long row0 = 0) {
+                                                  long long row0 = 0, const double* rdiag = nullptr) {
   __shared__ double xs[TILE * DMAX];
   __shared__ double ws[TILE * QMAX];
-  __shared__ double red[4 * (DMAX + 2)];
+  __shared__ double red[4 * (DMAX + 3)];
   if (abort_flag && *abort_flag) return;
   int ti, tj;
   const int blk = blk0 + (int)blockIdx.x;
@@ -1522,7 +1524,8 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
   }
 #pragma unroll
   for (int k = 0; k < QMAX; ++k) wi[k] = (k < q1) ? Wa[gi + (long long)k * ldw] : 0.0;
-  double accE = 0.0, accT = 0.0;
+  double accE = 0.0, accT = 0.0, accR = 0.0;
+  const double ri = (rdiag && gi < n_valid && ti == tj) ? rdiag[gi] : 0.0;
   __syncthreads();
   if (gi < n_valid) {
     const double* acol = Ainv + (gi - row0) + (long long)tj * TILE * lda;
@@ -1554,6 +1557,7 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
         // the diagonal entry goes to accT; adding the zeros the selects leave is exact
         const bool dg = gj == gi;
         accT += dg ? mij : 0.0;
+        accR += dg ? mij * ri : 0.0;
         const double me = dg ? 0.0 : mij * exp(-s);
         accE += me;
 #pragma unroll
@@ -1562,7 +1566,7 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
     }
   }
   // block reduction, fixed order
-  const int nv = d + 2;
+  const int nv = d + 3;
   const int lane = tid & 63, wave = tid >> 6;
   for (int k = 0; k < nv; ++k) {
     double v = 0.0;
@@ -1571,13 +1575,14 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
       if (kk == k) v = acc[kk];
     if (k == d) v = accE;
     if (k == d + 1) v = accT;
+    if (k == d + 2) v = accR;
     for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-    if (lane == 0) red[wave * (DMAX + 2) + k] = v;
+    if (lane == 0) red[wave * (DMAX + 3) + k] = v;
   }
   __syncthreads();
   if (tid < nv) {
-    const double s = (red[tid] + red[(DMAX + 2) + tid]) +
-                     (red[2 * (DMAX + 2) + tid] + red[3 * (DMAX + 2) + tid]);
+    const double s = (red[tid] + red[(DMAX + 3) + tid]) +
+                     (red[2 * (DMAX + 3) + tid] + red[3 * (DMAX + 3) + tid]);
     part[(long long)blk * nv + tid] = s;
   }
 }

@@ -97,13 +97,17 @@ inline std::vector<double> small_t2(const SmallAlgebra& sa, int q, double cfac) 
 
 // gradient from the contraction sums red[0:d] = sum M E dx_k^2, red[d] = sum_{i>j} M E,
 // red[d+1] = tr M (the d+2 outputs of k_contract); coff/cdiag as the K-build's
+// red = [S_1..S_d, E, T, R] from k_contract; std_r: the std kernel with a per-point r,
+// whose sigma derivative the reference takes as A - diag(r) although A carries no r
+// (_emulatoroptimise.py:476-478 vs _emulatorclasses.py:572-575): -1/2 sum_i M_ii r_i
 inline void small_grad(const double* red, int d, bool alt_nug, double nu, bool fitnug, bool gp4ml,
-                       double gscale, double s2, double coff, double cdiag, int n_hp, double* grad) {
+                       double gscale, double s2, double coff, double cdiag, int n_hp, double* grad,
+                       bool std_r = false) {
   const double pref = alt_nug ? 1.0 : (1.0 - nu);
   const double SE = 2.0 * red[d], Tr = red[d + 1];
   for (int k = 0; k < d; ++k) grad[k] = 0.5 * gscale * pref * 2.0 * red[k];
   if (fitnug) grad[d] = alt_nug ? 0.5 * gscale * nu * nu * Tr : 0.5 * gscale * (-0.5 * nu) * SE;
-  if (gp4ml) grad[n_hp - 1] = 0.5 * s2 * (coff * SE + cdiag * Tr);
+  if (gp4ml) grad[n_hp - 1] = 0.5 * s2 * (coff * SE + cdiag * Tr) - (std_r ? 0.5 * red[d + 2] : 0.0);
 }
 
 }  // namespace gpe

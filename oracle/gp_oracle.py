@@ -176,8 +176,10 @@ def objective_ref(X, f, H, hp, variant, kind, fit_nugget, r=None, want_grad=True
         dA = grad_nugget_ref(n, nu_eff, e, gs2, kind)
         grad[d] = _grad_term_ref(L, dA, f, invA_f, invA_H_B, H_B, Kq, sKH, invA_H, factor)
     if variant == GP4ML:
+        # :476-478 subtracts data.r for every kernel, though make_A adds r only for
+        # the alt-nugget kernel (:572-575): for the std kernel with r set, dA = A - diag(r)
         dA = A.copy()
-        if kind == ALT and r is not None:
+        if r is not None:
             dA[np.diag_indices_from(dA)] -= r
         grad[-1] = _grad_term_ref(L, dA, f, invA_f, invA_H_B, H_B, Kq, sKH, invA_H, factor)
     return llh, grad, sig2
@@ -248,6 +250,8 @@ def objective_fast(X, f, H, hp, variant, kind, fit_nugget, r=None, want_grad=Tru
             grad[d] = 0.5 * gscale * np.sum(M * (-0.5 * nu_eff * s2) * Eful * offd)
     if variant == GP4ML:
         grad[-1] = 0.5 * np.sum(M * (s2 * C))
+        if kind == STD and r is not None:      # the reference's A - diag(r) (objective_ref)
+            grad[-1] -= 0.5 * float(np.diag(M) @ np.asarray(r, dtype=np.float64))
     return llh, grad, sig2
 
 

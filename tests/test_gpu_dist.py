@@ -83,6 +83,7 @@ def test_loopback_gradient_matches_oracle(P, n):
 
 @pytest.mark.parametrize("variant,kernel,use_r,d,P", [(native.MUCM, native.KERNEL_STD, False, 4, 3),
                                                        (native.GP4ML, native.KERNEL_ALT_NUG, True, 4, 2),
+                                                       (native.GP4ML, native.KERNEL_STD, True, 4, 3),
                                                        (native.GP4ML, native.KERNEL_STD, False, 10, 4),
                                                        (native.GP4ML, native.KERNEL_STD, False, 20, 3)])
 def test_loopback_gradient_matches_single_gpu(ctx, variant, kernel, use_r, d, P):

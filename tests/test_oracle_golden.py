@@ -16,6 +16,8 @@ CASES = [
     ("alt_gp4ml_fitnug", orc.ALT, orc.GP4ML, True, False),
     ("alt_gp4ml_fixnug", orc.ALT, orc.GP4ML, False, False),
     ("alt_gp4ml_fitnug_r", orc.ALT, orc.GP4ML, True, True),
+    ("std_gp4ml_fitnug_r", orc.STD, orc.GP4ML, True, True),
+    ("std_gp4ml_fixnug_r", orc.STD, orc.GP4ML, False, True),
 ]
 
 
