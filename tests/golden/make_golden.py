@@ -197,12 +197,35 @@ def make_g3():
             rs = np.random.RandomState(17)
             xs = rs.uniform(size=(20, d))
             mean, var = quiet(g.posterior, E, xs)
+            # a14, before optimalbeta changes E.par.beta: seeded posterior_sample
+            # (emulatorfunctions.py:255-286), and on a validation-style set (outputs
+            # drawn around the posterior, some >= 2 sd away) interval /
+            # indiv_standard_error / mahalanobis_distance (_emulatorclasses.py:635-676)
+            np.random.seed(23)
+            sample = quiet(g.posterior_sample, E, xs)
+            rs2 = np.random.RandomState(29)
+            ys = mean + rs2.normal(scale=1.5, size=mean.size) * np.sqrt(np.abs(np.diag(var)))
+            Dv = emuc.Data(xs.copy(), ys.copy(), E.basis, E.par, E.beliefs, E.K)
+            p = quiet(emuc.Posterior, Dv, E.training, E.par, E.beliefs, E.K)
+            p.interval()
+            buf = io.StringIO()
+            with contextlib.redirect_stdout(buf):
+                ise_retrain = p.indiv_standard_error(ise=2.0)
+            ise_text = buf.getvalue()
+            buf = io.StringIO()
+            with contextlib.redirect_stdout(buf):
+                p.mahalanobis_distance()
+            md_text = buf.getvalue()
+            md = float(md_text.split("calculated Mahalanobis_distance:")[1].split()[0])
             beta_stored = E.par.beta.copy()
             A = E.training.A.copy()
             quiet(E.opt_T.optimalbeta)
             beta_opt = E.par.beta.copy()
             out = dict(XT=E.training.inputs, fT=E.training.outputs, HT=E.training.H,
                        xs=xs, mean=mean, var=var, A_trace=np.trace(A), A_sum=A.sum(),
+                       sample_seed=np.array(23), sample=sample, ys=ys, LI=p.LI, UI=p.UI,
+                       ise_retrain=np.array(ise_retrain), ise_text=np.array(ise_text),
+                       md=np.array(md), md_text=np.array(md_text),
                        beta=beta_stored, beta_opt=beta_opt,
                        delta=np.array(E.par.delta, float), nu=np.array(E.par.nugget),
                        sigma=np.array(E.par.sigma),

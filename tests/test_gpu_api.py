@@ -5,7 +5,8 @@
   the same trained hyperparameters, sigma and beta (1e-6 relative).
   The same again with the objective routed through the row-block distributed
   path (distributed.enable_objective, loopback transport, 3 logical ranks).
-* g.posterior() on the reconstructed emulators (G3) within 1e-8.
+* g.posterior() on the reconstructed emulators (G3) within 1e-8, and the seeded
+  posterior_sample, interval, indiv_standard_error and mahalanobis_distance (a14).
 """
 import json
 import os
@@ -110,3 +111,36 @@ def test_plot_and_sample(workdir, monkeypatch):
     np.random.seed(3)
     s = g.posterior_sample(E, np.random.uniform(size=(15, 2)))
     assert s.shape == (15,) and np.all(np.isfinite(s))
+
+
+@pytest.mark.parametrize("sub,conf,tag", [
+    ("toy-sim/reconstruct", "toy-sim_config_recon", "toysim"),
+    ("sensitivity_recon", "toysim3D_config0_recon", "toysim3d_o0"),
+    ("sensitivity_recon", "toysim3D_config1_recon", "toysim3d_o1")])
+def test_sample_interval_diagnostics_golden(workdir, capsys, sub, conf, tag):
+    """a14 against the reference's own outputs (G3): the seeded posterior_sample
+    (emulatorfunctions.py:255-286: mean + chol(var) randn), and on a validation-style
+    set Posterior.interval, indiv_standard_error (flagged points and their printed
+    lines) and mahalanobis_distance (_emulatorclasses.py:635-676).  Tolerance 1e-8 on
+    values; the printed text must match (its numbers are rounded by the reference)."""
+    from gp_emu_uqsa_amd import model
+    z = np.load(os.path.join(GOLD, f"posterior_{tag}.npz"))
+    workdir(sub)
+    E = g.setup(conf, datashuffle=False)
+    xs = z["xs"]
+    np.random.seed(int(z["sample_seed"]))
+    s = g.posterior_sample(E, xs)
+    assert np.max(np.abs(s - z["sample"])) < 1e-8, np.max(np.abs(s - z["sample"]))
+    Dv = model.Data(xs.copy(), z["ys"].copy(), E.basis, E.par, E.beliefs, E.K)
+    p = model.Posterior(Dv, E.training, E.par, E.beliefs, E.K)
+    p.interval()
+    assert np.max(np.abs(p.LI - z["LI"])) < 1e-8 and np.max(np.abs(p.UI - z["UI"])) < 1e-8
+    capsys.readouterr()
+    assert p.indiv_standard_error(ise=2.0) == bool(z["ise_retrain"])
+    assert capsys.readouterr().out == str(z["ise_text"])
+    p.mahalanobis_distance()
+    out = capsys.readouterr().out
+    ref_lines, lines = str(z["md_text"]).splitlines(), out.splitlines()
+    assert lines[0] == ref_lines[0]                         # theoretical mean / variance
+    md = float(lines[1].split(":")[1])
+    assert abs(md - float(z["md"])) <= 1e-8 * abs(float(z["md"])), (md, float(z["md"]))
