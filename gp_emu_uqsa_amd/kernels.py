@@ -15,6 +15,13 @@ import numpy as _np
 
 from . import native
 
+# the reference sets NumPy's global print options when its kernel, optimiser and
+# plotting modules are imported (_emulatorkernels.py:6-7, _emulatoroptimise.py:19-20,
+# _emulatorplotting.py:6-7); its printed arrays (hyperparameters, "Bad predictions")
+# depend on them
+_np.set_printoptions(precision=6)
+_np.set_printoptions(suppress=True)
+
 
 class _GaussianBase:
     kind = native.KERNEL_STD
