@@ -113,7 +113,7 @@ def test_c3_train_loop(monkeypatch):
     assert np.max(np.abs(grad - res.jac)) <= 1e-9 * np.max(np.abs(res.jac))
     # L-BFGS-B stops on pgtol (projected gradient <= 1e-5) or on the relative reduction
     # of f (ftol = factr * eps = 2.2e-9): with LLH ~ 1e5 the latter can end the chain with
-    # a projected gradient of order ftol |f| per unit step; require whichever it reported
+    # a projected gradient of order ftol |f| (measured 2.2e-5 at |f| = 2.2e4); require the criterion it reported
     lo, hi = bounds[:, 0], bounds[:, 1]
     pg = np.clip(x - grad, lo, hi) - x
     msg = res.message if isinstance(res.message, str) else res.message.decode()
@@ -123,7 +123,7 @@ def test_c3_train_loop(monkeypatch):
         assert np.max(np.abs(pg)) <= 1e-5, pg
     else:
         assert "RELATIVE REDUCTION OF F" in msg, msg
-        assert np.max(np.abs(pg)) <= 1e3 * 2.2e-9 * abs(fun), (pg, fun)
+        assert np.max(np.abs(pg)) <= 10 * 2.2e-9 * abs(fun), (pg, fun)
 
 
 @pytest.mark.timeout(900)
