@@ -89,14 +89,14 @@ struct gpe_ctx {
 
   int* dinfo = nullptr;
   double* dinvdelta = nullptr;
-  double* dZ = nullptr;      // n_pad x SK_PMAX
-  double* dR2 = nullptr;     // n_pad x SK_PMAX
-  double* dWa = nullptr;     // n_pad x SK_PMAX
+  double* dZ = nullptr;      // n_pad x max(SK_PMAX, q + 1)
+  double* dR2 = nullptr;     // n_pad x max(SK_PMAX, q + 1)
+  double* dWa = nullptr;     // n_pad x max(SK_PMAX, q + 1)
   double* dskp = nullptr;    // skinny partials
   size_t skp_cap = 0;
   double* dgpart = nullptr;  // gram partials
-  double* dgram = nullptr;   // SK_PMAX^2
-  double* dT2 = nullptr;     // SK_PMAX^2
+  double* dgram = nullptr;   // GPE_MAX_COLS^2
+  double* dT2 = nullptr;     // GPE_MAX_COLS^2
   double* dcpart = nullptr;  // contraction partials
   size_t cpart_cap = 0;
   double* dcsum = nullptr;   // d+3
@@ -138,6 +138,12 @@ struct gpe_ctx {
   // noise_fit workspace (gpe_noise_sample): Dnew's r, the draws U^T, L U^T, e, z
   double* dRn = nullptr;
   size_t rn_cap = 0;
+  // full posterior covariance beyond one chunk: V = L^-1 K*, scaled points and
+  // T Kq^-T for every point, kept until the blocks of the m x m result are formed
+  double* dVall = nullptr;
+  double* dXall = nullptr;
+  double* dTall = nullptr;
+  size_t vall_cap = 0, xall_cap = 0, tall_cap = 0;
   double* dNU = nullptr;
   size_t nu_cap = 0;
 
@@ -232,6 +238,11 @@ inline int pmax_bucket(int P) { return P <= 8 ? 8 : (P <= 16 ? 16 : 32); }
 
 // ------------------------------------------------------------------ launches
 int launch_pairs(gpe_ctx* c, const PairArgs& a, int nblocks) {
+  if (a.d > 32) {   // any d: coordinates staged through LDS in chunks of 32
+    hipLaunchKernelGGL(k_pairs_wide, dim3(nblocks), dim3(256), 0, c->stream, a);
+    HIPCHK(c, hipGetLastError());
+    return GPE_OK;
+  }
   // the smallest padded width >= d (zero-padded dimensions cost one FMA each)
   static constexpr int widths[] = {2, 4, 6, 8, 10, 12, 16, 20, 24, 32};
   int dm = 32;
@@ -593,7 +604,7 @@ int ensure_fact(gpe_ctx* c, Fact& F, long long n_pad) {
 
 // scaled points for the training set
 int scale_training(gpe_ctx* c, const double* delta) {
-  CHK(ensure_pinned(c, 64));
+  CHK(ensure_pinned(c, GPE_MAX_DIMS + 64));
   for (int k = 0; k < c->d; ++k) {
     // zero or NaN length scale: the reference's covariance is NaN there and its Cholesky
     // raises LinAlgError (-> `return None`, _emulatoroptimise.py:374-376, :489-491)
@@ -694,7 +705,12 @@ int trtri(gpe_ctx* c, Fact& F) {
 // Y(0:n_rows, 0:P) = op(M) x R  with M lower-tiled (ld = n_pad) or full
 int skinny(gpe_ctx* c, bool transposed, const double* M, long long ldm, int ntr, int nit,
            bool lower, const double* R, long long ldr, int P, double* Y, long long ldy) {
-  if (P > SK_PMAX) return fail(c, GPE_ERR_UNSUPPORTED, "too many right-hand sides");
+  if (P > SK_PMAX) {   // columns are independent: 32 at a time
+    for (int c0 = 0; c0 < P; c0 += SK_PMAX)
+      CHK(skinny(c, transposed, M, ldm, ntr, nit, lower, R + (long long)c0 * ldr, ldr, std::min(SK_PMAX, P - c0),
+                 Y + (long long)c0 * ldy, ldy));
+    return GPE_OK;
+  }
   const int nch = lower ? (std::max(ntr, nit) + SK_CH - 1) / SK_CH : (ntr + SK_CH - 1) / SK_CH;
   const long long rows = (long long)nit * TILE;
   const size_t need = (size_t)nch * rows * P;
@@ -739,12 +755,30 @@ int skinny(gpe_ctx* c, bool transposed, const double* M, long long ldm, int ntr,
   return GPE_OK;
 }
 
+// Y = Z T (Z nrows x P, T P x Pout column-major)
+int apply_small(gpe_ctx* c, const double* Z, long long ldz, int P, const double* T, int Pout, double* Y,
+                long long ldy, int nrows, const int* abort_flag) {
+  const dim3 g((unsigned)((nrows + 255) / 256));
+  if (P <= SK_PMAX)
+    hipLaunchKernelGGL(k_apply_small, g, dim3(256), 0, c->stream, Z, ldz, P, T, Pout, Y, ldy, nrows, abort_flag);
+  else
+    hipLaunchKernelGGL(k_apply_big, g, dim3(256), 0, c->stream, Z, ldz, P, T, Pout, Y, ldy, nrows, abort_flag);
+  HIPCHK(c, hipGetLastError());
+  return GPE_OK;
+}
+
+inline int gram_pairs(int P) {
+  const int nch = (P + SK_PMAX - 1) / SK_PMAX;
+  return nch * (nch + 1) / 2;
+}
+
 // G = Z^T Z (P x P) on the host (doubles, row-major == col-major: symmetric)
 int gram(gpe_ctx* c, const double* Z, long long ldz, int P, int nrows, double* host_out) {
   const int nblk = (nrows + 255) / 256;
   const size_t need = (size_t)nblk * P * P;
   CHK(ensure_small(c, need + P * P));
-  hipLaunchKernelGGL(k_gram, dim3(nblk), dim3(256), 0, c->stream, Z, ldz, P, nrows, c->dsmall, c->dinfo);
+  hipLaunchKernelGGL(k_gram, dim3(nblk, gram_pairs(P)), dim3(256), 0, c->stream, Z, ldz, P, nrows, c->dsmall,
+                     c->dinfo);
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(k_reduce_rows, dim3(P * P), dim3(256), 0, c->stream, c->dsmall, nblk, P * P,
                      c->dgram);
@@ -762,7 +796,8 @@ int gram_async(gpe_ctx* c, const double* Z, long long ldz, int P, int nrows) {
   const int nblk = (nrows + 255) / 256;
   const size_t need = (size_t)nblk * P * P;
   CHK(ensure_small(c, need + P * P));
-  hipLaunchKernelGGL(k_gram, dim3(nblk), dim3(256), 0, c->stream, Z, ldz, P, nrows, c->dsmall, c->dinfo);
+  hipLaunchKernelGGL(k_gram, dim3(nblk, gram_pairs(P)), dim3(256), 0, c->stream, Z, ldz, P, nrows, c->dsmall,
+                     c->dinfo);
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(k_reduce_rows, dim3(P * P), dim3(256), 0, c->stream, c->dsmall, nblk, P * P,
                      c->dgram);
@@ -893,8 +928,9 @@ gpe_ctx* gpe_create(int32_t device) {
     return nullptr;
   }
   bool ok = dalloc(c, &c->dinfo, 4) == GPE_OK && dalloc(c, &c->dprobs, MAX_PROBS) == GPE_OK &&
-            dalloc(c, &c->dgram, SK_PMAX * SK_PMAX) == GPE_OK &&
-            dalloc(c, &c->dT2, SK_PMAX * SK_PMAX) == GPE_OK && dalloc(c, &c->dinvdelta, 64) == GPE_OK &&
+            dalloc(c, &c->dgram, GPE_MAX_COLS * GPE_MAX_COLS) == GPE_OK &&
+            dalloc(c, &c->dT2, GPE_MAX_COLS * GPE_MAX_COLS) == GPE_OK &&
+            dalloc(c, &c->dinvdelta, GPE_MAX_DIMS) == GPE_OK &&
             dalloc(c, &c->dcsum, 64) == GPE_OK;
   for (int i = 0; i < 16 && ok; ++i) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
   if (ok) {
@@ -921,7 +957,8 @@ void gpe_destroy(gpe_ctx* c) {
                     c->dX, c->dXw, c->dF, c->dr, c->tr.A, c->tr.B, c->tr.logdet, c->aux.A, c->aux.B,
                     c->aux.logdet, c->dinvdelta, c->dZ,
                     c->dR2, c->dWa, c->dskp, c->dgpart, c->dgram, c->dT2, c->dcpart, c->dcsum,
-                    c->dW1, c->dW2, c->dW3, c->dXs, c->dXsw, c->dsmall, c->dRn, c->dNU};
+                    c->dW1, c->dW2, c->dW3, c->dXs, c->dXsw, c->dsmall, c->dRn, c->dNU,
+                    c->dVall, c->dXall, c->dTall};
   for (double* b : bufs)
     if (b) hipFree(b);
   if (c->dinfo) hipFree(c->dinfo);
@@ -957,8 +994,8 @@ int gpe_set_data(gpe_ctx* c, int64_t n, int32_t d, int32_t q, const double* X, c
                  const double* H, const double* r) {
   if (!c) return GPE_ERR_ARG;
   if (n <= 0 || d <= 0 || q <= 0 || !X || !f || !H) return fail(c, GPE_ERR_ARG, "bad data arguments");
-  if (d > 32) return fail(c, GPE_ERR_UNSUPPORTED, "d > 32 input dimensions is not supported");
-  if (q + 1 > SK_PMAX) return fail(c, GPE_ERR_UNSUPPORTED, "q > 31 basis functions is not supported");
+  if (d > GPE_MAX_DIMS) return fail(c, GPE_ERR_UNSUPPORTED, "more than 128 input dimensions");
+  if (q + 1 > GPE_MAX_COLS) return fail(c, GPE_ERR_UNSUPPORTED, "more than 127 basis functions");
   if (n > (1LL << 20)) return fail(c, GPE_ERR_UNSUPPORTED, "n too large");
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -974,9 +1011,10 @@ int gpe_set_data(gpe_ctx* c, int64_t n, int32_t d, int32_t q, const double* X, c
     CHK(dalloc(c, &c->dXw, (size_t)n_pad * d));
     CHK(dalloc(c, &c->dF, (size_t)n_pad * (q + 1)));
     CHK(dalloc(c, &c->dr, (size_t)n_pad));
-    CHK(dalloc(c, &c->dZ, (size_t)n_pad * SK_PMAX));
-    CHK(dalloc(c, &c->dR2, (size_t)n_pad * SK_PMAX));
-    CHK(dalloc(c, &c->dWa, (size_t)n_pad * SK_PMAX));
+    const size_t cols = (size_t)std::max(SK_PMAX, q + 1);
+    CHK(dalloc(c, &c->dZ, (size_t)n_pad * cols));
+    CHK(dalloc(c, &c->dR2, (size_t)n_pad * cols));
+    CHK(dalloc(c, &c->dWa, (size_t)n_pad * cols));
     const size_t cp = (size_t)c->NB * (c->NB + 1) / 2 * (d + 3);
     CHK(dalloc(c, &c->dcpart, cp));
     c->cpart_cap = cp;
@@ -1105,16 +1143,16 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
     const std::vector<double> T2 = small_t2(sa, q, cfac);
     std::memcpy(c->hpin, T2.data(), T2.size() * sizeof(double));
     HIPCHK(c, hipMemcpyAsync(c->dT2, c->hpin, T2.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    hipLaunchKernelGGL(k_apply_small, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, c->stream,
-                       c->dZ, np, P, c->dT2, P, c->dR2, np, (int)np, c->dinfo);
-    HIPCHK(c, hipGetLastError());
+    CHK(apply_small(c, c->dZ, np, P, c->dT2, P, c->dR2, np, (int)np, c->dinfo));
     CHK(skinny(c, true, c->tr.B, np, c->NB, c->NB, true, c->dR2, np, P, c->dWa, np));
     ev_rec(c, 6);
     // contraction; sum_i M_ii r_i for the std kernel's sigma gradient when r is set
     const double* rdiag = (gp4ml && kernel == GPE_KERNEL_STD && c->has_r) ? c->dr : nullptr;
     const int nblk = c->NB * (c->NB + 1) / 2;
     const int bucket = std::max(d, P);
-    if (d == 10 && P <= 13) {   // the headline configuration: no padded dimensions
+    if (d > 32 || P > 33) {   // any d and q: staged through LDS in chunks of 32
+      hipLaunchKernelGGL(k_contract_wide, dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
+    } else if (d == 10 && P <= 13) {   // the headline configuration: no padded dimensions
       hipLaunchKernelGGL((k_contract<10, 13>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
     } else if (bucket <= 8) {
       hipLaunchKernelGGL((k_contract<8, 9>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
@@ -1227,8 +1265,9 @@ int gpe_sense_pairs(gpe_ctx* c, int32_t J, const double* w, const double* u, int
   if (J <= 0 || J > 65535 || p <= 0 || !w || !u || !Z || !trace_out || !quad_out)
     return fail(c, GPE_ERR_ARG, "bad sense_pairs args");
   const int d = c->d;
-  const int need_d = std::max(d, p - 2);
-  if (d > 32 || p > 34) return fail(c, GPE_ERR_UNSUPPORTED, "sense_pairs supports d <= 32, p <= 34");
+  if (d > 32) return fail(c, GPE_ERR_UNSUPPORTED, "sense_pairs supports d <= 32 input dimensions");
+  // Z columns in chunks of at most 32 (one launch each; PMAX = the chunk bucket + 2)
+  const int pchunk = std::min(p, 32);
   const long long np = c->n_pad, n = c->n;
   const int NB = c->NB;
   CHK(ensure_ainv(c));
@@ -1256,15 +1295,19 @@ int gpe_sense_pairs(gpe_ctx* c, int32_t J, const double* w, const double* u, int
     for (int k = 0; k < p; ++k) c->hpin[i + k * np] = Z[i * p + k];
   HIPCHK(c, hipMemcpyAsync(c->dSZ, c->hpin, (size_t)np * p * sizeof(double), hipMemcpyHostToDevice, c->stream));
   const dim3 grid((unsigned)NB, (unsigned)J, (unsigned)CS);
+  const int need_d = std::max(d, pchunk - 2);
+  for (int zc0 = 0; zc0 < p; zc0 += pchunk) {
+    const int pc = std::min(pchunk, p - zc0);
 #define SENSE_LAUNCH(DM, PM)                                                                              \
   hipLaunchKernelGGL((k_sense_pairs<DM, PM>), grid, dim3(256), 0, c->stream, c->tr.A, np, c->dX, d, c->dSW, \
-                     c->dSU, np, c->dSZ, np, p, (int)n, cslice, c->dSpart, ldp)
-  if (need_d <= 4) SENSE_LAUNCH(4, 6);
-  else if (need_d <= 8) SENSE_LAUNCH(8, 10);
-  else if (need_d <= 16) SENSE_LAUNCH(16, 18);
-  else SENSE_LAUNCH(32, 34);
+                     c->dSU, np, c->dSZ, np, p, (int)n, cslice, c->dSpart, ldp, zc0, pc)
+    if (need_d <= 4) SENSE_LAUNCH(4, 6);
+    else if (need_d <= 8) SENSE_LAUNCH(8, 10);
+    else if (need_d <= 16) SENSE_LAUNCH(16, 18);
+    else SENSE_LAUNCH(32, 34);
 #undef SENSE_LAUNCH
-  HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipGetLastError());
+  }
   hipLaunchKernelGGL(k_reduce_rows, dim3((unsigned)ldp), dim3(256), 0, c->stream, c->dSpart, NB * CS * 4,
                      (int)ldp, c->dSout);
   HIPCHK(c, hipGetLastError());
@@ -1355,7 +1398,18 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
     HIPCHK(c, hipGetLastError());
     c->x32_valid = true;
   }
-  if (full_var && m > CHUNK) return fail(c, GPE_ERR_UNSUPPORTED, "full posterior variance limited to m <= 16384");
+  // full covariance of more than one chunk: every chunk's V, scaled points and T Kq^-T
+  // are kept on the device, then the m x m result is formed block by block (below)
+  const bool big = full_var && m > CHUNK;
+  const long long mtot = ((m + TILE - 1) / TILE) * TILE;
+  const int kq = ((q + 15) / 16) * 16;
+  std::vector<double> Th;
+  if (big) {
+    CHK(grow(c, &c->dVall, &c->vall_cap, (size_t)np * mtot));
+    CHK(grow(c, &c->dXall, &c->xall_cap, (size_t)mtot * d));
+    CHK(grow(c, &c->dTall, &c->tall_cap, (size_t)mtot * kq));
+    Th.assign((size_t)mtot * kq, 0.0);
+  }
   // [gamma, G] = A^-1 [f - H beta, H]
   CHK(ensure_pinned(c, (size_t)P * P + 64));
   {
@@ -1368,9 +1422,7 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
     std::memcpy(c->hpin, T.data(), T.size() * sizeof(double));
     HIPCHK(c, hipMemcpyAsync(c->dT2, c->hpin, T.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
   }
-  hipLaunchKernelGGL(k_apply_small, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, c->stream,
-                     c->dF, np, P, c->dT2, P, c->dR2, np, (int)np, nullptr);
-  HIPCHK(c, hipGetLastError());
+  CHK(apply_small(c, c->dF, np, P, c->dT2, P, c->dR2, np, (int)np, nullptr));
   CHK(skinny(c, false, c->tr.B, np, c->NB, c->NB, true, c->dR2, np, P, c->dZ, np));   // L^-1 [f-Hb, H]
   CHK(skinny(c, true, c->tr.B, np, c->NB, c->NB, true, c->dZ, np, P, c->dWa, np));   // A^-1 [f-Hb, H]
   std::vector<double> G((size_t)P * P);
@@ -1425,32 +1477,35 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
     double* dY = c->dR2;   // reuse (np >= ... not guaranteed) -> use dsmall
     CHK(ensure_small(c, (size_t)mp * P + 64));
     dY = c->dsmall;
-    {
-      // skinny transposed over a full matrix: M = K* (np x mp), k tiles = NB, out tiles = mt
+    // skinny transposed over a full matrix: M = K* (np x mp), k tiles = NB, out tiles = mt;
+    // 32 columns of [gamma, G] at a time
+    for (int c0 = 0; c0 < P; c0 += SK_PMAX) {
+      const int pc = std::min(SK_PMAX, P - c0);
       const int nch = (c->NB + SK_CH - 1) / SK_CH;
-      const size_t needp = (size_t)nch * mp * P;
+      const size_t needp = (size_t)nch * mp * pc;
       if (needp > c->skp_cap) {
         CHK(dalloc(c, &c->dskp, needp));
         c->skp_cap = needp;
       }
       SkinnyArgs a;
-      a.M = c->dW1; a.ldm = np; a.R = c->dWa; a.ldr = np; a.part = c->dskp; a.ldp = mp;
-      a.pstride = mp * P; a.P = P; a.ntr = c->NB; a.lower = 0; a.nit = mt; a.abort_flag = nullptr;
-      const int pm = pmax_bucket(P);
+      a.M = c->dW1; a.ldm = np; a.R = c->dWa + (long long)c0 * np; a.ldr = np; a.part = c->dskp; a.ldp = mp;
+      a.pstride = mp * pc; a.P = pc; a.ntr = c->NB; a.lower = 0; a.nit = mt; a.abort_flag = nullptr;
+      const int pm = pmax_bucket(pc);
       dim3 grid(mt * nch);
       if (c->skinny_valu) {
         if (pm == 8) hipLaunchKernelGGL(k_trmm_skinny_t<8>, grid, dim3(256), 0, c->stream, a);
         else if (pm == 16) hipLaunchKernelGGL(k_trmm_skinny_t<16>, grid, dim3(256), 0, c->stream, a);
         else hipLaunchKernelGGL(k_trmm_skinny_t<32>, grid, dim3(256), 0, c->stream, a);
-      } else if (P <= 16) {
+      } else if (pc <= 16) {
         hipLaunchKernelGGL((k_skinny_mfma<16, true>), grid, dim3(256), 0, c->stream, a);
       } else {
         hipLaunchKernelGGL((k_skinny_mfma<32, true>), grid, dim3(256), 0, c->stream, a);
       }
       HIPCHK(c, hipGetLastError());
-      const long long tot = mp * P;
+      const long long tot = mp * pc;
       hipLaunchKernelGGL(k_reduce_chunks, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
-                         c->dskp, (long long)(mp * P), dY, mp, P, (int)mp, c->NB, 2, nullptr);
+                         c->dskp, (long long)(mp * pc), dY + (long long)c0 * mp, mp, pc, (int)mp, c->NB, 2,
+                         nullptr);
       HIPCHK(c, hipGetLastError());
     }
     // V = L^-1 K*   (np x mp), X lower-triangular -> kend = (ti+1)*128
@@ -1472,7 +1527,8 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
                          c->stream, c->dX32, np, K32, np, V32, np, c->NB, (int)np, 1);
       HIPCHK(c, hipGetLastError());
     } else {
-      std::vector<GemmProb> pv = {mkprob(c->tr.B, np, c->dW1, np, c->dW2, np, c->NB, mt, (int)np,
+      double* vdst = big ? c->dVall + s0 * np : c->dW2;
+      std::vector<GemmProb> pv = {mkprob(c->tr.B, np, c->dW1, np, vdst, np, c->NB, mt, (int)np,
                                          G_KEND_TI, 1.0, 0.0)};
       pv[0].tile_begin = 0;
       pv[0].ntiles = c->NB * mt;
@@ -1497,6 +1553,14 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
         Tt[s * q + o] = acc;
       }
     }
+    if (big) {
+      // keep this chunk's scaled points and T Kq^-T for the blocks formed after the loop
+      HIPCHK(c, hipMemcpyAsync(c->dXall + s0 * d, c->dXsw, (size_t)mp * d * sizeof(double), hipMemcpyDeviceToDevice,
+                               c->stream));
+      for (long long s = 0; s < mc; ++s)
+        for (int o = 0; o < q; ++o) Th[(s0 + s) + (size_t)o * mtot] = Tt[s * q + o];
+      continue;
+    }
     if (!full_var) {
       CHK(ensure_small(c, (size_t)mp * P + mp + 64));
       double* dn = c->dsmall + (size_t)mp * P;
@@ -1517,7 +1581,6 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
     } else {
       // C = s2 * (A** - V^T V + Tt Tt^T), all tiles (full symmetric)
       const size_t needc = (size_t)mp * mp;
-      const int kq = ((q + 15) / 16) * 16;
       if (needc + (size_t)mp * kq > c->w3_cap) {
         CHK(dalloc(c, &c->dW3, needc + (size_t)mp * kq));
         c->w3_cap = needc + (size_t)mp * kq;
@@ -1564,6 +1627,60 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
       HIPCHK(c, hipMemcpy(hc.data(), dC, hc.size() * sizeof(double), hipMemcpyDeviceToHost));
       for (long long j = 0; j < mc; ++j)
         std::memcpy(var_out + j * m, hc.data() + (size_t)j * mp, (size_t)mc * sizeof(double));
+    }
+  }
+  if (big) {
+    // blocks (a, b), b >= a, of C = s2 (A** - V^T V + T T^T) over chunk pairs, each formed
+    // in dW3 and written to the host at rows a, columns b (and mirrored)
+    HIPCHK(c, hipMemcpyAsync(c->dTall, Th.data(), Th.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const size_t needc = (size_t)CHUNK * CHUNK;
+    if (needc > c->w3_cap) {
+      CHK(dalloc(c, &c->dW3, needc));
+      c->w3_cap = needc;
+    }
+    double* dC = c->dW3;
+    std::vector<double> hc;
+    for (long long a0 = 0; a0 < m; a0 += CHUNK) {
+      const long long mca = std::min(CHUNK, m - a0), mpa = ((mca + TILE - 1) / TILE) * TILE;
+      const int mta = (int)(mpa / TILE);
+      for (long long b0 = a0; b0 < m; b0 += CHUNK) {
+        const long long mcb = std::min(CHUNK, m - b0), mpb = ((mcb + TILE - 1) / TILE) * TILE;
+        const int mtb = (int)(mpb / TILE);
+        const bool dg = a0 == b0;
+        PairArgs a;   // A** block: the diagonal block as the single-chunk path, else rectangular
+        a.xr = c->dXall + a0 * d; a.xc = c->dXall + b0 * d; a.out = dC; a.ld = mpa; a.d = d;
+        a.nr_valid = (int)mca; a.nc_valid = (int)mcb; a.mt = mta; a.nt = mtb; a.mode = dg ? (1 | 2 | 4) : 0;
+        a.s2 = s2; a.coff = coff; a.cdiag = cdiag; a.rscale = 0.0; a.r = nullptr;
+        if (dg && rnew) {
+          CHK(grow(c, &c->dRn, &c->rn_cap, (size_t)mpa));
+          HIPCHK(c, hipMemcpy(c->dRn, rnew + a0, (size_t)mca * sizeof(double), hipMemcpyHostToDevice));
+          a.r = c->dRn;
+          a.rscale = s2 * rnew_scale;
+        }
+        CHK(launch_pairs(c, a, dg ? mta * (mta + 1) / 2 : mta * mtb));
+        std::vector<GemmProb> p2 = {
+            mkprob(c->dVall + a0 * np, np, c->dVall + b0 * np, np, dC, mpa, mta, mtb, (int)np, 0, -s2, 1.0),
+            mkprob(c->dTall + a0, mtot, c->dTall + b0, mtot, dC, mpa, mta, mtb, kq, 0, s2, 1.0)};
+        p2[0].tile_begin = 0; p2[0].ntiles = mta * mtb;
+        p2[1].tile_begin = 0; p2[1].ntiles = mta * mtb;
+        HIPCHK(c, hipMemcpyAsync(c->dprobs + ADHOC_DESC_BASE + 1, p2.data(), 2 * sizeof(GemmProb),
+                                 hipMemcpyHostToDevice, c->stream));
+        Launch L1{2, ADHOC_DESC_BASE + 1, 1, mta * mtb, 0.0};
+        CHK(launch_gemm_range(c, L1));
+        Launch L2{0, ADHOC_DESC_BASE + 2, 1, mta * mtb, 0.0};
+        CHK(launch_gemm_range(c, L2));
+        hc.resize((size_t)mpa * mpb);
+        HIPCHK(c, hipMemcpyAsync(hc.data(), dC, hc.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        // dC(i, j) = C(a0 + i, b0 + j), column-major; var_out row-major m x m
+        for (long long j = 0; j < mcb; ++j)
+          for (long long i = 0; i < mca; ++i) {
+            const double v = hc[(size_t)i + (size_t)j * mpa];
+            var_out[(a0 + i) * m + (b0 + j)] = v;
+            if (!dg) var_out[(b0 + j) * m + (a0 + i)] = v;
+          }
+      }
     }
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1650,7 +1767,7 @@ int gpe_kernel_var(gpe_ctx* c, int32_t kernel, const double* delta, int32_t d, d
                    int32_t predict, int64_t m, const double* X, const double* r, double r_scale,
                    double* A_out) {
   if (!c) return GPE_ERR_ARG;
-  if (!delta || !X || !A_out || m <= 0 || d <= 0 || d > 32) return fail(c, GPE_ERR_ARG, "bad kernel_var args");
+  if (!delta || !X || !A_out || m <= 0 || d <= 0 || d > GPE_MAX_DIMS) return fail(c, GPE_ERR_ARG, "bad kernel_var args");
   HIPCHK(c, hipSetDevice(c->device));
   const long long mp = ((m + TILE - 1) / TILE) * TILE;
   const int mt = (int)(mp / TILE);
@@ -1702,7 +1819,7 @@ int gpe_kernel_var(gpe_ctx* c, int32_t kernel, const double* delta, int32_t d, d
 int gpe_kernel_grad(gpe_ctx* c, const double* delta, int32_t d, int64_t m, const double* X,
                     const double* col, double col_scale, double pre, double* G_out) {
   if (!c) return GPE_ERR_ARG;
-  if (!delta || !X || !G_out || m <= 0 || d <= 0 || d > 32) return fail(c, GPE_ERR_ARG, "bad kernel_grad args");
+  if (!delta || !X || !G_out || m <= 0 || d <= 0 || d > GPE_MAX_DIMS) return fail(c, GPE_ERR_ARG, "bad kernel_grad args");
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   const long long mp = ((m + TILE - 1) / TILE) * TILE;
@@ -1814,7 +1931,7 @@ int gpe_lhc_maximin(gpe_ctx* c, int32_t N, int64_t n, int32_t dim, const double*
 int gpe_kernel_covar(gpe_ctx* c, int32_t kernel, const double* delta, int32_t d, double nu,
                      int64_t n, const double* XT, int64_t m, const double* XV, double* C_out) {
   if (!c) return GPE_ERR_ARG;
-  if (!delta || !XT || !XV || !C_out || n <= 0 || m <= 0 || d <= 0 || d > 32)
+  if (!delta || !XT || !XV || !C_out || n <= 0 || m <= 0 || d <= 0 || d > GPE_MAX_DIMS)
     return fail(c, GPE_ERR_ARG, "bad kernel_covar args");
   HIPCHK(c, hipSetDevice(c->device));
   // compute C^T (m x n, column-major == n x m row-major)

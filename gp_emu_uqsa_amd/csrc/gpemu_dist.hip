@@ -114,6 +114,63 @@ __global__ void __launch_bounds__(256) k_dist_kbuild(DistPairArgs a) {
   }
 }
 
+// k_dist_kbuild for d > 32: coordinates staged through LDS 32 dimensions at a time
+// (as k_pairs_wide; the same sums in the same order)
+__global__ void __launch_bounds__(256) k_dist_kbuild_wide(DistPairArgs a) {
+  __shared__ double xs_col[TILE * PW_CH];
+  const int li = blockIdx.x % a.nloc, tj = blockIdx.x / a.nloc;
+  const int gt = li * a.nranks + a.rank;
+  if (tj > gt) return;
+  const int tid = threadIdx.x, r = tid & (TILE - 1), h = tid >> 7;
+  double* out = a.out + (long long)li * TILE + (long long)tj * TILE * a.ld;
+  if (gt == a.NB) {
+    for (int c = h; c < TILE; c += 2) {
+      const int gj = tj * TILE + c;
+      const double v = (tj < a.NB && r < a.Pc) ? a.F[gj + (long long)r * a.ldF] : 0.0;
+      out[r + (long long)c * a.ld] = v;
+    }
+    return;
+  }
+  const int d = a.d;
+  const int gi = gt * TILE + r;
+  double s[TILE / 2];
+#pragma unroll
+  for (int u = 0; u < TILE / 2; ++u) s[u] = 0.0;
+  for (int k0 = 0; k0 < d; k0 += PW_CH) {
+    __syncthreads();
+    for (int e = tid; e < TILE * PW_CH; e += 256) {
+      const int c = e / PW_CH, k = e - c * PW_CH;
+      xs_col[e] = k0 + k < d ? a.xw[(long long)(tj * TILE + c) * d + k0 + k] : 0.0;
+    }
+    double xi[PW_CH];
+#pragma unroll
+    for (int k = 0; k < PW_CH; ++k) xi[k] = (k0 + k < d) ? a.xw[(long long)gi * d + k0 + k] : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < TILE / 2; ++u) {
+      const int c = h + 2 * u;
+#pragma unroll
+      for (int k = 0; k < PW_CH; ++k) {
+        const double df = xi[k] - xs_col[c * PW_CH + k];
+        s[u] = fma(df, df, s[u]);
+      }
+    }
+  }
+  const double pre = a.s2 * a.coff;
+  const bool row_pad = gi >= a.n_valid;
+  double vdiag = a.s2 * a.cdiag;
+  if (a.r && gt == tj && !row_pad) vdiag += a.rscale * a.r[gi];
+#pragma unroll
+  for (int u = 0; u < TILE / 2; ++u) {
+    const int c = h + 2 * u;
+    const int gj = tj * TILE + c;
+    double v = pre * exp(-s[u]);
+    const bool diag = gi == gj;
+    v = (row_pad || gj >= a.n_valid) ? (diag ? 1.0 : 0.0) : (diag ? vdiag : v);
+    out[r + (long long)c * a.ld] = v;
+  }
+}
+
 // panel tiles (local rows li0 .. li0+cnt-1, column k) -> dst, 128x128 column-major each
 __global__ void __launch_bounds__(256) k_dist_pack(const double* Aloc, long long ld, int li0, int k,
                                                    double* dst) {
@@ -759,7 +816,8 @@ int kbuild(gpe_dist* h, int kernel, double nu, double s2, double rscale) {
     else if (h->d <= 10) hipLaunchKernelGGL(k_dist_kbuild<10>, grid, dim3(256), 0, h->stream, a);
     else if (h->d <= 16) hipLaunchKernelGGL(k_dist_kbuild<16>, grid, dim3(256), 0, h->stream, a);
     else if (h->d <= 20) hipLaunchKernelGGL(k_dist_kbuild<20>, grid, dim3(256), 0, h->stream, a);
-    else hipLaunchKernelGGL(k_dist_kbuild<32>, grid, dim3(256), 0, h->stream, a);
+    else if (h->d <= 32) hipLaunchKernelGGL(k_dist_kbuild<32>, grid, dim3(256), 0, h->stream, a);
+    else hipLaunchKernelGGL(k_dist_kbuild_wide, grid, dim3(256), 0, h->stream, a);
     DCHK_HIP(h, hipGetLastError());
   }
   return GPE_OK;
@@ -806,7 +864,9 @@ void contract_launch(gpe_dist* h, const double* slab, long long lds, long long r
   const long long np = h->n_pad;
   const dim3 g(nblk);
   const int nv = (int)h->n;
-  if (d == 10 && Pc <= 13)
+  if (d > 32 || Pc > 33)
+    hipLaunchKernelGGL(k_contract_wide, g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0, rdiag);
+  else if (d == 10 && Pc <= 13)
     hipLaunchKernelGGL((k_contract<10, 13>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0, rdiag);
   else if (d == 20 && Pc <= 21)   // BASELINE configs[3]
     hipLaunchKernelGGL((k_contract<20, 21>), g, dim3(256), 0, h->stream, slab, lds, h->dXw, d, wpart, np, q1, nv, h->cpart, h->dinfo, blk0, row0, rdiag);
@@ -906,7 +966,7 @@ const char* gpe_dist_last_error(gpe_dist* h) { return h ? h->err.c_str() : "null
 int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double* X, const double* f,
                       const double* H, const double* r) {
   if (!h) return GPE_ERR_ARG;
-  if (n <= 0 || d <= 0 || d > 32 || q < 0 || q + 1 > 128 || !X || !f || (q > 0 && !H))
+  if (n <= 0 || d <= 0 || d > GPE_MAX_DIMS || q < 0 || q + 1 > GPE_MAX_COLS || !X || !f || (q > 0 && !H))
     return dfail(h, GPE_ERR_ARG, "bad shapes");
   DCHK_HIP(h, hipSetDevice(h->device));
   DCHK_HIP(h, hipStreamSynchronize(h->stream));
@@ -948,7 +1008,7 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
     std::memcpy(h->hpin, r, (size_t)n * sizeof(double));
     DCHK_HIP(h, hipMemcpy(h->dr, h->hpin, (size_t)np * sizeof(double), hipMemcpyHostToDevice));
   }
-  DCHK(dalloc(h, &h->dinvdelta, 32, &h->shared_bytes));
+  DCHK(dalloc(h, &h->dinvdelta, GPE_MAX_DIMS, &h->shared_bytes));
   // local ranks and their sweep buffers
   build_groups(h);
   h->T0 = nloc_of(h->NB, h->P, 0);
@@ -1093,8 +1153,12 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
       Rank& R = h->ranks[s];
       DCHK_HIP(h, hipMemsetAsync(R.wpart, 0, (size_t)np * TILE * sizeof(double), h->stream));
       if (R.nlx == 0) continue;
-      hipLaunchKernelGGL(k_apply_small, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, h->stream, R.dZ, np, Pc,
-                         h->dT2, Pc, R.dR2, np, (int)np, h->dinfo);
+      if (Pc <= SK_PMAX)
+        hipLaunchKernelGGL(k_apply_small, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, h->stream, R.dZ, np, Pc,
+                           h->dT2, Pc, R.dR2, np, (int)np, h->dinfo);
+      else
+        hipLaunchKernelGGL(k_apply_big, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, h->stream, R.dZ, np, Pc,
+                           h->dT2, Pc, R.dR2, np, (int)np, h->dinfo);
       DCHK_HIP(h, hipGetLastError());
       const long long e = (long long)R.nlx * TILE;
       hipLaunchKernelGGL(k_dist_rows, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, h->stream, R.dR2, np, Pc,

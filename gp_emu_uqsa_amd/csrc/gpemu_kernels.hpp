@@ -111,6 +111,70 @@ static __global__ void __launch_bounds__(256) k_pairs(PairArgs a) {
   }
 }
 
+// k_pairs for any d (the reference's kernel takes any number of inputs,
+// _emulatorkernels.py:39-50): coordinates staged through LDS 32 dimensions at a
+// time, each thread keeping the running squared distances of its 64 columns.  The
+// sum over k = 0..d-1 is taken in the same order with the same fma as k_pairs.
+constexpr int PW_CH = 32;
+static __global__ void __launch_bounds__(256) k_pairs_wide(PairArgs a) {
+  __shared__ double xs_col[TILE * PW_CH];
+  int ti, tj;
+  if (a.mode & 1) tri_decode(blockIdx.x, ti, tj);
+  else { ti = blockIdx.x % a.mt; tj = blockIdx.x / a.mt; }
+  const int tid = threadIdx.x, h = tid >> 7;
+  const int d = a.d;
+  const int r = tid & (TILE - 1);
+  const int gi = ti * TILE + r;
+  double s[TILE / 2];
+#pragma unroll
+  for (int u = 0; u < TILE / 2; ++u) s[u] = 0.0;
+  for (int k0 = 0; k0 < d; k0 += PW_CH) {
+    __syncthreads();
+    for (int e = tid; e < TILE * PW_CH; e += 256) {
+      const int c = e / PW_CH, k = e - c * PW_CH;
+      xs_col[e] = k0 + k < d ? a.xc[(long long)(tj * TILE + c) * d + k0 + k] : 0.0;
+    }
+    double xi[PW_CH];
+#pragma unroll
+    for (int k = 0; k < PW_CH; ++k) xi[k] = (k0 + k < d) ? a.xr[(long long)gi * d + k0 + k] : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < TILE / 2; ++u) {
+      const int c = h + 2 * u;
+#pragma unroll
+      for (int k = 0; k < PW_CH; ++k) {
+        const double df = xi[k] - xs_col[c * PW_CH + k];
+        s[u] = fma(df, df, s[u]);
+      }
+    }
+  }
+  const double pre = a.s2 * a.coff;
+  const bool train = (a.mode & 2) != 0;
+  const bool zero_diag = (a.mode & 8) != 0;
+  const bool row_pad = gi >= a.nr_valid;
+  double vdiag = a.s2 * a.cdiag;
+  if (train && a.r && ti == tj && !row_pad) vdiag += a.rscale * a.r[gi];
+  const double fi = a.fcol ? a.fcol[gi] : 0.0;
+  double* out = a.out + gi;
+#pragma unroll
+  for (int u = 0; u < TILE / 2; ++u) {
+    const int c = h + 2 * u;
+    const int gj = tj * TILE + c;
+    double v = pre * exp(-s[u]);
+    if (a.fcol) {
+      const double df = (fi - a.fcol[gj]) * a.fscale;
+      v *= df * df;
+    }
+    const bool pad = row_pad || gj >= a.nc_valid;
+    const bool diag = gi == gj;
+    if (train) v = pad ? (diag ? 1.0 : 0.0) : (diag ? vdiag : v);
+    else v = pad ? 0.0 : v;
+    if (zero_diag && diag) v = 0.0;
+    out[(long long)gj * a.ld] = v;
+    if ((a.mode & 4) && ti != tj) a.out[(long long)gj + (long long)gi * a.ld] = v;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // diagonal-block Cholesky + inverse of one 128x128 tile, recursive and MFMA-based.
 // In : A tile (kt,kt) lower part.  Out: L_kk (lower, in place), Dinv_kk = L_kk^-1
@@ -1406,25 +1470,57 @@ static __global__ void k_reduce_chunks(const double* part, long long pstride, do
 }
 
 // ---------------------------------------------------------------------------
-// Gram: part[blk][a*P+b] = sum_{rows in blk} Z(row,a) Z(row,b); rows 256 per block
+// Gram: part[blk][a + b P] = sum_{rows in blk} Z(row,a) Z(row,b); rows 256 per block.
+// Any P: blockIdx.y enumerates pairs of 32-column chunks (ca <= cb); a pair of
+// different chunks writes its block and the mirror.  With P <= 32 there is one pair
+// and the sums are those of the single-chunk form.
 // ---------------------------------------------------------------------------
 static __global__ void __launch_bounds__(256) k_gram(const double* Z, long long ldz, int P, int nrows,
                                               double* part, const int* abort_flag) {
-  __shared__ double zs[256 * (SK_PMAX + 1)];
+  __shared__ double za[256 * (SK_PMAX + 1)];
+  __shared__ double zb[256 * (SK_PMAX + 1)];
   if (abort_flag && *abort_flag) return;
   const int tid = threadIdx.x;
   const int r0 = blockIdx.x * 256;
-  for (int e = tid; e < 256 * P; e += 256) {
+  const int nch = (P + SK_PMAX - 1) / SK_PMAX;
+  int pi = blockIdx.y, ca = 0;
+  while (pi >= nch - ca) { pi -= nch - ca; ++ca; }
+  const int cb = ca + pi;
+  const int a0 = ca * SK_PMAX, pa = min(SK_PMAX, P - a0);
+  const int b0 = cb * SK_PMAX, pb = min(SK_PMAX, P - b0);
+  for (int e = tid; e < 256 * pa; e += 256) {
     int rr = e & 255, p = e >> 8;
     int row = r0 + rr;
-    zs[rr * (SK_PMAX + 1) + p] = (row < nrows) ? Z[row + (long long)p * ldz] : 0.0;
+    za[rr * (SK_PMAX + 1) + p] = (row < nrows) ? Z[row + (long long)(a0 + p) * ldz] : 0.0;
   }
+  if (cb != ca)
+    for (int e = tid; e < 256 * pb; e += 256) {
+      int rr = e & 255, p = e >> 8;
+      int row = r0 + rr;
+      zb[rr * (SK_PMAX + 1) + p] = (row < nrows) ? Z[row + (long long)(b0 + p) * ldz] : 0.0;
+    }
   __syncthreads();
-  for (int e = tid; e < P * P; e += 256) {
-    int x = e % P, y = e / P;
+  const double* zy = cb != ca ? zb : za;
+  double* out = part + (long long)blockIdx.x * P * P;
+  for (int e = tid; e < pa * pb; e += 256) {
+    int x = e % pa, y = e / pa;
     double s = 0.0;
-    for (int rr = 0; rr < 256; ++rr) s = fma(zs[rr * (SK_PMAX + 1) + x], zs[rr * (SK_PMAX + 1) + y], s);
-    part[(long long)blockIdx.x * P * P + e] = s;
+    for (int rr = 0; rr < 256; ++rr) s = fma(za[rr * (SK_PMAX + 1) + x], zy[rr * (SK_PMAX + 1) + y], s);
+    out[(a0 + x) + (long long)(b0 + y) * P] = s;
+    if (cb != ca) out[(b0 + y) + (long long)(a0 + x) * P] = s;
+  }
+}
+
+// Y(i, :) = Z(i, :) x T for any P (k_apply_small holds a row of Z in registers, P <= 32)
+static __global__ void k_apply_big(const double* Z, long long ldz, int P, const double* T, int Pout, double* Y,
+                                   long long ldy, int nrows, const int* abort_flag) {
+  if (abort_flag && *abort_flag) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nrows) return;
+  for (int o = 0; o < Pout; ++o) {
+    double s = 0.0;
+    for (int p = 0; p < P; ++p) s = fma(Z[i + (long long)p * ldz], T[p + o * P], s);
+    Y[i + (long long)o * ldy] = s;
   }
 }
 
@@ -1587,6 +1683,138 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
   }
 }
 
+// k_contract for any d and q (d > 32 or q + 1 > 33): the same sums, with the
+// coordinates and the columns of Wa staged through LDS 32 at a time.  Per pass over
+// a chunk of 32 per-dimension accumulators, each thread walks its 64 columns in four
+// groups of 16 (distances, M(i,j), then M E times the chunk's squared differences);
+// passes beyond the first recompute E (d / 32 passes in all).
+constexpr int CW_CH = 32;
+static __global__ void __launch_bounds__(256) k_contract_wide(const double* Ainv, long long lda,
+                                                             const double* xw, int d,
+                                                             const double* Wa, long long ldw, int q1,
+                                                             int n_valid, double* part,
+                                                             const int* abort_flag, int blk0,
+                                                             long long row0, const double* rdiag) {
+  __shared__ double st[TILE * CW_CH];
+  __shared__ double red[4 * CW_CH];
+  if (abort_flag && *abort_flag) return;
+  int ti, tj;
+  const int blk = blk0 + (int)blockIdx.x;
+  tri_decode(blk, ti, tj);
+  const int tid = threadIdx.x, h = tid >> 7, lane = tid & 63, wave = tid >> 6;
+  const int r = tid & (TILE - 1);
+  const int gi = ti * TILE + r;
+  const bool rv = gi < n_valid;
+  const int cend = rv ? min((ti == tj) ? r + 1 : TILE, n_valid - tj * TILE) : 0;
+  const double ri = (rdiag && rv && ti == tj) ? rdiag[gi] : 0.0;
+  const int nv = d + 3;
+  double accE = 0.0, accT = 0.0, accR = 0.0;
+  // wave sum of v into red[wave][k]; the caller adds the four waves in fixed order
+  auto block_sum = [&](double v, int k) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if (lane == 0) red[wave * CW_CH + k] = v;
+  };
+  for (int a0 = 0; a0 < d; a0 += CW_CH) {
+    double acc[CW_CH];
+#pragma unroll
+    for (int k = 0; k < CW_CH; ++k) acc[k] = 0.0;
+    for (int cg = 0; cg < 4; ++cg) {
+      double sd[16], m[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int c = h + 2 * (cg * 16 + u);
+        sd[u] = 0.0;
+        m[u] = (c < cend) ? Ainv[(gi - row0) + (long long)(tj * TILE + c) * lda] : 0.0;
+      }
+      for (int k0 = 0; k0 < d; k0 += CW_CH) {   // squared distances over every dimension
+        __syncthreads();
+        for (int e = tid; e < TILE * CW_CH; e += 256) {
+          const int c = e / CW_CH, k = e - c * CW_CH;
+          st[e] = k0 + k < d ? xw[(long long)(tj * TILE + c) * d + k0 + k] : 0.0;
+        }
+        double xi[CW_CH];
+#pragma unroll
+        for (int k = 0; k < CW_CH; ++k) xi[k] = (k0 + k < d) ? xw[(long long)gi * d + k0 + k] : 0.0;
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int c = h + 2 * (cg * 16 + u);
+#pragma unroll
+          for (int k = 0; k < CW_CH; ++k) {
+            const double df = xi[k] - st[c * CW_CH + k];
+            sd[u] += df * df;
+          }
+        }
+      }
+      for (int p0 = 0; p0 < q1; p0 += CW_CH) {  // M(i,j) = A^-1(i,j) - sum_p Wa(i,p) Wa(j,p)
+        __syncthreads();
+        for (int e = tid; e < TILE * CW_CH; e += 256) {
+          const int c = e / CW_CH, k = e - c * CW_CH;
+          st[e] = p0 + k < q1 ? Wa[(long long)(tj * TILE + c) + (long long)(p0 + k) * ldw] : 0.0;
+        }
+        double wi[CW_CH];
+#pragma unroll
+        for (int k = 0; k < CW_CH; ++k) wi[k] = (p0 + k < q1) ? Wa[gi + (long long)(p0 + k) * ldw] : 0.0;
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int c = h + 2 * (cg * 16 + u);
+#pragma unroll
+          for (int k = 0; k < CW_CH; ++k) m[u] = fma(-wi[k], st[c * CW_CH + k], m[u]);
+        }
+      }
+      // M E off the diagonal; trace terms once (first pass)
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int c = h + 2 * (cg * 16 + u);
+        const bool valid = c < cend, dg = tj * TILE + c == gi;
+        if (a0 == 0) {
+          accT += (valid && dg) ? m[u] : 0.0;
+          accR += (valid && dg) ? m[u] * ri : 0.0;
+        }
+        sd[u] = (valid && !dg) ? m[u] * exp(-sd[u]) : 0.0;   // now M E
+        if (a0 == 0) accE += sd[u];
+      }
+      // this pass's dimensions: acc_k += M E (x_ik - x_jk)^2
+      __syncthreads();
+      for (int e = tid; e < TILE * CW_CH; e += 256) {
+        const int c = e / CW_CH, k = e - c * CW_CH;
+        st[e] = a0 + k < d ? xw[(long long)(tj * TILE + c) * d + a0 + k] : 0.0;
+      }
+      double xi[CW_CH];
+#pragma unroll
+      for (int k = 0; k < CW_CH; ++k) xi[k] = (a0 + k < d) ? xw[(long long)gi * d + a0 + k] : 0.0;
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int c = h + 2 * (cg * 16 + u);
+#pragma unroll
+        for (int k = 0; k < CW_CH; ++k) {
+          const double df = xi[k] - st[c * CW_CH + k];
+          acc[k] = fma(sd[u], df * df, acc[k]);
+        }
+      }
+    }
+    // this pass's per-dimension sums
+    const int kn = min(CW_CH, d - a0);
+#pragma unroll
+    for (int k = 0; k < CW_CH; ++k)
+      if (k < kn) block_sum(acc[k], k);
+    __syncthreads();
+    if (tid < kn)
+      part[(long long)blk * nv + a0 + tid] =
+          (red[tid] + red[CW_CH + tid]) + (red[2 * CW_CH + tid] + red[3 * CW_CH + tid]);
+    __syncthreads();
+  }
+  block_sum(accE, 0);
+  block_sum(accT, 1);
+  block_sum(accR, 2);
+  __syncthreads();
+  if (tid < 3)
+    part[(long long)blk * nv + d + tid] =
+        (red[tid] + red[CW_CH + tid]) + (red[2 * CW_CH + tid] + red[3 * CW_CH + tid]);
+}
+
 // ---------------------------------------------------------------------------
 // sensitivity pair sums (reference sensitivity/_sensitivityclasses.py:90-102 Rtt,
 // :599-626 P_prod / Pw): J Gaussian pair kernels on the raw training inputs x,
@@ -1596,6 +1824,9 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
 // grid (NB, J, CS): row block ti of 128 rows, column slice z of CS (each slice a
 // multiple of SP_CT columns), two threads per row split the slice's columns.
 // part[((ti*CS + z)*4 + wave) * ldp + j*(1+p*p)] = trace part, then the p*p quad part.
+// Z columns zc0 .. zc0 + pc (pc <= PMAX) per launch: V = K Z[:, zc0:] and quad(a, zc0 + b)
+// for every a < p; the host covers any p in such column chunks (the trace part is the
+// same in each).
 // ---------------------------------------------------------------------------
 constexpr int SP_CT = 64;   // columns staged in LDS per pass
 template <int DMAX, int PMAX>
@@ -1603,7 +1834,7 @@ static __global__ void __launch_bounds__(256) k_sense_pairs(const double* Ainv, 
                                                            int d, const double* w, const double* u,
                                                            long long ldu, const double* Z, long long ldz,
                                                            int p, int n_valid, int cslice, double* part,
-                                                           long long ldp) {
+                                                           long long ldp, int zc0, int pc) {
   __shared__ double xs[SP_CT * DMAX];
   __shared__ double zs[SP_CT * PMAX];
   __shared__ double us[SP_CT];
@@ -1629,9 +1860,9 @@ static __global__ void __launch_bounds__(256) k_sense_pairs(const double* Ainv, 
       const int c = e / DMAX, k = e - c * DMAX, g = c0 + c;
       xs[e] = (k < d && g < n_valid) ? x[(long long)g * d + k] : 0.0;
     }
-    for (int e = tid; e < SP_CT * PMAX; e += 256) {
+    for (int e = tid; e < SP_CT * PMAX; e += 256) {   // Z columns zc0 .. zc0 + pc
       const int c = e % SP_CT, k = e / SP_CT, g = c0 + c;
-      zs[c * PMAX + k] = (k < p && g < n_valid) ? Z[g + (long long)k * ldz] : 0.0;
+      zs[c * PMAX + k] = (k < pc && g < n_valid) ? Z[g + (long long)(zc0 + k) * ldz] : 0.0;
     }
     if (tid < SP_CT) us[tid] = (c0 + tid < n_valid) ? u[j * ldu + c0 + tid] : 0.0;
     __syncthreads();
@@ -1665,10 +1896,10 @@ static __global__ void __launch_bounds__(256) k_sense_pairs(const double* Ainv, 
     const double za = rv ? Z[gi + (long long)a * ldz] : 0.0;
 #pragma unroll
     for (int b = 0; b < PMAX; ++b) {
-      if (b < p) {
+      if (b < pc) {
         double s = za * v[b];
         for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
-        if (lane == 0) out[1 + a * p + b] = s;
+        if (lane == 0) out[1 + a * p + zc0 + b] = s;
       }
     }
   }

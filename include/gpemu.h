@@ -50,6 +50,13 @@ enum gpe_kernel { GPE_KERNEL_STD = 0, GPE_KERNEL_ALT_NUG = 1 };
 /* objective: _emulatoroptimise.py:412 (gp4ml) and :305 (mucm) */
 enum gpe_variant { GPE_GP4ML = 0, GPE_MUCM = 1 };
 
+/* Shape limits: input dimensions d and columns q + 1 of [f H] (the reference's
+ * linear mean has q = d + 1).  The kernels for d <= 32 and q + 1 <= 32 keep
+ * coordinates and basis rows in registers; beyond that they stage them through LDS
+ * in chunks of 32. */
+#define GPE_MAX_DIMS 128
+#define GPE_MAX_COLS 128
+
 typedef struct gpe_ctx gpe_ctx;
 
 int gpe_abi_version(void);
@@ -95,8 +102,9 @@ int gpe_beta(gpe_ctx* ctx, double* beta_out);
 
 /* Posterior at m points: replaces Posterior.make_covar/make_mean/make_var
  * (_emulatorclasses.py:607-631) with the resident factor.  Xs m x d, Hs m x q.
- * mean_out m; var_out m x m when full_var != 0 (m <= 16384), else its diagonal
- * (m values), streamed in chunks for any m.  sigma is par.sigma.
+ * mean_out m; var_out m x m (row-major) when full_var != 0, else its diagonal
+ * (m values); any m, in chunks of 16384 points (full: blocks of the m x m result
+ * formed on the device and written to the host).  sigma is par.sigma.
  * precision 64: everything in fp64.  precision 32 (diagonal only; SURVEY 8b/8d,
  * BASELINE config C5): the dominant product L^-1 K* (n^2 m flops) runs on fp32
  * MFMA from fp32 copies of L^-1 and K*; the mean and the q x q terms stay fp64. */

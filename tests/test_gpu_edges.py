@@ -43,15 +43,13 @@ def test_nan_hyperparameter_is_not_pd(ctx):
 
 
 def test_argument_limits(ctx):
+    """GPE_MAX_DIMS = GPE_MAX_COLS = 128 (include/gpemu.h); beyond: a loud error."""
     X, f, H = orc.synthetic_problem(100, 3, seed=1)
     ctx.set_data(X, f, H)
-    with pytest.raises(RuntimeError):      # more than 32 input dimensions
-        ctx.kernel_var(native.KERNEL_STD, np.ones(33), 1e-3, np.zeros((10, 33)))
-    ctx.factor(native.KERNEL_STD, np.ones(3), 1e-3, 1.0, 0.0)
-    beta = ctx.beta()
-    with pytest.raises(RuntimeError):      # full posterior covariance is limited to m <= 16384
-        xs = np.zeros((16385, 3))
-        ctx.posterior(xs, orc.linear_basis(xs), beta, 1.0, full_var=True)
+    with pytest.raises(RuntimeError):      # more than 128 input dimensions
+        ctx.kernel_var(native.KERNEL_STD, np.ones(129), 1e-3, np.zeros((10, 129)))
+    with pytest.raises(RuntimeError):      # more than 127 basis functions
+        ctx.set_data(X, f, np.ones((100, 128)))
 
 
 def test_noise_sample_single_point(ctx):
