@@ -99,11 +99,11 @@ def test_many_basis_columns(ctx):
     n, d = 500, 3
     X = rs.uniform(size=(n, d))
     f = np.sin(4 * X[:, 0]) + X[:, 1] ** 2 + 0.01 * rs.randn(n)
-    # 1, x, x^2, ..., a 40-column polynomial basis in the three inputs
-    cols = [np.ones(n)]
-    for p in range(1, 14):
+    # a 40-column basis in the three inputs: 1, x_k, sin / cos(pi j x_k), j = 1..6
+    cols = [np.ones(n)] + [X[:, k] for k in range(d)]
+    for j in range(1, 7):
         for k in range(d):
-            cols.append(X[:, k] ** p)
+            cols += [np.sin(np.pi * j * X[:, k]), np.cos(np.pi * j * X[:, k])]
     H = np.stack(cols, axis=1)
     assert H.shape[1] == 40
     hp = np.array([0.7, 0.8, 0.9, 1e-2, 1.1])
@@ -111,7 +111,7 @@ def test_many_basis_columns(ctx):
     llh, g, _ = ctx.objective(native.GP4ML, native.KERNEL_STD, hp)
     ref = orc.objective_ref(X, f, H, hp, orc.GP4ML, orc.STD, True)
     assert abs(llh - ref[0]) <= 1e-9 * abs(ref[0]), (llh, ref[0])
-    ok, err = _grad_ok(g, ref[1], 1e-6)   # Q = H^T A^-1 H of a degree-13 basis: cond ~1e12
+    ok, err = _grad_ok(g, ref[1])
     assert ok, err
 
 
