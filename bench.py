@@ -59,7 +59,7 @@ def parse(argv=None):
     ap.add_argument("--d", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-full", action="store_true",
-                    help="also time the CPU fast-mode objective at the full n (~2-3 min)")
+                    help="also time the op-for-op CPU reference at n=4096, 3 reps (~3 min)")
     ap.add_argument("--no-profile", action="store_true",
                     help="time without per-launch HIP events (roofline omitted)")
     ap.add_argument("--no-other-configs", dest="other_configs", action="store_false",
@@ -168,16 +168,20 @@ def _host_info():
 
 
 def cpu_baseline(d, n_full, full=False):
-    """The oracle's ref-mode (op-for-op restatement of the reference: pdist /
-    squareform, np.linalg.cholesky, LU-based np.linalg.solve for every triangular
-    solve, one dense dA per hyperparameter) MEASURED at n=4096 (BASELINE configs[1]),
-    3 repetitions, median, with the BLAS on every CPU this process may use (the
-    affinity mask, capped by the cgroup quota).  The n=16384 value is that time
-    scaled by (16384/4096)^3 -- the reference's evaluation is ~68 n^3 flops of
-    LAPACK LU solves -- and is labelled an estimate; the reference
-    itself measured 1230.7 s at n=16384 on 8 cores in the survey container.
-    fast_mode: the GPU's formulation on LAPACK (Cholesky, explicit inverse,
-    contraction), measured at n=4096, and with full=True at n=16384 itself."""
+    """CPU baseline on this host, with the BLAS on every CPU this process may use (the
+    affinity mask, capped by the cgroup quota), at the metric's size n_full:
+
+    * value (kind "port"): the reference's evaluation (_emulatoroptimise.py:412-493)
+      spends 90-94% of its time in np.linalg.solve with the n x n factor L (SURVEY.md
+      6): 24 calls with n right-hand sides (two per hyperparameter, :452-479) and 5
+      with at most q (:426-430), each an LU of L (dgesv).  One call of each kind is
+      timed at n_full and the evaluation is taken as 24 t_n + 5 t_q; it omits the
+      Cholesky, the 12 dense dA builds and the products, so the value is an UPPER bound
+      on the reference's evals/s.
+    * fast_mode: the oracle's objective_fast (the GPU's algorithm on LAPACK: Cholesky,
+      explicit inverse, contraction), one evaluation measured at n_full.
+    * full=True adds configs[1]: the op-for-op ref-mode objective at n=4096, 3 reps
+      (median), ~3 minutes."""
     from oracle import gp_oracle as orc
     host = _host_info()
     threads = host.get("affinity_cpus") or os.cpu_count() or 1
@@ -188,39 +192,50 @@ def cpu_baseline(d, n_full, full=False):
         limiter = threadpool_limits(limits=threads, user_api="blas")
     except Exception:
         limiter = None
+    out = {}
     try:
-        n2 = 4096
-        X, f, H = orc.synthetic_problem(n2, d, seed=0)
+        n, q = n_full, d + 1
+        rs = np.random.RandomState(0)
+        w = np.eye(512) + np.tril(rs.uniform(size=(512, 512))) / 512
+        np.linalg.solve(w, w)   # start the BLAS thread pool outside the timed calls
+        L = np.tril(rs.uniform(-1.0, 1.0, size=(n, n))) / n + np.eye(n)   # a lower-triangular factor
+        B = rs.uniform(-1.0, 1.0, size=(n, n))
+        t = time.perf_counter()
+        np.linalg.solve(L, B)
+        t_n = time.perf_counter() - t
+        del B
+        Bq = rs.uniform(-1.0, 1.0, size=(n, q))
+        t = time.perf_counter()
+        np.linalg.solve(L, Bq)
+        t_q = time.perf_counter() - t
+        del L, Bq
+        t_ref = 24 * t_n + 5 * t_q
+        out.update({"value": 1.0 / t_ref, "unit": "evals/s", "cores": int(threads), "kind": "port",
+                    "host": host,
+                    "sample": (f"reference op order at n={n}: np.linalg.solve(L, n x n) {t_n:.1f} s and "
+                               f"np.linalg.solve(L, n x {q}) {t_q:.1f} s measured once each on {threads} BLAS "
+                               f"threads; evaluation = 24 x + 5 x those = {t_ref:.0f} s (upper bound on "
+                               f"evals/s: Cholesky, dA builds and products omitted)")})
+        X, f, H = orc.synthetic_problem(n, d, seed=0)
         hp = eval_point(d, 0)
-        reps = []
-        for _ in range(3):
-            t = time.perf_counter()
-            orc.objective_ref(X, f, H, hp, orc.GP4ML, orc.STD, True)
-            reps.append(time.perf_counter() - t)
-        t2 = float(np.median(reps))
-        scale = (n_full / n2) ** 3
         t = time.perf_counter()
         orc.objective_fast(X, f, H, hp, orc.GP4ML, orc.STD, True)
-        tf2 = time.perf_counter() - t
-        fast = {"n4096_s_per_eval": tf2, "value_estimate": 1.0 / (tf2 * scale), "unit": "evals/s",
-                "sample": f"oracle fast-mode at n={n2}, {tf2:.2f} s/eval; n={n_full} estimate = x (n/{n2})^3"}
+        tf = time.perf_counter() - t
+        out["fast_mode"] = {"value": 1.0 / tf, "unit": "evals/s", "s_per_eval": tf,
+                            "sample": f"oracle objective_fast measured at n={n}, d={d}: {tf:.1f} s/eval"}
         if full:
-            Xf, ff, Hf = orc.synthetic_problem(n_full, d, seed=0)
-            t = time.perf_counter()
-            orc.objective_fast(Xf, ff, Hf, hp, orc.GP4ML, orc.STD, True)
-            tff = time.perf_counter() - t
-            fast.update({"value": 1.0 / tff, "measured_s_per_eval": tff,
-                         "sample": f"oracle fast-mode measured at n={n_full}: {tff:.1f} s/eval"})
+            X2, f2, H2 = orc.synthetic_problem(4096, d, seed=0)
+            reps = []
+            for _ in range(3):
+                t = time.perf_counter()
+                orc.objective_ref(X2, f2, H2, hp, orc.GP4ML, orc.STD, True)
+                reps.append(time.perf_counter() - t)
+            out["c2_n4096_ref_mode"] = {"s_per_eval_median": float(np.median(reps)), "reps_s": reps,
+                                        "evals_per_s": 1.0 / float(np.median(reps))}
     finally:
         if limiter is not None:
             limiter.unregister()
-    return {"value": 1.0 / (t2 * scale), "unit": "evals/s", "cores": int(threads), "kind": "port",
-            "host": host,
-            "c2_n4096": {"s_per_eval_median": t2, "reps_s": reps, "evals_per_s": 1.0 / t2},
-            "sample": (f"oracle ref-mode (reference op order, NumPy/OpenBLAS, {threads} threads) measured at "
-                       f"n={n2} d={d} (BASELINE configs[1]): 3 reps, median {t2:.2f} s/eval; n={n_full} value is "
-                       f"an ESTIMATE = x ({n_full}/{n2})^3 -> {t2 * scale:.0f} s/eval"),
-            "fast_mode": fast}
+    return out
 
 
 # ---------------------------------------------------------------------------
