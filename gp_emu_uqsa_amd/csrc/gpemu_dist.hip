@@ -28,6 +28,13 @@
 //   whole n x n), and rank 0 also carries the -W W^T term; W = [sqrt(c) alpha, W] is
 //   all-reduced (n x (q+1)) and then only the d+3 sums.
 //
+// Look-ahead: the chain of a column group (diagonal factor, Dinv broadcast, panels,
+// all-gather) runs on a critical stream; the group's trailing update is split into
+// the next group's columns (queued first) and the rest, on the compute stream.  The
+// next group's chain waits only for the first part, so its collectives overlap the
+// rest of the update.  The panel buffer (and the TRTRI's group rows, organised the
+// same way by rows) is double-buffered by group parity.
+//
 // Every logical rank owns all of its buffers (tile rows, Dinv, panel, all-gather
 // buffer, Gram, log-det, X rows, broadcast row, W, slab, sums).  The two transports
 // differ only in the collective call (coll_* below): RCCL on this process's one
@@ -233,14 +240,14 @@ struct Rank {              // one rank's buffers (one per process over RCCL, P i
   double* A = nullptr;     // nloc*128 x (NB+1)*128, column-major
   double* logdet = nullptr;   // NB+1 (own steps; all-reduced)
   double* dinv = nullptr;  // 128 x 128
-  double* panel = nullptr; // (NB+1)*128 x wmax*128: the current column group's gathered panels
+  double* panel = nullptr; // 2 x (NB+1)*128 x wmax*128: gathered panels of a group (by group parity)
   double* recv = nullptr;  // all-gather buffer, P segments of the largest panel
   double* gram = nullptr;  // Pc x Pc
   // gradient
   double* X = nullptr;     // L^-1 rows, ld as A, NB*128 columns
   double* xrow = nullptr;  // 128 x n_pad: X(k, 0:k+1), broadcast per step
-  double* xgrp = nullptr;  // wmax*128 x n_pad (ld wmax*128): the current group's X rows, zero
-                           // right of each row's diagonal tile within the group
+  double* xgrp = nullptr;  // 2 x wmax*128 x n_pad (ld wmax*128): a group's X rows (by group
+                           // parity), zero right of each row's diagonal tile within the group
   double* dZ = nullptr;    // n_pad x Pc: L^-1 [f H] (broadcast)
   double* dR2 = nullptr;   // n_pad x Pc
   double* r2loc = nullptr; // local rows of R2, 128 columns (zero beyond Pc)
@@ -262,7 +269,7 @@ struct SlabLaunch {        // one slab of a rank's partial of A^-1: GEMM + contr
 };
 
 constexpr int DIST_DESC_MAX = 1 << 20;
-constexpr size_t SLAB_DOUBLES = (size_t)1 << 27;   // 1 GiB per rank for the A^-1 slab
+constexpr size_t SLAB_DOUBLES = (size_t)1 << 26;   // 512 MiB per rank for the A^-1 slab
 
 int nloc_of(int NB, int P, int r) { return r <= NB ? (NB - r) / P + 1 : 0; }
 // first local row of rank r whose global tile row exceeds k
@@ -274,7 +281,9 @@ struct gpe_dist {
   int device = 0, P = 1, rank = 0;
   bool loop = true;
   ncclComm_t comm = nullptr;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // compute stream (bulk updates, everything outside the sweeps)
+  hipStream_t crit = nullptr;     // critical stream (a group's chain and its collectives)
+  hipStream_t cs = nullptr;       // the stream launches and collectives are issued on
   std::string err;
 
   long long n = 0, n_pad = 0;
@@ -294,12 +303,17 @@ struct gpe_dist {
   // columns}, first match wins, else 1 (GPEMU_DIST_W="8:160,4:80,2:40" style)
   std::vector<std::pair<int, int>> groups = {{8, 160}, {4, 80}, {2, 40}};
   std::vector<int> gstart;   // per step: first column of its group
+  std::vector<int> gid;      // per step: index of its group
+  std::vector<int> gs;       // group starts, then NB
   int wmax = 1;
+  size_t panel_sz = 0;       // doubles per panel buffer (two per rank)
+  std::vector<hipEvent_t> ev_chain, ev_next;   // per group (sweep or TRTRI, reused)
+  hipEvent_t ev_join = nullptr;
   int* dli0 = nullptr;       // [NB][P] first local row with global row > k
   int* dcnt = nullptr;       // [NB][P] panel tiles of rank r at step k
   GemmProb* dprobs = nullptr;
   unsigned* dtiles = nullptr;
-  std::vector<DLaunch> diag, panel_l, upd;   // per step
+  std::vector<DLaunch> diag, panel_l, upd_next, upd_rest;   // per step (updates: group ends)
   std::vector<int> maxT;                       // per step: max panel tiles over ranks
   int T0 = 0;                                  // the most panel tiles any rank contributes
   double* hpin = nullptr;
@@ -315,7 +329,7 @@ struct gpe_dist {
   int slab_rows = 1;                           // tile rows per slab of A^-1
   double* dT2 = nullptr;
   GemmProb* gprobs = nullptr;
-  std::vector<DLaunch> tri_p, tri_x, tri_u, wa_l;
+  std::vector<DLaunch> tri_p, tri_x, tri_un, tri_ur, wa_l;
   std::vector<std::vector<SlabLaunch>> slabs;  // per local rank
 };
 
@@ -418,12 +432,12 @@ int ensure_events(gpe_dist* h, size_t n) {
 
 int comm_begin(gpe_dist* h) {
   DCHK(ensure_events(h, (size_t)h->ev + 2));
-  DCHK_HIP(h, hipEventRecord(h->cev[h->ev], h->stream));
+  DCHK_HIP(h, hipEventRecord(h->cev[h->ev], h->cs));
   return GPE_OK;
 }
 
 int comm_end(gpe_dist* h) {
-  DCHK_HIP(h, hipEventRecord(h->cev[h->ev + 1], h->stream));
+  DCHK_HIP(h, hipEventRecord(h->cev[h->ev + 1], h->cs));
   h->ev += 2;
   return GPE_OK;
 }
@@ -433,12 +447,12 @@ int coll_bcast(gpe_dist* h, double* Rank::*buf, long long off, size_t count, int
   DCHK(comm_begin(h));
   if (!h->loop) {
     double* p = h->ranks[0].*buf + off;
-    DCHK_NCCL(h, ncclBroadcast(p, p, count, ncclDouble, root, h->comm, h->stream));
+    DCHK_NCCL(h, ncclBroadcast(p, p, count, ncclDouble, root, h->comm, h->cs));
   } else {
     const double* src = rank_slot(h, root)->*buf + off;
     for (Rank& R : h->ranks) {
       if (R.rank == root) continue;
-      DCHK_HIP(h, hipMemcpyAsync(R.*buf + off, src, count * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+      DCHK_HIP(h, hipMemcpyAsync(R.*buf + off, src, count * sizeof(double), hipMemcpyDeviceToDevice, h->cs));
     }
   }
   return comm_end(h);
@@ -449,14 +463,14 @@ int coll_allgather(gpe_dist* h, double* Rank::*buf, size_t seg) {
   DCHK(comm_begin(h));
   if (!h->loop) {
     double* p = h->ranks[0].*buf;
-    DCHK_NCCL(h, ncclAllGather(p + (size_t)h->rank * seg, p, seg, ncclDouble, h->comm, h->stream));
+    DCHK_NCCL(h, ncclAllGather(p + (size_t)h->rank * seg, p, seg, ncclDouble, h->comm, h->cs));
   } else {
     for (Rank& D : h->ranks)
       for (const Rank& S : h->ranks) {
         if (S.rank == D.rank) continue;
         const size_t o = (size_t)S.rank * seg;
         DCHK_HIP(h, hipMemcpyAsync(D.*buf + o, S.*buf + o, seg * sizeof(double), hipMemcpyDeviceToDevice,
-                                   h->stream));
+                                   h->cs));
       }
   }
   return comm_end(h);
@@ -467,18 +481,18 @@ int coll_allreduce_sum(gpe_dist* h, double* Rank::*buf, long long off, size_t co
   DCHK(comm_begin(h));
   if (!h->loop) {
     double* p = h->ranks[0].*buf + off;
-    DCHK_NCCL(h, ncclAllReduce(p, p, count, ncclDouble, ncclSum, h->comm, h->stream));
+    DCHK_NCCL(h, ncclAllReduce(p, p, count, ncclDouble, ncclSum, h->comm, h->cs));
   } else if (h->ranks.size() > 1) {
     double* acc = h->ranks[0].*buf + off;
     const unsigned g = (unsigned)std::min<size_t>((count + 255) / 256, 2048);
     for (size_t s = 1; s < h->ranks.size(); ++s) {
-      hipLaunchKernelGGL(k_dist_add, dim3(g), dim3(256), 0, h->stream, acc, h->ranks[s].*buf + off,
+      hipLaunchKernelGGL(k_dist_add, dim3(g), dim3(256), 0, h->cs, acc, h->ranks[s].*buf + off,
                          (long long)count);
       DCHK_HIP(h, hipGetLastError());
     }
     for (size_t s = 1; s < h->ranks.size(); ++s)
       DCHK_HIP(h, hipMemcpyAsync(h->ranks[s].*buf + off, acc, count * sizeof(double), hipMemcpyDeviceToDevice,
-                                 h->stream));
+                                 h->cs));
   }
   return comm_end(h);
 }
@@ -488,7 +502,7 @@ int coll_allreduce_sum(gpe_dist* h, double* Rank::*buf, long long off, size_t co
 int coll_info_max(gpe_dist* h) {
   if (h->loop) return GPE_OK;
   DCHK(comm_begin(h));
-  DCHK_NCCL(h, ncclAllReduce(h->dinfo, h->dinfo, 1, ncclInt32, ncclMax, h->comm, h->stream));
+  DCHK_NCCL(h, ncclAllReduce(h->dinfo, h->dinfo, 1, ncclInt32, ncclMax, h->comm, h->cs));
   return comm_end(h);
 }
 
@@ -499,22 +513,38 @@ int coll_info_max(gpe_dist* h) {
 void build_groups(gpe_dist* h) {
   const int NB = h->NB;
   h->gstart.assign(NB, 0);
+  h->gid.assign(NB, 0);
+  h->gs.clear();
   h->wmax = 1;
   for (int g = 0; g < NB;) {
     int w = 1;
     for (const auto& r : h->groups)
       if (NB - g > r.second) { w = r.first; break; }
     w = std::max(1, std::min(w, NB - g));
-    for (int k = g; k < g + w; ++k) h->gstart[k] = g;
+    for (int k = g; k < g + w; ++k) {
+      h->gstart[k] = g;
+      h->gid[k] = (int)h->gs.size();
+    }
+    h->gs.push_back(g);
     h->wmax = std::max(h->wmax, w);
     g += w;
   }
+  h->gs.push_back(NB);
 }
 
 int group_end(const gpe_dist* h, int k) {   // one past the last column of k's group
-  int e = k + 1;
-  while (e < h->NB && h->gstart[e] == h->gstart[k]) ++e;
-  return e;
+  return h->gs[h->gid[k] + 1];
+}
+
+// one past the last column of the group after k's (NB when k's group is the last)
+int next_group_end(const gpe_dist* h, int k) {
+  const int g = h->gid[k];
+  return g + 2 < (int)h->gs.size() ? h->gs[g + 2] : h->NB;
+}
+
+// the panel buffer of step k's group (double-buffered by group parity)
+double* panel_of(const gpe_dist* h, const Rank& R, int k) {
+  return R.panel + (size_t)(h->gid[k] & 1) * h->panel_sz;
 }
 
 // every per-step GEMM descriptor and tile list, for the current n and partition
@@ -525,7 +555,8 @@ int build_schedule(gpe_dist* h) {
   std::vector<unsigned> tiles;
   h->diag.assign(NB, DLaunch());
   h->panel_l.assign(NB, DLaunch());
-  h->upd.assign(NB, DLaunch());
+  h->upd_next.assign(NB, DLaunch());
+  h->upd_rest.assign(NB, DLaunch());
   h->maxT.assign(NB, 0);
   std::vector<int> li0((size_t)NB * P), cnt((size_t)NB * P);
   for (int k = 0; k < NB; ++k) {
@@ -562,7 +593,7 @@ int build_schedule(gpe_dist* h) {
         const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
         if (c == 0) continue;
         GemmProb p = dprob(R.A + (long long)a * TILE + (long long)gb * TILE * R.ld, R.ld,
-                           R.panel + (long long)k * TILE, ldp,
+                           panel_of(h, R, k) + (long long)k * TILE, ldp,
                            R.A + (long long)a * TILE + (long long)k * TILE * R.ld, R.ld, c, 1, Kp, 0, -1.0, 1.0);
         p.tile_begin = dl.tiles;
         p.ntiles = c;
@@ -588,28 +619,34 @@ int build_schedule(gpe_dist* h) {
     }
     h->panel_l[k] = pl;
     // the step closing a group: trailing update of each local rank's rows by the
-    // whole group, columns ge <= j <= i, K = 128 (ge - gb)
+    // whole group, columns ge <= j <= i, K = 128 (ge - gb), in two launches: the next
+    // group's columns ge <= j < ge2 (its chain waits for these only), then j >= ge2
     if (k + 1 != ge) continue;
-    DLaunch ul;
-    ul.first = (int)probs.size();
-    ul.list = (long long)tiles.size();
-    int pi = 0;
-    for (Rank& R : h->ranks) {
-      const int a = li0_of(k, P, R.rank);
-      if (a >= R.nloc) continue;
-      GemmProb p = dprob(R.A + (long long)gb * TILE * R.ld, R.ld, R.panel, ldp, R.A, R.ld,
-                         R.nloc, NB + 1, (ge - gb) * TILE, 0, -1.0, 1.0);
-      for (int li = a; li < R.nloc; ++li) {
-        const int gt = li * P + R.rank;
-        for (int j = ge; j <= gt; ++j) tiles.push_back(((unsigned)pi << 24) | ((unsigned)li << 12) | (unsigned)j);
+    const int ge2 = next_group_end(h, k);
+    for (int part = 0; part < 2; ++part) {
+      const int j0 = part == 0 ? ge : ge2, j1 = part == 0 ? ge2 : NB + 1;   // columns [j0, j1)
+      DLaunch ul;
+      ul.first = (int)probs.size();
+      ul.list = (long long)tiles.size();
+      int pi = 0;
+      for (Rank& R : h->ranks) {
+        const int a = li0_of(k, P, R.rank);
+        if (a >= R.nloc) continue;
+        GemmProb p = dprob(R.A + (long long)gb * TILE * R.ld, R.ld, panel_of(h, R, k), ldp, R.A, R.ld,
+                           R.nloc, NB + 1, (ge - gb) * TILE, 0, -1.0, 1.0);
+        for (int li = a; li < R.nloc; ++li) {
+          const int gt = li * P + R.rank;
+          for (int j = j0; j < j1 && j <= gt; ++j)
+            tiles.push_back(((unsigned)pi << 24) | ((unsigned)li << 12) | (unsigned)j);
+        }
+        probs.push_back(p);
+        ++pi;
+        ++ul.count;
       }
-      probs.push_back(p);
-      ++pi;
-      ++ul.count;
+      ul.tiles = (int)(tiles.size() - ul.list);
+      if (ul.tiles == 0) ul.count = 0;
+      (part == 0 ? h->upd_next : h->upd_rest)[k] = ul;
     }
-    ul.tiles = (int)(tiles.size() - ul.list);
-    if (ul.tiles == 0) ul.count = 0;
-    h->upd[k] = ul;
   }
   if ((int)probs.size() > DIST_DESC_MAX) return dfail(h, GPE_ERR_UNSUPPORTED, "distributed schedule too large");
   DCHK(dalloc(h, &h->dprobs, probs.size()));
@@ -631,9 +668,9 @@ int launch(gpe_dist* h, const DLaunch& L, const GemmProb* base = nullptr) {
   const GemmProb* pr = (base ? base : h->dprobs) + L.first;
   const dim3 g(L.tiles);
   switch (L.kind) {
-    case 1: hipLaunchKernelGGL((k_gemm<false, true>), g, dim3(256), lds, h->stream, pr, L.count, tl, h->dinfo); break;
-    case 2: hipLaunchKernelGGL((k_gemm<true, true>), g, dim3(256), lds, h->stream, pr, L.count, tl, h->dinfo); break;
-    default: hipLaunchKernelGGL((k_gemm<false, false>), g, dim3(256), lds, h->stream, pr, L.count, tl, h->dinfo); break;
+    case 1: hipLaunchKernelGGL((k_gemm<false, true>), g, dim3(256), lds, h->cs, pr, L.count, tl, h->dinfo); break;
+    case 2: hipLaunchKernelGGL((k_gemm<true, true>), g, dim3(256), lds, h->cs, pr, L.count, tl, h->dinfo); break;
+    default: hipLaunchKernelGGL((k_gemm<false, false>), g, dim3(256), lds, h->cs, pr, L.count, tl, h->dinfo); break;
   }
   DCHK_HIP(h, hipGetLastError());
   return GPE_OK;
@@ -654,7 +691,7 @@ int ensure_grad(gpe_dist* h) {
     R.nlx = R.rank <= NB - 1 ? (NB - 1 - R.rank) / P + 1 : 0;
     DCHK(dalloc(h, &R.X, (size_t)R.ld * NB * TILE, &R.bytes));
     DCHK(dalloc(h, &R.xrow, (size_t)TILE * np, &R.bytes));
-    DCHK(dalloc(h, &R.xgrp, (size_t)h->wmax * TILE * np, &R.bytes));
+    DCHK(dalloc(h, &R.xgrp, 2 * (size_t)h->wmax * TILE * np, &R.bytes));
     DCHK(dalloc(h, &R.dZ, (size_t)np * Pc, &R.bytes));
     DCHK(dalloc(h, &R.dR2, (size_t)np * Pc, &R.bytes));
     DCHK(dalloc(h, &R.r2loc, (size_t)R.ld * TILE, &R.bytes));
@@ -673,9 +710,12 @@ int ensure_grad(gpe_dist* h) {
   // i >= ge with the whole group, R(i, 0:ge) -= L(i, gb:ge) X(gb:ge, 0:ge), K = 128 W.
   std::vector<GemmProb> probs;
   const long long ldx = (long long)h->wmax * TILE;
+  const size_t xg_sz = (size_t)ldx * np;
+  auto xgrp_of = [&](const Rank& R, int k) { return R.xgrp + (size_t)(h->gid[k] & 1) * xg_sz; };
   h->tri_p.assign(NB, DLaunch());
   h->tri_x.assign(NB, DLaunch());
-  h->tri_u.assign(NB, DLaunch());
+  h->tri_un.assign(NB, DLaunch());
+  h->tri_ur.assign(NB, DLaunch());
   for (int k = 0; k < NB; ++k) {
     const int lk = k / P;
     const int gb = h->gstart[k], ge = group_end(h, k), w = k - gb;
@@ -683,7 +723,7 @@ int ensure_grad(gpe_dist* h) {
     if (O && k > 0) {
       double* row = O->X + (long long)lk * TILE;
       if (w > 0) {
-        GemmProb p = dprob(O->A + (long long)lk * TILE + (long long)gb * TILE * O->ld, O->ld, O->xgrp, ldx,
+        GemmProb p = dprob(O->A + (long long)lk * TILE + (long long)gb * TILE * O->ld, O->ld, xgrp_of(*O, k), ldx,
                            row, O->ld, 1, k, w * TILE, 0, -1.0, 1.0);
         p.ntiles = k;
         DLaunch L;
@@ -701,21 +741,27 @@ int ensure_grad(gpe_dist* h) {
       probs.push_back(p);
     }
     if (k + 1 != ge) continue;
-    DLaunch ul;
-    ul.first = (int)probs.size();
-    ul.kind = 1;
-    for (Rank& R : h->ranks) {
-      const int a = lstart_of(ge, P, R.rank), c = R.nlx - a;
-      if (c <= 0) continue;
-      GemmProb p = dprob(R.A + (long long)a * TILE + (long long)gb * TILE * R.ld, R.ld, R.xgrp, ldx,
-                         R.X + (long long)a * TILE, R.ld, c, ge, (ge - gb) * TILE, 0, -1.0, 1.0);
-      p.tile_begin = ul.tiles;
-      p.ntiles = c * ge;
-      ul.tiles += p.ntiles;
-      probs.push_back(p);
-      ++ul.count;
+    // the group's rows applied to every rank's rows below it, in two launches: the
+    // rows of the next group (its chain waits for these only), then the rest
+    const int ge2 = next_group_end(h, k);
+    for (int part = 0; part < 2; ++part) {
+      const int r0 = part == 0 ? ge : ge2, r1 = part == 0 ? ge2 : NB;   // global tile rows [r0, r1)
+      DLaunch ul;
+      ul.first = (int)probs.size();
+      ul.kind = 1;
+      for (Rank& R : h->ranks) {
+        const int a = lstart_of(r0, P, R.rank), b = std::min(R.nlx, lstart_of(r1, P, R.rank)), c = b - a;
+        if (c <= 0) continue;
+        GemmProb p = dprob(R.A + (long long)a * TILE + (long long)gb * TILE * R.ld, R.ld, xgrp_of(R, k), ldx,
+                           R.X + (long long)a * TILE, R.ld, c, ge, (ge - gb) * TILE, 0, -1.0, 1.0);
+        p.tile_begin = ul.tiles;
+        p.ntiles = c * ge;
+        ul.tiles += p.ntiles;
+        probs.push_back(p);
+        ++ul.count;
+      }
+      (part == 0 ? h->tri_un : h->tri_ur)[k] = ul;
     }
-    h->tri_u[k] = ul;
   }
   h->wa_l.assign(h->ranks.size(), DLaunch());
   h->slabs.assign(h->ranks.size(), std::vector<SlabLaunch>());
@@ -768,7 +814,7 @@ int ensure_grad(gpe_dist* h) {
 }
 
 // TRTRI step k: owner applies its group's pending rows and finishes X(k, :), broadcast
-// into every rank's group rows; the step closing a group updates every rank's rows below it
+// into every rank's group rows (the group-closing updates are issued by trtri_all)
 int trtri_step(gpe_dist* h, int k) {
   const int P = h->P, owner = k % P, lk = k / P;
   const int gb = h->gstart[k], ge = group_end(h, k), w = k - gb;
@@ -777,20 +823,19 @@ int trtri_step(gpe_dist* h, int k) {
   if (k == h->NB - 1) return GPE_OK;   // no rows below
   if (Rank* O = rank_slot(h, owner))
     DCHK_HIP(h, hipMemcpy2DAsync(O->xrow, TILE * sizeof(double), O->X + (long long)lk * TILE, O->ld * sizeof(double),
-                                 TILE * sizeof(double), (size_t)(k + 1) * TILE, hipMemcpyDeviceToDevice, h->stream));
+                                 TILE * sizeof(double), (size_t)(k + 1) * TILE, hipMemcpyDeviceToDevice, h->cs));
   DCHK(coll_bcast(h, &Rank::xrow, 0, (size_t)(k + 1) * TILE * TILE, owner));
   // X(k, 0:k+1) -> the group's row block w; zero its columns k+1 .. ge-1, which the
   // group's later rows and the closing update read as X(k, c) = 0
   const long long ldx = (long long)h->wmax * TILE;
   for (Rank& R : h->ranks) {
-    double* blk = R.xgrp + (long long)w * TILE;
+    double* blk = R.xgrp + (size_t)(h->gid[k] & 1) * ldx * h->n_pad + (long long)w * TILE;
     DCHK_HIP(h, hipMemcpy2DAsync(blk, ldx * sizeof(double), R.xrow, TILE * sizeof(double), TILE * sizeof(double),
-                                 (size_t)(k + 1) * TILE, hipMemcpyDeviceToDevice, h->stream));
+                                 (size_t)(k + 1) * TILE, hipMemcpyDeviceToDevice, h->cs));
     if (ge > k + 1)
       DCHK_HIP(h, hipMemset2DAsync(blk + (long long)(k + 1) * TILE * ldx, ldx * sizeof(double), 0,
-                                   TILE * sizeof(double), (size_t)(ge - k - 1) * TILE, h->stream));
+                                   TILE * sizeof(double), (size_t)(ge - k - 1) * TILE, h->cs));
   }
-  DCHK(launch(h, h->tri_u[k], h->gprobs));
   return GPE_OK;
 }
 
@@ -823,7 +868,7 @@ int kbuild(gpe_dist* h, int kernel, double nu, double s2, double rscale) {
   return GPE_OK;
 }
 
-// one column step: diag, Dinv broadcast, panel, pack + all-gather + unpermute, trailing update
+// one column step of a group's chain: diag, Dinv broadcast, panel, pack + all-gather + unpermute
 int step(gpe_dist* h, int k) {
   const int P = h->P, owner = k % P;
   DCHK(launch(h, h->diag[k]));
@@ -832,29 +877,67 @@ int step(gpe_dist* h, int k) {
     if (Rank* O = rank_slot(h, owner))
       DCHK_HIP(h, hipMemcpy2DAsync(O->X + (long long)(k / P) * TILE + (long long)k * TILE * O->ld,
                                    O->ld * sizeof(double), O->dinv, TILE * sizeof(double), TILE * sizeof(double),
-                                   TILE, hipMemcpyDeviceToDevice, h->stream));
+                                   TILE, hipMemcpyDeviceToDevice, h->cs));
   }
   DCHK(launch(h, h->panel_l[k]));
   const long long ldp = (long long)(h->NB + 1) * TILE;
-  const long long pcol = (long long)(k - h->gstart[k]) * TILE * ldp;   // the group's panel block
+  const long long pcol = (long long)(k - h->gstart[k]) * TILE * ldp;   // block of k in its group's panels
   const int T = h->maxT[k];
   if (T > 0) {
     const size_t seg = (size_t)T * TILE * TILE;
     for (Rank& R : h->ranks) {
       const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
       if (c == 0) continue;
-      hipLaunchKernelGGL(k_dist_pack, dim3(c), dim3(256), 0, h->stream, R.A, R.ld, a, k,
+      hipLaunchKernelGGL(k_dist_pack, dim3(c), dim3(256), 0, h->cs, R.A, R.ld, a, k,
                          R.recv + (size_t)R.rank * seg);
       DCHK_HIP(h, hipGetLastError());
     }
     DCHK(coll_allgather(h, &Rank::recv, seg));
     for (Rank& R : h->ranks) {
-      hipLaunchKernelGGL(k_dist_unpermute, dim3(T, P), dim3(256), 0, h->stream, R.recv, (long long)seg,
-                         h->dli0 + (size_t)k * P, h->dcnt + (size_t)k * P, P, R.panel + pcol, ldp);
+      hipLaunchKernelGGL(k_dist_unpermute, dim3(T, P), dim3(256), 0, h->cs, R.recv, (long long)seg,
+                         h->dli0 + (size_t)k * P, h->dcnt + (size_t)k * P, P, panel_of(h, R, k) + pcol, ldp);
       DCHK_HIP(h, hipGetLastError());
     }
   }
-  DCHK(launch(h, h->upd[k]));
+  return GPE_OK;
+}
+
+int ensure_group_events(gpe_dist* h, size_t ng) {
+  while (h->ev_chain.size() < ng) {
+    hipEvent_t a, b;
+    DCHK_HIP(h, hipEventCreateWithFlags(&a, hipEventDisableTiming));
+    DCHK_HIP(h, hipEventCreateWithFlags(&b, hipEventDisableTiming));
+    h->ev_chain.push_back(a);
+    h->ev_next.push_back(b);
+  }
+  return GPE_OK;
+}
+
+// The column groups with one group of look-ahead.  Group g's chain (its steps) runs on
+// the critical stream after the previous group's update of g's own columns; its
+// trailing update then runs on the compute stream, next group's columns first
+// (ev_next[g] releases the next chain), the rest behind them, overlapping the next
+// chain and its collectives.  The compute stream ends after every chain (it waited on
+// each ev_chain), so work queued on it afterwards follows the whole sweep.
+// tri = false: the Cholesky sweep (step); tri = true: the row TRTRI (trtri_step).
+int group_sweep(gpe_dist* h, bool tri) {
+  const int ng = (int)h->gs.size() - 1;
+  DCHK(ensure_group_events(h, (size_t)ng));
+  DCHK_HIP(h, hipEventRecord(h->ev_join, h->stream));
+  DCHK_HIP(h, hipStreamWaitEvent(h->crit, h->ev_join, 0));
+  for (int g = 0; g < ng; ++g) {
+    const int gb = h->gs[g], ge = h->gs[g + 1];
+    h->cs = h->crit;
+    if (g > 0) DCHK_HIP(h, hipStreamWaitEvent(h->crit, h->ev_next[g - 1], 0));
+    for (int k = gb; k < ge; ++k) DCHK(tri ? trtri_step(h, k) : step(h, k));
+    DCHK_HIP(h, hipEventRecord(h->ev_chain[g], h->crit));
+    h->cs = h->stream;
+    DCHK_HIP(h, hipStreamWaitEvent(h->stream, h->ev_chain[g], 0));
+    DCHK(tri ? launch(h, h->tri_un[ge - 1], h->gprobs) : launch(h, h->upd_next[ge - 1]));
+    DCHK_HIP(h, hipEventRecord(h->ev_next[g], h->stream));
+    DCHK(tri ? launch(h, h->tri_ur[ge - 1], h->gprobs) : launch(h, h->upd_rest[ge - 1]));
+  }
+  h->cs = h->stream;
   return GPE_OK;
 }
 
@@ -924,7 +1007,11 @@ gpe_dist* gpe_dist_create(int32_t device, int32_t nranks, int32_t rank, const ui
       pos = end + 1;
     }
   }
-  bool ok = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess &&
+  int lo = 0, hi = 0;   // the critical stream at the highest priority the device offers
+  bool ok = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+            hipStreamCreateWithPriority(&h->crit, hipStreamNonBlocking, hi) == hipSuccess &&
+            hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) == hipSuccess &&
+            hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess &&
             hipEventCreate(&h->e0) == hipSuccess && hipEventCreate(&h->e1) == hipSuccess &&
             hipMalloc((void**)&h->dinfo, sizeof(int)) == hipSuccess;
   if (ok && !h->loop) {
@@ -943,6 +1030,7 @@ void gpe_dist_destroy(gpe_dist* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->crit) (void)hipStreamSynchronize(h->crit);
   if (h->comm) (void)ncclCommDestroy(h->comm);
   for (Rank& R : h->ranks) free_rank(R);
   double** bufs[] = {&h->dX, &h->dXw, &h->dF, &h->dr, &h->dinvdelta, &h->cpart, &h->dT2};
@@ -957,7 +1045,11 @@ void gpe_dist_destroy(gpe_dist* h) {
   for (hipEvent_t e : h->cev) (void)hipEventDestroy(e);
   if (h->e0) (void)hipEventDestroy(h->e0);
   if (h->e1) (void)hipEventDestroy(h->e1);
+  for (hipEvent_t e : h->ev_chain) (void)hipEventDestroy(e);
+  for (hipEvent_t e : h->ev_next) (void)hipEventDestroy(e);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->stream) (void)hipStreamDestroy(h->stream);
+  if (h->crit) (void)hipStreamDestroy(h->crit);
   delete h;
 }
 
@@ -970,6 +1062,7 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
     return dfail(h, GPE_ERR_ARG, "bad shapes");
   DCHK_HIP(h, hipSetDevice(h->device));
   DCHK_HIP(h, hipStreamSynchronize(h->stream));
+  DCHK_HIP(h, hipStreamSynchronize(h->crit));
   h->n = n;
   h->d = d;
   h->q = q;
@@ -1011,6 +1104,7 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
   DCHK(dalloc(h, &h->dinvdelta, GPE_MAX_DIMS, &h->shared_bytes));
   // local ranks and their sweep buffers
   build_groups(h);
+  h->panel_sz = (size_t)(h->NB + 1) * TILE * TILE * h->wmax;
   h->T0 = nloc_of(h->NB, h->P, 0);
   for (int rr = 0; rr < h->P; ++rr) {
     if (!h->loop && rr != h->rank) continue;
@@ -1023,7 +1117,7 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
     DCHK(dalloc(h, &B.A, (size_t)B.ld * (size_t)(h->NB + 1) * TILE, &B.bytes));
     DCHK(dalloc(h, &B.logdet, (size_t)h->NB + 1, &B.bytes));
     DCHK(dalloc(h, &B.dinv, (size_t)TILE * TILE, &B.bytes));
-    DCHK(dalloc(h, &B.panel, (size_t)(h->NB + 1) * TILE * TILE * h->wmax, &B.bytes));
+    DCHK(dalloc(h, &B.panel, 2 * h->panel_sz, &B.bytes));
     DCHK(dalloc(h, &B.recv, (size_t)h->P * h->T0 * TILE * TILE, &B.bytes));
     DCHK(dalloc(h, &B.gram, (size_t)Pc * Pc, &B.bytes));
   }
@@ -1055,6 +1149,7 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
   if (want_grad) DCHK(ensure_grad(h));
   h->grad_now = want_grad != 0;
   h->ev = 0;
+  h->cs = h->stream;
   Rank& R0 = h->ranks[0];   // every rank holds the reduced results; read this process's first
 
   DCHK(pinned(h, (size_t)NB + 1 + (size_t)Pc * Pc + (size_t)(d + 3) + 64));
@@ -1076,7 +1171,7 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
       DCHK_HIP(h, hipMemsetAsync(R.X, 0, (size_t)R.ld * NB * TILE * sizeof(double), h->stream));
   }
   DCHK(kbuild(h, kernel, nu, s2, rscale));
-  for (int k = 0; k < NB; ++k) DCHK(step(h, k));
+  DCHK(group_sweep(h, false));
 
   // Gram of L^-1 [f H] = -(tile (NB, NB)), and Z = L^-1 [f H], from the owner of tile row NB
   const int ra = NB % P;
@@ -1102,8 +1197,7 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
   DCHK_HIP(h, hipMemcpyAsync(hgram, R0.gram, (size_t)Pc * Pc * sizeof(double), hipMemcpyDeviceToHost, h->stream));
   DCHK_HIP(h, hipMemcpyAsync(hgram + Pc * Pc, h->dinfo, sizeof(int), hipMemcpyDeviceToHost, h->stream));
   DCHK_HIP(h, hipEventRecord(h->e1, h->stream));
-  if (h->grad_now)
-    for (int k = 0; k < NB; ++k) DCHK(trtri_step(h, k));
+  if (h->grad_now) DCHK(group_sweep(h, true));
   DCHK_HIP(h, hipEventSynchronize(h->e1));
   int info = 0;
   std::memcpy(&info, hgram + Pc * Pc, sizeof(int));

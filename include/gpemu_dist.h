@@ -59,7 +59,7 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
 /* Objective (and gradient when want_grad != 0), arguments and outputs as
  * gpe_objective.  All ranks call it collectively and all receive the same llh,
  * gradient and sigma2.  The gradient buffers (this rank's rows of L^-1 and a slab
- * of at most 1 GiB of its partial of A^-1) are allocated on the first want_grad
+ * of at most 512 MiB of its partial of A^-1) are allocated on the first want_grad
  * call. */
 int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const double* hp,
                        int32_t n_hp, double nu_fixed, int32_t want_grad, double* llh_out,
