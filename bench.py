@@ -183,6 +183,9 @@ def cpu_baseline(d, n_full, full=False):
     * full=True adds configs[1]: the op-for-op ref-mode objective at n=4096, 3 reps
       (median), ~3 minutes."""
     from oracle import gp_oracle as orc
+
+    def note(msg):   # progress on stderr: the CPU legs run for minutes
+        print(f"[cpu_baseline] {msg}", file=sys.stderr, flush=True)
     host = _host_info()
     threads = host.get("affinity_cpus") or os.cpu_count() or 1
     if host.get("cgroup_cpu_quota"):
@@ -203,11 +206,13 @@ def cpu_baseline(d, n_full, full=False):
         t = time.perf_counter()
         np.linalg.solve(L, B)
         t_n = time.perf_counter() - t
+        note(f"np.linalg.solve(L, {n} x {n}): {t_n:.1f} s")
         del B
         Bq = rs.uniform(-1.0, 1.0, size=(n, q))
         t = time.perf_counter()
         np.linalg.solve(L, Bq)
         t_q = time.perf_counter() - t
+        note(f"np.linalg.solve(L, {n} x {q}): {t_q:.1f} s")
         del L, Bq
         t_ref = 24 * t_n + 5 * t_q
         out.update({"value": 1.0 / t_ref, "unit": "evals/s", "cores": int(threads), "kind": "port",
@@ -221,6 +226,7 @@ def cpu_baseline(d, n_full, full=False):
         t = time.perf_counter()
         orc.objective_fast(X, f, H, hp, orc.GP4ML, orc.STD, True)
         tf = time.perf_counter() - t
+        note(f"objective_fast n={n}: {tf:.1f} s")
         out["fast_mode"] = {"value": 1.0 / tf, "unit": "evals/s", "s_per_eval": tf,
                             "sample": f"oracle objective_fast measured at n={n}, d={d}: {tf:.1f} s/eval"}
         if full:
@@ -230,6 +236,7 @@ def cpu_baseline(d, n_full, full=False):
                 t = time.perf_counter()
                 orc.objective_ref(X2, f2, H2, hp, orc.GP4ML, orc.STD, True)
                 reps.append(time.perf_counter() - t)
+                note(f"objective_ref n=4096: {reps[-1]:.1f} s")
             out["c2_n4096_ref_mode"] = {"s_per_eval_median": float(np.median(reps)), "reps_s": reps,
                                         "evals_per_s": 1.0 / float(np.median(reps))}
     finally:
