@@ -870,6 +870,11 @@ int gpe_debug_trace(uint64_t* out, int32_t n) {
 
 int gpe_abi_version(void) { return GPE_ABI_VERSION; }
 
+#ifndef GPE_SOURCE_HASH
+#define GPE_SOURCE_HASH "unknown"
+#endif
+const char* gpe_build_id(void) { return GPE_SOURCE_HASH; }
+
 int gpe_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;

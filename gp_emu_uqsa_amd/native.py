@@ -15,7 +15,8 @@ import threading as _threading
 import numpy as _np
 
 _HERE = _os.path.dirname(_os.path.abspath(__file__))
-LIB_PATH = _os.environ.get("GPEMU_LIB", _os.path.join(_HERE, "libgpemu.so"))
+_DEFAULT_LIB = _os.path.join(_HERE, "libgpemu.so")
+LIB_PATH = _os.environ.get("GPEMU_LIB", _DEFAULT_LIB)
 
 GPE_OK = 0
 GPE_NOT_PD = 1
@@ -30,6 +31,7 @@ _VP = _ct.c_void_p
 # name -> (restype, argtypes); the full exported surface of include/gpemu.h
 SIGNATURES = {
     "gpe_abi_version": (_ct.c_int, []),
+    "gpe_build_id": (_ct.c_char_p, []),
     "gpe_device_count": (_ct.c_int, []),
     "gpe_device_synchronize": (_ct.c_int, [_ct.c_int32]),
     "gpe_create": (_VP, [_ct.c_int32]),
@@ -107,9 +109,23 @@ def load_library(path: str | None = None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        # provenance: the in-tree library must be built from the sources beside it (a
+        # probe build named by GPEMU_LIB or `path` is the caller's choice)
+        from . import buildinfo
+        want = buildinfo.source_hash() if p == _DEFAULT_LIB else None
+        have = lib.gpe_build_id().decode()
+        if want is not None and have != want:
+            raise NativeUnavailable(
+                f"{p} was built from other sources (build id {have[:12]}, sources {want[:12]}): "
+                "rebuild it with `python -c 'import __graft_entry__ as g; g.build()'`")
         if path is None:
             _lib = lib
         return lib
+
+
+def build_id() -> str:
+    """SHA-256 of the sources the loaded library was built from."""
+    return load_library().gpe_build_id().decode()
 
 
 def _ptr(a):

@@ -33,7 +33,7 @@ extern "C" {
 #define GPE_ABI_VERSION 8   /* 3: gpe_dist_objective gained want_grad / grad_out; 4: sensitivity;
                                 5: gpe_noise_sample (noise_fit); 6: gpe_kernel_grad;
                                 7: gpe_lhc_maximin; 8: gpe_dist_rank_bytes,
-                                gpe_device_synchronize */
+                                gpe_device_synchronize, gpe_build_id */
 
 enum gpe_status {
     GPE_OK = 0,
@@ -60,6 +60,8 @@ enum gpe_variant { GPE_GP4ML = 0, GPE_MUCM = 1 };
 typedef struct gpe_ctx gpe_ctx;
 
 int gpe_abi_version(void);
+/* SHA-256 (hex) of the sources the library was built from (gp_emu_uqsa_amd/buildinfo.py). */
+const char* gpe_build_id(void);
 int gpe_device_count(void);
 /* Wait for all work on GPU `device` (the timed-region bracket of bench.py). */
 int gpe_device_synchronize(int32_t device);

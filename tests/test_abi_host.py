@@ -46,3 +46,23 @@ def test_literal_parser_accepts_numpy2_reprs():
     assert literal("[[np.float64(0.0157), np.float64(0.9854)], [0.1, 2]]") == [[0.0157, 0.9854], [0.1, 2]]
     assert literal("[ ]") == []
     assert literal("[[0.05,1.0],[0.05,10.00]]") == [[0.05, 1.0], [0.05, 10.0]]
+
+
+def test_library_built_from_these_sources():
+    """Provenance: the in-tree library carries the SHA-256 of the sources it was built
+    from (gpe_build_id), equal to the sources present; a different one is refused."""
+    from gp_emu_uqsa_amd import buildinfo
+    assert native.build_id() == buildinfo.source_hash()
+    assert len(native.build_id()) == 64
+
+
+def test_source_hash_tracks_contents(tmp_path):
+    from gp_emu_uqsa_amd import buildinfo
+    root = tmp_path / "tree"
+    (root / "gp_emu_uqsa_amd" / "csrc").mkdir(parents=True)
+    (root / "include").mkdir()
+    (root / "gp_emu_uqsa_amd" / "csrc" / "a.hip").write_text("x")
+    (root / "include" / "b.h").write_text("y")
+    h1 = buildinfo.source_hash(str(root))
+    (root / "include" / "b.h").write_text("z")
+    assert buildinfo.source_hash(str(root)) != h1
