@@ -110,3 +110,23 @@ def test_bench_single_rank_needs_no_group():
     r = _bench(["--gpus", "1", "--rendezvous-check"])
     assert r.returncode == 0, r.stderr
     assert json.loads(r.stdout.strip().splitlines()[-1])["ranks"] == [[0, 0, 1]]
+
+
+def test_bench_under_torchrun():
+    """The driver's N > 1 launch: `python -m torch.distributed.run ... bench.py --gpus N`;
+    the ranks find each other through MASTER_PORT and their common parent."""
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "GPEMU_RDZV_DIR"):
+        e.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rendezvous-check"],
+                       env=e, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and json.loads(lines[0])["ranks"] == [[0, 0, 2], [1, 1, 2]]
