@@ -93,6 +93,12 @@ def spawn_ranks(nprocs: int, argv: list[str]) -> int:
                        LOCAL_WORLD_SIZE=str(nprocs), MASTER_ADDR="127.0.0.1",
                        GPEMU_RDZV_DIR=rdzv)
             env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            if os.environ.get("GPEMU_BENCH_ONE_DEVICE") == "1":
+                # rehearsal with every rank on GPU 0: RCCL refuses two ranks on one device
+                # of one host, so each rank names its own host and RCCL connects them
+                # with its socket transport over the loopback interface
+                env.update(NCCL_HOSTID=f"gpemu-bench-rank-{r}", NCCL_SOCKET_IFNAME="lo",
+                           NCCL_IB_DISABLE="1")
             procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
         rc = 0
         pending = list(procs)
@@ -346,8 +352,9 @@ def guarded_rowblock(native, synthetic, group, rank, world, local, args, sync_al
     visible; a failure on any rank makes all skip; an exception is recorded; and if
     the leg outlives --rowblock-timeout (a rank stuck in a collective), rank 0
     prints the line with the error and every rank exits."""
-    if os.environ.get("GPEMU_BENCH_ONE_DEVICE") == "1":
-        return {"skipped": "one-device rehearsal: RCCL refuses two ranks on one GPU"}
+    if os.environ.get("GPEMU_BENCH_ONE_DEVICE") == "1" and not os.environ.get("NCCL_HOSTID"):
+        return {"skipped": "one-device rehearsal without per-rank NCCL_HOSTID: RCCL refuses two ranks "
+                           "on one GPU of one host"}
     ok = native.load_library().gpe_device_count() > local
     if not all(group.all_gather(bool(ok))):
         return {"skipped": "a rank does not see its GPU"}

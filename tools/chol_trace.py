@@ -34,5 +34,6 @@ for k in range(NB):
 print(" k   d.upd  d.fac  d.pub  p.upd  p.wait  p.mul  seen-pub  gap   step")
 for r in rows[:3] + rows[60:63] + rows[100:103] + rows[-6:]:
     print("%3d " % r[0] + " ".join("%6.1f" % v for v in r[1:]))
-late = np.array([r[1:] for r in rows[88:NB - 1]])
-print("mean over steps 88..%d:" % (NB - 2), " ".join("%6.1f" % v for v in late.mean(axis=0)))
+for lo, hi in ((1, 48), (48, 88), (88, NB - 1)):
+    seg = np.array([r[1:] for r in rows[lo:hi]])
+    print("mean over steps %3d..%3d:" % (lo, hi - 1), " ".join("%6.1f" % v for v in seg.mean(axis=0)))
