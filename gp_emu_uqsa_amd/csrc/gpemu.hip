@@ -33,7 +33,7 @@ constexpr int AUX_DESC_BASE = 1 << 15;
 constexpr int ADHOC_DESC_BASE = MAX_PROBS - 64;
 
 struct Launch {       // one grouped GEMM launch of the cached schedule
-  int kind;           // 0: <0,0>, 1: <1,0>, 2: <1,1>, 3: <0,1>
+  int kind;           // 0: <0,0>, 1: <1,0>, 2: <1,1>, 3: <0,1>, 4: <0,0> fused Cholesky step
   int first, count;   // descriptor range
   int tiles;
   double flops;       // algorithmic flops
@@ -284,7 +284,8 @@ int launch_gemm_range(gpe_ctx* c, const Launch& L, hipStream_t st = nullptr) {
     case 0: hipLaunchKernelGGL((k_gemm<false, false>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, tl, c->dinfo); break;
     case 1: hipLaunchKernelGGL((k_gemm<true, false>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, tl, c->dinfo); break;
     case 2: hipLaunchKernelGGL((k_gemm<true, true>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, tl, c->dinfo); break;
-    default: hipLaunchKernelGGL((k_gemm<false, true>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, tl, c->dinfo); break;
+    case 3: hipLaunchKernelGGL((k_gemm<false, true>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, tl, c->dinfo); break;
+    default: hipLaunchKernelGGL((k_gemm<false, false, true>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, tl, c->dinfo); break;
   }
   HIPCHK(c, hipGetLastError());
   if (c->prof) {
@@ -349,6 +350,16 @@ std::vector<unsigned> order_tiles(const std::vector<GemmProb>& probs) {
   for (size_t j = 0; j < longest; ++j)
     for (int x = 0; x < NX; ++x)
       if (j < bins[x].size()) out.push_back(bins[x][j]);
+  // The launch starts on an idle GPU and its first 512 workgroups fill two slots per CU
+  // in order: workgroup 256 lands on the CU of workgroup 0, the G_DIAG tile
+  // (tools/hip/placement_probe.hip: 256 of 256 pairs i, i - 256 share a CU).  Give
+  // that slot the first panel tile: after its own update it waits on the flag and
+  // leaves the SIMDs to the diagonal factorisation, which beside a bulk tile's MFMAs
+  // runs ~1.7x slower.
+  if (!out.empty() && (probs[out[0] >> 24].flags & G_DIAG) && !tail.empty() && out.size() > 256) {
+    out.insert(out.begin() + 256, tail.front());
+    tail.erase(tail.begin());
+  }
   out.insert(out.end(), tail.begin(), tail.end());
   return out;
 }
@@ -497,7 +508,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
         bulk(fp, fl, rng[h].first, rng[h].second, g0, Kb);
       }
       pl.fused[t] = (int)pl.launches.size();
-      add_launch(pl, 0, fp, fl);
+      add_launch(pl, 4, fp, fl);
     }
   }
   for (int kt = 0; kt + 1 < NB; ++kt) {
@@ -943,7 +954,8 @@ gpe_ctx* gpe_create(int32_t device) {
     ok = hipFuncSetAttribute((const void*)k_gemm<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
          hipFuncSetAttribute((const void*)k_gemm<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
          hipFuncSetAttribute((const void*)k_gemm<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
-         hipFuncSetAttribute((const void*)k_gemm<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess;
+         hipFuncSetAttribute((const void*)k_gemm<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_gemm<false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess;
     if (!ok) c->err = "hipFuncSetAttribute(max dynamic LDS) failed";
   }
   if (!ok) {

@@ -670,7 +670,8 @@ int launch(gpe_dist* h, const DLaunch& L, const GemmProb* base = nullptr) {
   switch (L.kind) {
     case 1: hipLaunchKernelGGL((k_gemm<false, true>), g, dim3(256), lds, h->cs, pr, L.count, tl, h->dinfo); break;
     case 2: hipLaunchKernelGGL((k_gemm<true, true>), g, dim3(256), lds, h->cs, pr, L.count, tl, h->dinfo); break;
-    default: hipLaunchKernelGGL((k_gemm<false, false>), g, dim3(256), lds, h->cs, pr, L.count, tl, h->dinfo); break;
+    default:   // kind 0 launches may carry G_DIAG / G_PANEL problems
+      hipLaunchKernelGGL((k_gemm<false, false, true>), g, dim3(256), lds, h->cs, pr, L.count, tl, h->dinfo); break;
   }
   DCHK_HIP(h, hipGetLastError());
   return GPE_OK;

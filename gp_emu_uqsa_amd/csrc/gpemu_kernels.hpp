@@ -639,6 +639,16 @@ __device__ __forceinline__ double gld1(const double* p) {
 __device__ __forceinline__ void gst1(double* p, double v) {
   *(__attribute__((address_space(1))) double*)(p) = v;
 }
+__device__ __forceinline__ void gst2(double* p, double x, double y) {
+  *(__attribute__((address_space(1))) gvec2*)(p) = gvec2{x, y};
+}
+// value held by lane l ^ 1 (DPP quad_perm [1,0,3,2], two 32-bit moves)
+__device__ __forceinline__ double dpp_xor1(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, 0xB1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0xB1, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 
 template <bool AK, bool BK>
 __device__ __forceinline__ void gemm_gload(const double* __restrict__ Ab,
@@ -846,18 +856,42 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
   __syncthreads();   // callers reuse the staging LDS
 }
 
+// Epilogue and C preload move 16 B per lane: in the MFMA layout lanes l and l ^ 1 hold
+// rows m and m ^ 1 of the same columns, so for each register pair (r, r + 1) the even
+// lane trades its column-(r + 1) value for the odd lane's column-r value (one DPP
+// exchange) and each lane then owns rows (m & ~1, m | 1) of one column: half the store
+// (load) instructions of the 8-byte form, same bytes and addresses.
+// The fused Cholesky's kernel (k_gemm FUSED) keeps the 8-byte form: there the exchange's
+// live values push the factor/panel paths past 256 VGPRs (~150 spilled).
+template <bool WIDE = true>
 __device__ __forceinline__ void gemm_store(double* Cb, long long ldc, double alpha, const d4 (&acc)[4][4]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  if constexpr (!WIDE) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = wm + i * 16 + (lane & 15);
+          const int n = wn + j * 16 + mfma64_row(lane, r);
+          gst1(Cb + m + (long long)n * ldc, alpha * acc[i][j][r]);
+        }
+    return;
+  }
+  const bool odd = lane & 1;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = wm + i * 16 + (lane & 15);
-        const int n = wn + j * 16 + mfma64_row(lane, r);
-        gst1(Cb + m + (long long)n * ldc, alpha * acc[i][j][r]);
+      for (int r = 0; r < 4; r += 2) {
+        const int m = wm + i * 16 + (lane & 14);
+        const int n = wn + j * 16 + mfma64_row(lane, odd ? r + 1 : r);
+        const double a = acc[i][j][r], b = acc[i][j][r + 1];
+        const double got = dpp_xor1(odd ? a : b);
+        gst2(Cb + m + (long long)n * ldc, alpha * (odd ? got : a), alpha * (odd ? b : got));
       }
 }
 
@@ -897,7 +931,10 @@ __device__ unsigned long long gemm_trace[8 * 4096];
 #define GTRACE(P, slot) do {} while (0)
 #endif
 
-template <bool AK, bool BK>
+// FUSED (only <false, false, true>): the fused Cholesky's launches, whose problems may be
+// G_DIAG / G_PANEL; the other instances hold no factor / panel code, so they stay well
+// inside the register budget and use the 16-byte C preload and epilogue.
+template <bool AK, bool BK, bool FUSED = false>
 static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restrict__ probs, int nprob,
                                                   const unsigned* __restrict__ tiles,
                                                   int* __restrict__ abort_flag) {
@@ -956,7 +993,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
   // the C read latency overlaps the first K stage (no per-element RMW chain).
   double* Cb = P.C + (long long)ti * TILE + (long long)tj * TILE * P.ldc;
   d4 acc[4][4];
-  if (P.beta != 0.0) {
+  if (P.beta != 0.0 && FUSED) {   // the fused kernel keeps the 8-byte form (see gemm_store)
     const double sc = P.beta / P.alpha;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -968,6 +1005,22 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
           const int n = wn + j * 16 + mfma64_row(lane, r);
           acc[i][j][r] = sc * gld1(Cb + m + (long long)n * P.ldc);
         }
+  } else if (P.beta != 0.0) {
+    const double sc = P.beta / P.alpha;
+    const bool odd = lane & 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {   // 16-B loads, the inverse of gemm_store's exchange
+          const int m = wm + i * 16 + (lane & 14);
+          const int n = wn + j * 16 + mfma64_row(lane, odd ? r + 1 : r);
+          const double2 v = gld2(Cb + m + (long long)n * P.ldc);
+          const double got = dpp_xor1(odd ? v.x : v.y);
+          acc[i][j][r] = sc * (odd ? got : v.x);
+          acc[i][j][r + 1] = sc * (odd ? v.y : got);
+        }
   } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -978,7 +1031,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
   const int nk = (kend - kbeg) / GK;
   if (nk > 0) gemm_kloop<AK, BK>(Ab, Bb, P.lda, P.ldb, kbeg, nk, lds, acc);
 
-  if constexpr (!AK && !BK) {
+  if constexpr (FUSED) {
     if (P.flags & G_DIAG) {
       GTRACE(P, 1);
       // updated diagonal tile -> block-packed LDS (lower half), then factor + invert;
@@ -1009,7 +1062,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
       // updated panel tile -> C; wait for the diagonal inverse X of this launch;
       // then L = C X^T over the same tile
       if (ti == 0) GTRACE(P, 5);
-      gemm_store(Cb, P.ldc, P.alpha, acc);
+      gemm_store<false>(Cb, P.ldc, P.alpha, acc);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       int* ready = reinterpret_cast<int*>(lds + G_LDS_LAUNCH_DOUBLES - 1);   // staging is idle here
       if (tid == 0) *ready = gemm_wait_flag(P.flag);
@@ -1026,12 +1079,12 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
       gemm_kloop<false, false>(Cb, P.X, P.ldc, P.ldx, 0, TILE / GK, lds, acc);
-      gemm_store(Cb, P.ldc, 1.0, acc);
+      gemm_store<false>(Cb, P.ldc, 1.0, acc);
       if (ti == 0) GTRACE(P, 7);
       return;
     }
   }
-  gemm_store(Cb, P.ldc, P.alpha, acc);
+  gemm_store<!FUSED>(Cb, P.ldc, P.alpha, acc);
 }
 
 // ---------------------------------------------------------------------------

@@ -2,7 +2,10 @@
 (dev tool): k contexts (own HIP stream and buffers), one host thread each (ctypes
 drops the GIL during library calls), each evaluating the objective `reps` times
 at its own hyperparameters, as concurrent multistart tries would.
-usage: python tools/concurrent_evals.py [n] [k] [reps]"""
+usage: python tools/concurrent_evals.py [n] [k] [reps] [stagger_ms]
+stagger_ms: try i starts i * stagger_ms later (so the tries' phases are offset); the
+rate then discounts the stagger (k * reps / (span - (k-1) * stagger)), and each
+try's own rate is printed."""
 import sys
 import threading
 import time
@@ -15,6 +18,7 @@ from gp_emu_uqsa_amd import native, synthetic  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+stagger = float(sys.argv[4]) / 1e3 if len(sys.argv) > 4 else 0.0
 d = 10
 X, f, H = synthetic.problem(n, d, seed=0)
 ctxs = []
@@ -26,11 +30,15 @@ hps = [np.concatenate([np.full(d, 1.0 + 0.05 * i), [1e-3, 1.0]]) for i in range(
 for c, hp in zip(ctxs, hps):
     c.objective(0, 0, hp)
 res = [None] * k
+span = [[0.0, 0.0] for _ in range(k)]
 
 
 def work(i):
+    time.sleep(i * stagger)
+    span[i][0] = time.perf_counter()
     for _ in range(reps):
         res[i] = ctxs[i].objective(0, 0, hps[i])
+    span[i][1] = time.perf_counter()
 
 
 for trial in range(2):
@@ -40,9 +48,10 @@ for trial in range(2):
         t.start()
     for t in th:
         t.join()
-    dt = time.perf_counter() - t0
-    print(f"k={k} n={n}: {k * reps} evals in {dt:.3f} s -> {k * reps / dt:.2f} evals/s "
-          f"({dt / reps * 1e3:.1f} ms per round of {k})", flush=True)
+    dt = time.perf_counter() - t0 - (k - 1) * stagger
+    own = " ".join(f"{reps / (e - b):.2f}" for b, e in span)
+    print(f"k={k} n={n} stagger {stagger * 1e3:.0f} ms: {k * reps} evals -> {k * reps / dt:.2f} evals/s "
+          f"({dt / reps * 1e3:.1f} ms per round of {k}); per try {own}", flush=True)
 single = native.Context(0)
 single.set_data(X, f, H)
 single.objective(0, 0, hps[0])

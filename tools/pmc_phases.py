@@ -1,0 +1,67 @@
+"""Per-launch PMC picture of one objective evaluation, grouped by phase (dev tool,
+run on the GPU box): shader clock and MFMA busy, L2 hit rate, HBM bytes.
+
+Separate rocprofv3 --pmc passes (counter-block limits; FETCH_SIZE and WRITE_SIZE
+apart), each over one evaluation at (n, d) (tools/prof_objective.py).  Launches are
+matched across passes by their order.  Per MI355X_MICROARCH.md: clock = GRBM_GUI_ACTIVE
+/ 8 / wall time, MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (clock cycles x 1024 SIMDs),
+FETCH_SIZE doubled on gfx950 (KiB).
+Phases: the 128 fused Cholesky launches in column groups (steps 1-47 / 48-87 / 88-127),
+the TRTRI launches, the LAUUM.
+usage: python tools/pmc_phases.py [n] [d]"""
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+d = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+passes = [["GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES"],
+          ["TCC_HIT_sum", "TCC_MISS_sum"],
+          ["FETCH_SIZE"],
+          ["WRITE_SIZE"]]
+launches = None
+for i, counters in enumerate(passes):
+    odir = os.path.join(root, "gpurun_out", f"pmc_phase{i}")
+    cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", *counters, "-d", odir, "-o", "run",
+           "--output-format", "csv", "--", sys.executable, os.path.join(root, "tools", "prof_objective.py"),
+           str(n), str(d), "1"]
+    subprocess.run(cmd, check=True, cwd=root, env=dict(os.environ, TMPDIR="/tmp"))
+    rows = {}
+    for f in glob.glob(os.path.join(odir, "**", "*counter_collection*.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "k_gemm" not in r["Kernel_Name"]:
+                continue
+            k = int(r["Dispatch_Id"])
+            e = rows.setdefault(k, {"ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
+                                    "kind": r["Kernel_Name"].split("(")[0].replace("void gpe::", "")})
+            e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    seq = [rows[k] for k in sorted(rows)]
+    if launches is None:
+        launches = seq
+    else:
+        assert len(seq) == len(launches), (len(seq), len(launches))
+        for a, b in zip(launches, seq):
+            for key, v in b.items():
+                if key not in ("ns", "kind"):
+                    a[key] = v
+assert len(launches) == 143, len(launches)   # 128 Cholesky + 14 TRTRI + 1 LAUUM at n = 16384
+groups = {"chol 1-47": launches[1:48], "chol 48-87": launches[48:88], "chol 88-127": launches[88:128],
+          "trtri": launches[128:142], "lauum": launches[142:143]}
+out = {"n": n, "d": d, "phases": {}}
+for name, ls in groups.items():
+    ns = sum(e["ns"] for e in ls)
+    gui = sum(e.get("GRBM_GUI_ACTIVE", 0.0) for e in ls)
+    clk = gui / 8 / (ns * 1e-9)
+    busy = sum(e.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) for e in ls) / (clk * ns * 1e-9 * 1024)
+    hit = sum(e.get("TCC_HIT_sum", 0.0) for e in ls)
+    miss = sum(e.get("TCC_MISS_sum", 0.0) for e in ls)
+    fetch = 2.0 * 1024.0 * sum(e.get("FETCH_SIZE", 0.0) for e in ls)
+    write = 1024.0 * sum(e.get("WRITE_SIZE", 0.0) for e in ls)
+    out["phases"][name] = {"launches": len(ls), "ms": ns / 1e6, "clock_ghz": clk / 1e9, "mfma_busy": busy,
+                           "l2_hit": hit / max(hit + miss, 1.0), "hbm_read_gb": fetch / 1e9,
+                           "hbm_write_gb": write / 1e9, "hbm_tb_s": (fetch + write) / (ns * 1e-9) / 1e12}
+print(json.dumps(out, indent=1))
