@@ -410,6 +410,10 @@ def main(argv=None):
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     if os.environ.get("GPEMU_BENCH_ONE_DEVICE") == "1":
         local = 0   # rehearsal of the N-rank path with every rank on GPU 0 (one-GPU box)
+        if world > 1:   # under a launcher too: each rank names its own host for RCCL (see spawn_ranks)
+            os.environ.setdefault("NCCL_HOSTID", f"gpemu-bench-rank-{rank}")
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+            os.environ.setdefault("NCCL_IB_DISABLE", "1")
 
     from gp_emu_uqsa_amd import rendezvous
     group = rendezvous.init_from_env() if world > 1 else None
