@@ -537,7 +537,11 @@ def main(argv=None):
                                "ms_per_launch": gemm_ms / gemm_n}
             whole = K * 4398e9 * (args.n / 16384) ** 3 / 1e12   # ~n^3 algorithmic flops per eval
             step_tflops = whole / (elapsed / args.steps)
-            out["extra"] = {"phase_ms": {k: v / max(prof_steps, 1) for k, v in phase_acc.items()},
+            phase_ms = {k: v / max(prof_steps, 1) for k, v in phase_acc.items()}
+            third = float(args.n) ** 3 / 3.0   # algorithmic flops of POTRF, TRTRI and LAUUM each
+            out["extra"] = {"phase_ms": phase_ms,
+                            "phase_tflops": {k: third / (phase_ms[k] * 1e-3) / 1e12
+                                             for k in ("cholesky", "trtri", "inverse") if phase_ms.get(k)},
                             "roofline_sample": f"HIP events around every GEMM launch of timed step "
                                                f"{args.steps} (its {K} evals run one at a time)",
                             "eval_tflops_algorithmic": step_tflops,
