@@ -38,6 +38,7 @@ struct Launch {       // one grouped GEMM launch of the cached schedule
   int tiles;
   double flops;       // algorithmic flops
   long long list = -1;  // offset of its tile list in the device list array (-1: implicit order)
+  bool cdef = false;    // k_gemm's CDEF instance (gemm_cdef of some problem)
 };
 
 struct Plan {
@@ -280,12 +281,23 @@ int launch_gemm_range(gpe_ctx* c, const Launch& L, hipStream_t st = nullptr) {
     }
     HIPCHK(c, hipEventRecord(c->gev[c->gev_used], st));
   }
-  switch (L.kind) {
-    case 0: hipLaunchKernelGGL((k_gemm<false, false>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, tl, c->dinfo); break;
-    case 1: hipLaunchKernelGGL((k_gemm<true, false>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, tl, c->dinfo); break;
-    case 2: hipLaunchKernelGGL((k_gemm<true, true>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, tl, c->dinfo); break;
-    case 3: hipLaunchKernelGGL((k_gemm<false, true>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, tl, c->dinfo); break;
-    default: hipLaunchKernelGGL((k_gemm<false, false, true>), dim3(L.tiles), dim3(256), lds, st, pr, L.count, tl, c->dinfo); break;
+  const dim3 g(L.tiles), b(256);
+  if (L.cdef) {
+    switch (L.kind) {
+      case 0: hipLaunchKernelGGL((k_gemm<false, false, false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
+      case 1: hipLaunchKernelGGL((k_gemm<true, false, false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
+      case 2: hipLaunchKernelGGL((k_gemm<true, true, false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
+      case 3: hipLaunchKernelGGL((k_gemm<false, true, false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
+      default: hipLaunchKernelGGL((k_gemm<false, false, true, true>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
+    }
+  } else {
+    switch (L.kind) {
+      case 0: hipLaunchKernelGGL((k_gemm<false, false>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
+      case 1: hipLaunchKernelGGL((k_gemm<true, false>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
+      case 2: hipLaunchKernelGGL((k_gemm<true, true>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
+      case 3: hipLaunchKernelGGL((k_gemm<false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
+      default: hipLaunchKernelGGL((k_gemm<false, false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
+    }
   }
   HIPCHK(c, hipGetLastError());
   if (c->prof) {
@@ -375,6 +387,7 @@ void add_launch(Plan& pl, int kind, std::vector<GemmProb> probs, double flops) {
     p.tile_begin = t;
     p.ntiles = prob_tiles(p);
     t += p.ntiles;
+    L.cdef = L.cdef || gemm_cdef(p);
     listable = listable && p.mt <= 4096 && p.nt <= 4096;
     pl.probs.push_back(p);
   }
@@ -951,7 +964,12 @@ gpe_ctx* gpe_create(int32_t device) {
   for (int i = 0; i < 16 && ok; ++i) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
   if (ok) {
     const int gl = G_LDS_DOUBLES * (int)sizeof(double);
-    ok = hipFuncSetAttribute((const void*)k_gemm<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
+    ok = hipFuncSetAttribute((const void*)k_gemm<false, false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_gemm<true, false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_gemm<true, true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_gemm<false, true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_gemm<false, false, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_gemm<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
          hipFuncSetAttribute((const void*)k_gemm<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
          hipFuncSetAttribute((const void*)k_gemm<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
          hipFuncSetAttribute((const void*)k_gemm<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
@@ -2080,6 +2098,7 @@ int gpe_test_gemm(gpe_ctx* c, int32_t trans_a, int32_t trans_b, int64_t M, int64
     HIPCHK(c, hipMemsetAsync(c->dinfo, 0, sizeof(int), c->stream));
     const int kind = trans_a ? (trans_b ? 2 : 1) : (trans_b ? 3 : 0);
     Launch L{kind, ADHOC_DESC_BASE + 8, 1, p.ntiles, 0.0};
+    L.cdef = gemm_cdef(p);
     rc = launch_gemm_range(c, L);
     if (rc == GPE_OK) {
       hipError_t e = hipStreamSynchronize(c->stream);
@@ -2125,6 +2144,7 @@ int gpe_bench_gemm(gpe_ctx* c, int32_t trans_a, int32_t trans_b, int32_t mt, int
     HIPCHK(c, hipMemsetAsync(c->dinfo, 0, sizeof(int), c->stream));
     const int kind = trans_a ? (trans_b ? 2 : 1) : (trans_b ? 3 : 0);
     Launch L{kind, ADHOC_DESC_BASE + 16, 1, p.ntiles, 0.0};
+    L.cdef = gemm_cdef(p);
     const bool prof = c->prof;
     c->prof = false;
     rc = launch_gemm_range(c, L);   // warm-up

@@ -261,6 +261,7 @@ struct DLaunch {           // one grouped k_gemm launch
   int first = 0, count = 0, tiles = 0;
   long long list = -1;
   int kind = 0;            // 0 <false,false>, 1 <false,true>, 2 <true,true>
+  bool cdef = false;       // k_gemm's CDEF instance (gemm_cdef of some problem)
 };
 
 struct SlabLaunch {        // one slab of a rank's partial of A^-1: GEMM + contraction
@@ -583,6 +584,7 @@ int build_schedule(gpe_dist* h) {
       p.tile_begin = dl.tiles;
       p.ntiles = 1;
       dl.tiles += 1;
+      dl.cdef = dl.cdef || gemm_cdef(p);
       probs.push_back(p);
       ++dl.count;
     }
@@ -598,6 +600,7 @@ int build_schedule(gpe_dist* h) {
         p.tile_begin = dl.tiles;
         p.ntiles = c;
         dl.tiles += c;
+        dl.cdef = dl.cdef || gemm_cdef(p);
         probs.push_back(p);
         ++dl.count;
       }
@@ -639,6 +642,7 @@ int build_schedule(gpe_dist* h) {
           for (int j = j0; j < j1 && j <= gt; ++j)
             tiles.push_back(((unsigned)pi << 24) | ((unsigned)li << 12) | (unsigned)j);
         }
+        ul.cdef = ul.cdef || gemm_cdef(p);
         probs.push_back(p);
         ++pi;
         ++ul.count;
@@ -667,11 +671,21 @@ int launch(gpe_dist* h, const DLaunch& L, const GemmProb* base = nullptr) {
   const unsigned* tl = L.list >= 0 ? h->dtiles + L.list : nullptr;
   const GemmProb* pr = (base ? base : h->dprobs) + L.first;
   const dim3 g(L.tiles);
-  switch (L.kind) {
-    case 1: hipLaunchKernelGGL((k_gemm<false, true>), g, dim3(256), lds, h->cs, pr, L.count, tl, h->dinfo); break;
-    case 2: hipLaunchKernelGGL((k_gemm<true, true>), g, dim3(256), lds, h->cs, pr, L.count, tl, h->dinfo); break;
-    default:   // kind 0 launches may carry G_DIAG / G_PANEL problems
-      hipLaunchKernelGGL((k_gemm<false, false, true>), g, dim3(256), lds, h->cs, pr, L.count, tl, h->dinfo); break;
+  const dim3 b(256);
+  if (L.cdef) {
+    switch (L.kind) {
+      case 1: hipLaunchKernelGGL((k_gemm<false, true, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo); break;
+      case 2: hipLaunchKernelGGL((k_gemm<true, true, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo); break;
+      default:   // kind 0 launches may carry G_DIAG / G_PANEL problems
+        hipLaunchKernelGGL((k_gemm<false, false, true, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo); break;
+    }
+  } else {
+    switch (L.kind) {
+      case 1: hipLaunchKernelGGL((k_gemm<false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo); break;
+      case 2: hipLaunchKernelGGL((k_gemm<true, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo); break;
+      default:   // kind 0 launches may carry G_DIAG / G_PANEL problems
+        hipLaunchKernelGGL((k_gemm<false, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo); break;
+    }
   }
   DCHK_HIP(h, hipGetLastError());
   return GPE_OK;
@@ -729,6 +743,7 @@ int ensure_grad(gpe_dist* h) {
         p.ntiles = k;
         DLaunch L;
         L.first = (int)probs.size(); L.count = 1; L.tiles = k; L.kind = 1;
+        L.cdef = gemm_cdef(p);
         h->tri_p[k] = L;
         probs.push_back(p);
       }
@@ -758,6 +773,7 @@ int ensure_grad(gpe_dist* h) {
         p.tile_begin = ul.tiles;
         p.ntiles = c * ge;
         ul.tiles += p.ntiles;
+        ul.cdef = ul.cdef || gemm_cdef(p);
         probs.push_back(p);
         ++ul.count;
       }
@@ -782,6 +798,7 @@ int ensure_grad(gpe_dist* h) {
       p.ntiles = 1;
       ++wl.tiles;
       ++wl.count;
+      wl.cdef = wl.cdef || gemm_cdef(p);
       probs.push_back(p);
     }
     h->wa_l[s] = wl;

@@ -608,6 +608,16 @@ struct GemmProb {
   int* flag;          // G_DIAG releases, G_PANEL waits
 };
 
+// dev-tool per-tile timeline (-DGEMM_TTRACE build only, tools/hip/tile_probe.hip): per
+// workgroup, [0] start, [1] C and first stage landed, [2] K loop done, [3] stores done,
+// [4] hardware id, [5] XCC id
+#ifdef GEMM_TTRACE
+__device__ unsigned long long gemm_ttrace[8 * 65536];
+#define TTRACE(slot) do { if (threadIdx.x == 0 && blockIdx.x < 65536) gemm_ttrace[blockIdx.x * 8 + (slot)] = wall_clock64(); } while (0)
+#else
+#define TTRACE(slot) do {} while (0)
+#endif
+
 constexpr int GK = 16;
 constexpr int GP = 144;    // [k][m] image of an M-contiguous operand: pitch 144 doubles
 constexpr int GQ = 18;     // [m][k] image of a K-contiguous operand: pitch 18 doubles
@@ -790,6 +800,99 @@ __device__ __forceinline__ void gemm_mfmas(d4 (&acc)[4][4], const double (&af)[4
     acc[u >> 2][u & 3] = __builtin_amdgcn_mfma_f64_16x16x4f64(bf[u & 3], af[u >> 2], acc[u >> 2][u & 3], 0, 0, 0);
 }
 
+// C added inside the K loop (beta != 0, >= 10 stages), in eight chunks of two
+// accumulator blocks (chunk c = blocks (c >> 1, 2 (c & 1) + {0, 1}), 8 values per lane):
+// chunk c is loaded in stage c after that stage's operand loads, into buffer c & 1, and
+// added at the top of stage c + 2.  The stage-end wait lets the chunk just issued stay in
+// flight (vmcnt counts in issue order), so each chunk has ~1.5 stages to arrive.  The
+// tile's first MFMA then waits only for its first stage, not for the 128 KB of C: the
+// up-front preload costs ~11 us per tile at K = 512 (tools/hip/tile_probe.hip), and with
+// one stage of slack the chunks stall the loop by as much.  Chunk indices are template
+// constants (the first ten stages are unrolled): no register is indexed at run time.
+// WIDE: the 16-byte form of gemm_store (DPP exchange at the add).
+template <int V> struct gemm_ic { static constexpr int v = V; };
+constexpr int C_CHUNKS = 8;
+// host: a launch holding this problem uses the CDEF instance of k_gemm (tiles with fewer
+// than C_CHUNKS + 2 stages still preload C there)
+// (ldc bound: the chunk loads' 32-bit buffer offsets reach 64 columns of C)
+inline bool gemm_cdef(const GemmProb& p) {
+  return p.beta != 0.0 && p.K >= (C_CHUNKS + 2) * GK && p.ldc <= (1ll << 21);
+}
+
+// The chunk loads are buffer loads off one per-wave resource (SGPRs), one per-lane byte
+// offset (one VGPR) and a scalar offset per load: with 64-bit per-load addresses the
+// straight-line prologue keeps every chunk's addresses live and spills.
+struct CSrc {
+  __amdgpu_buffer_rsrc_t rsrc;   // C tile + this wave's (wm, wn) corner
+  int voff;                      // lane part of the element offset, bytes
+  int ldc8;                      // ldc in bytes
+};
+
+template <bool WIDE>
+__device__ __forceinline__ CSrc c_src(const double* Cb, long long ldc, int lane, int wm, int wn) {
+  CSrc c;
+  const double* base = Cb + __builtin_amdgcn_readfirstlane(wm) + (long long)__builtin_amdgcn_readfirstlane(wn) * ldc;
+  c.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, -1, 0x00020000);
+  const int ml = WIDE ? (lane & 14) : (lane & 15);
+  const int nl = (lane >> 4) + (WIDE ? 4 * (lane & 1) : 0);   // WIDE: odd lanes read row r + 1
+  c.voff = (int)((ml + (long long)nl * ldc) * 8);
+  c.ldc8 = (int)(ldc * 8);
+  return c;
+}
+
+template <int CI, bool WIDE>
+__device__ __forceinline__ void c_chunk_load(const CSrc& c, double (&ct)[8]) {
+  constexpr int I = CI >> 1;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int j = 2 * (CI & 1) + q;
+    if constexpr (WIDE) {
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        const int so = I * 16 * 8 + (j * 16 + 4 * r) * c.ldc8;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(c.rsrc, c.voff, so, 0);
+        ct[4 * q + r] = __longlong_as_double(((long long)v[1] << 32) | v[0]);
+        ct[4 * q + r + 1] = __longlong_as_double(((long long)v[3] << 32) | v[2]);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int so = I * 16 * 8 + (j * 16 + 4 * r) * c.ldc8;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(c.rsrc, c.voff, so, 0);
+        ct[4 * q + r] = __longlong_as_double(((long long)v[1] << 32) | v[0]);
+      }
+    }
+  }
+}
+
+// use == false (a tile of a CDEF launch whose C is preloaded or absent): add nothing,
+// by selection rather than a branch (a branch here costs the stage-end wait its count)
+template <int CI, bool WIDE>
+__device__ __forceinline__ void c_chunk_add(d4 (&acc)[4][4], int lane, bool use, double sc, const double (&ct)[8]) {
+  constexpr int I = CI >> 1;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    d4& a = acc[I][2 * (CI & 1) + q];
+    if constexpr (WIDE) {
+      const bool odd = lane & 1;
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        const double x = ct[4 * q + r], y = ct[4 * q + r + 1];
+        const double got = dpp_xor1(odd ? x : y);
+        a[r] += use ? sc * (odd ? got : x) : 0.0;
+        a[r + 1] += use ? sc * (odd ? y : got) : 0.0;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] += use ? sc * ct[4 * q + r] : 0.0;
+    }
+    // pin the adds here, ahead of the stage's loads: sunk past the `if (more)` loads they
+    // would sit at a join point where the waitcnt pass falls back to vmcnt(0)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(a[r]));
+  }
+}
+
 // K loop of one 128x128 output tile: acc += opA(Ab) opB(Bb) over nk stages of GK.
 // Software pipeline (source order): the fragments of the next k-step are read while
 // the 16 MFMAs of the current one issue; at a stage boundary the last 4 MFMAs are
@@ -802,13 +905,17 @@ __device__ __forceinline__ void gemm_mfmas(d4 (&acc)[4][4], const double (&af)[4
 #else
 #define GEMM_SB() do {} while (0)
 #endif
-template <bool AK, bool BK>
+template <bool AK, bool BK, bool WIDE = true, bool CDEF = false>
 __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
                                            long long lda, long long ldb, int kbeg, int nk, double* lds,
-                                           d4 (&acc)[4][4]) {
+                                           d4 (&acc)[4][4], bool cuse = false, const double* Cb = nullptr,
+                                           long long ldc = 0, double sc = 0.0) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   double fa0[4], fb0[4], fa1[4], fb1[4];
+  double ct0[8], ct1[8];   // CDEF: C chunks in flight (buffer c & 1)
+  CSrc csrc;
+  if constexpr (CDEF) csrc = c_src<WIDE>(Cb, ldc, lane, wm, wn);
 #ifdef GEMM_REGSTAGE
   double ra[8], rb[8];
   gemm_gload<AK, BK>(Ab, Bb, lda, ldb, kbeg, tid, ra, rb);
@@ -818,14 +925,28 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   __syncthreads();
+  TTRACE(1);
   gemm_frags<AK, BK>(lds, lds + G_OPND, 0, lane, wm, wn, fa0, fb0);
-  for (int s = 0; s < nk; ++s) {
-    const bool more = s + 1 < nk;
+  // stage s; CI >= 0 (CDEF's first 10 stages, unrolled): C chunk CI is loaded here
+  // and chunk CI - 2 added (nothing added unless cuse).  CDEF is a kernel template
+  // parameter, not a branch: two inlined K loops in one kernel push the allocator past
+  // 256 VGPRs, and run-time branches around the chunks cost the waitcnt pass its counts.
+  auto stage = [&](int s, auto cc) {
+    constexpr int CI = decltype(cc)::v;
+    const bool more = (CI >= 0 && CI + 2 < C_CHUNKS + 2) || s + 1 < nk;   // prologue: nk >= C_CHUNKS + 2
+    if constexpr (CI >= 0) __builtin_amdgcn_sched_barrier(0);   // prologue stages stay apart
+    if constexpr (CDEF && CI >= 2) c_chunk_add<CI - 2, WIDE>(acc, lane, cuse, sc, (CI & 1) ? ct1 : ct0);
 #ifdef GEMM_REGSTAGE
     if (more) gemm_gload<AK, BK>(Ab, Bb, lda, ldb, kbeg + (s + 1) * GK, tid, ra, rb);
 #else
     if (more) gemm_glds<AK, BK>(Ab, Bb, lda, ldb, kbeg + (s + 1) * GK, tid, lds, (s + 1) & 1);
 #endif
+    constexpr bool CLOAD = CDEF && CI >= 0 && CI < C_CHUNKS;
+    if constexpr (CLOAD) {
+      __builtin_amdgcn_sched_barrier(0);   // the chunk's loads issue after the stage's
+      c_chunk_load<CI, WIDE>(csrc, (CI & 1) ? ct1 : ct0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     const double* As = lds + (s & 1) * (2 * G_OPND);
     const double* Bs = As + G_OPND;
     gemm_frags<AK, BK>(As, Bs, 1, lane, wm, wn, fa1, fb1);
@@ -842,17 +963,46 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
     if (more) {
 #ifdef GEMM_REGSTAGE
       gemm_sstore<AK, BK>(lds, (s + 1) & 1, tid, ra, rb);
-#else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stage s+1 pieces landed
-#endif
       __syncthreads();
+#else
+      // this wave's stage s+1 pieces landed; a chunk issued after them may stay in flight
+      if constexpr (CLOAD && WIDE) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if constexpr (CLOAD) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // bare barrier: __syncthreads' workgroup fence would add a vmcnt(0) (the chunk in
+      // flight); this stage's fragment reads were all consumed by its MFMAs, and the
+      // clobber keeps the compiler from moving LDS accesses across
+      asm volatile("s_barrier" ::: "memory");
+#endif
       const double* An = lds + ((s + 1) & 1) * (2 * G_OPND);
       gemm_frags<AK, BK>(An, An + G_OPND, 0, lane, wm, wn, fa0, fb0);
     }
     GEMM_SB();
     gemm_mfmas<12, 16>(acc, fa1, fb1);
     GEMM_SB();
+    if constexpr (CI >= 0) __builtin_amdgcn_sched_barrier(0);
+  };
+  // CDEF prologue: the first C_CHUNKS + 2 stages as straight-line code (no branch between
+  // a chunk's load and its add, so the waitcnt pass keeps its counts; at a join it falls
+  // back to vmcnt(0)); shorter tiles (never cuse) take the loop alone
+  int s0 = 0;
+  if constexpr (CDEF) {
+    static_assert(C_CHUNKS == 8, "prologue length");
+    if (nk >= C_CHUNKS + 2) {
+      stage(0, gemm_ic<0>{});
+      stage(1, gemm_ic<1>{});
+      stage(2, gemm_ic<2>{});
+      stage(3, gemm_ic<3>{});
+      stage(4, gemm_ic<4>{});
+      stage(5, gemm_ic<5>{});
+      stage(6, gemm_ic<6>{});
+      stage(7, gemm_ic<7>{});
+      stage(8, gemm_ic<8>{});
+      stage(9, gemm_ic<9>{});
+      s0 = C_CHUNKS + 2;
+    }
   }
+  for (int s = s0; s < nk; ++s) stage(s, gemm_ic<-1>{});
   __syncthreads();   // callers reuse the staging LDS
 }
 
@@ -934,7 +1084,7 @@ __device__ unsigned long long gemm_trace[8 * 4096];
 // FUSED (only <false, false, true>): the fused Cholesky's launches, whose problems may be
 // G_DIAG / G_PANEL; the other instances hold no factor / panel code, so they stay well
 // inside the register budget and use the 16-byte C preload and epilogue.
-template <bool AK, bool BK, bool FUSED = false>
+template <bool AK, bool BK, bool FUSED = false, bool CDEF = false>
 static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restrict__ probs, int nprob,
                                                   const unsigned* __restrict__ tiles,
                                                   int* __restrict__ abort_flag) {
@@ -982,6 +1132,13 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  TTRACE(0);
+#ifdef GEMM_TTRACE
+  if (threadIdx.x == 0 && blockIdx.x < 65536) {
+    gemm_ttrace[blockIdx.x * 8 + 4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    gemm_ttrace[blockIdx.x * 8 + 5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+  }
+#endif
   if (P.flags & G_DIAG) GTRACE(P, 0);
   if ((P.flags & G_PANEL) && ti == 0) GTRACE(P, 4);
 
@@ -989,11 +1146,19 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
   const double* Bb = BK ? P.B + (long long)tj * TILE * P.ldb : P.B + (long long)tj * TILE;
 
   // operands are swapped in the MFMA, so D = (A B)^T: lane&15 -> m, row map -> n.
-  // beta != 0: the accumulators start at (beta/alpha) C, loaded in one burst so
-  // the C read latency overlaps the first K stage (no per-element RMW chain).
+  // beta != 0: with >= 10 K stages C is added inside the K loop (c_chunk_load); shorter
+  // tiles start the accumulators at (beta/alpha) C, loaded in one burst.
   double* Cb = P.C + (long long)ti * TILE + (long long)tj * TILE * P.ldc;
+  const int nk = (kend - kbeg) / GK;
+  // beta != 0 with >= 10 stages: C is added chunk by chunk inside the K loop (c_chunk_load)
+  const bool cdefer = CDEF && P.beta != 0.0 && nk >= C_CHUNKS + 2;
   d4 acc[4][4];
-  if (P.beta != 0.0 && FUSED) {   // the fused kernel keeps the 8-byte form (see gemm_store)
+  if (cdefer) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+  } else if (P.beta != 0.0 && FUSED) {   // the fused kernel keeps the 8-byte form (see gemm_store)
     const double sc = P.beta / P.alpha;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1028,8 +1193,9 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
       for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
   }
 
-  const int nk = (kend - kbeg) / GK;
-  if (nk > 0) gemm_kloop<AK, BK>(Ab, Bb, P.lda, P.ldb, kbeg, nk, lds, acc);
+  if (nk > 0) gemm_kloop<AK, BK, !FUSED, CDEF>(Ab, Bb, P.lda, P.ldb, kbeg, nk, lds, acc, cdefer, Cb, P.ldc,
+                                               P.beta / P.alpha);
+  TTRACE(2);
 
   if constexpr (FUSED) {
     if (P.flags & G_DIAG) {
@@ -1085,6 +1251,11 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
     }
   }
   gemm_store<!FUSED>(Cb, P.ldc, P.alpha, acc);
+#ifdef GEMM_TTRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  TTRACE(3);
+#endif
 }
 
 // ---------------------------------------------------------------------------
