@@ -30,7 +30,7 @@ for i, r in enumerate(seg):
     gap = (s - prev_end) / 1e3 if prev_end is not None else 0.0
     prev_end = e
     other_gemm = "gemm_other" in phase
-    if nm.startswith("k_gemm<false, false, true>") and not other_gemm:
+    if nm.startswith("k_gemm<false, false, true") and not other_gemm:   # FUSED (either C form)
         key = "chol"
         chol.append((wg, (e - s) / 1e3, gap))
     elif nm.startswith("k_gemm"):
