@@ -5,10 +5,13 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+# K = 144: 9 K stages, C preloaded; K = 160 (10 stages, the shortest) and 512: the CDEF
+# instances, C added chunk by chunk inside the K loop (csrc/gpemu_kernels.hpp, c_chunk_load)
+@pytest.mark.parametrize("K", [144, 160, 512])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (1, 0), (1, 1), (0, 1)])
-def test_gemm_forms(ctx, ta, tb):
-    rs = np.random.RandomState(ta * 2 + tb)
-    M, N, K = 256, 384, 144
+def test_gemm_forms(ctx, ta, tb, K):
+    rs = np.random.RandomState(ta * 2 + tb + K)
+    M, N = 256, 384
     A = rs.standard_normal((M, K))
     B = rs.standard_normal((K, N))
     C = rs.standard_normal((M, N))
