@@ -618,6 +618,10 @@ __device__ unsigned long long gemm_ttrace[8 * 65536];
 #define TTRACE(slot) do {} while (0)
 #endif
 
+// wave index as a scalar: the compiler treats threadIdx.x >> 6 as divergent, so every
+// wave-derived address (stage loads, LDS destinations, C corner) would be VALU math
+__device__ __forceinline__ int gemm_wave() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 constexpr int GK = 16;
 constexpr int GP = 144;    // [k][m] image of an M-contiguous operand: pitch 144 doubles
 constexpr int GQ = 18;     // [m][k] image of a K-contiguous operand: pitch 18 doubles
@@ -733,28 +737,32 @@ __device__ __forceinline__ void glds16(const double* src, double* lds_base) {
                                    (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
-template <bool AK, bool BK>
-__device__ __forceinline__ void gemm_glds(const double* __restrict__ Ab, const double* __restrict__ Bb,
+// Per-thread source of the stage loads: the lane-dependent part of the address, computed
+// once per tile; each stage then adds a uniform offset (one 64-bit add per load instead of
+// a per-lane 64-bit multiply).  K-contiguous operand: row m = 8 w + (lane >> 3) with
+// w = wave + 4 s, whose swizzle (m >> 1) & 7 = (4 wave + (lane >> 4)) & 7 does not depend
+// on s.
+template <bool K_CONTIG>
+__device__ __forceinline__ const double* glds_lane_base(const double* P, long long ld, int lane, int wave) {
+  if constexpr (!K_CONTIG) return P + 2 * lane + (long long)wave * ld;
+  const int kp = (lane & 7) ^ ((4 * wave + (lane >> 4)) & 7);
+  return P + (long long)(8 * wave + (lane >> 3)) * ld + 2 * kp;
+}
+
+template <bool AK, bool BK, bool SW = true>
+__device__ __forceinline__ void gemm_glds(const double* __restrict__ Al, const double* __restrict__ Bl,
                                           long long lda, long long ldb, int k0, int tid, double* lds,
                                           int buf) {
   double* As = lds + buf * (2 * G_OPND);
   double* Bs = As + G_OPND;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int wave = SW ? gemm_wave() : tid >> 6;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int w = wave + 4 * s;   // wave-instruction index 0..15
-    if (!AK) {
-      glds16(Ab + 2 * lane + (long long)(k0 + w) * lda, As + w * GP);
-    } else {
-      const int m = 8 * w + (lane >> 3), kp = (lane & 7) ^ ((m >> 1) & 7);
-      glds16(Ab + (long long)m * lda + k0 + 2 * kp, As + 8 * w * GK);
-    }
-    if (!BK) {
-      glds16(Bb + 2 * lane + (long long)(k0 + w) * ldb, Bs + w * GP);
-    } else {
-      const int n = 8 * w + (lane >> 3), kp = (lane & 7) ^ ((n >> 1) & 7);
-      glds16(Bb + (long long)n * ldb + k0 + 2 * kp, Bs + 8 * w * GK);
-    }
+    if (!AK) glds16(Al + (long long)(k0 + 4 * s) * lda, As + w * GP);
+    else glds16(Al + (long long)(32 * s) * lda + k0, As + 8 * w * GK);
+    if (!BK) glds16(Bl + (long long)(k0 + 4 * s) * ldb, Bs + w * GP);
+    else glds16(Bl + (long long)(32 * s) * ldb + k0, Bs + 8 * w * GK);
   }
 }
 
@@ -905,14 +913,18 @@ __device__ __forceinline__ void c_chunk_add(d4 (&acc)[4][4], int lane, bool use,
 #else
 #define GEMM_SB() do {} while (0)
 #endif
-template <bool AK, bool BK, bool WIDE = true, bool CDEF = false>
+template <bool AK, bool BK, bool WIDE = true, bool CDEF = false, bool SW = true>
 __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
                                            long long lda, long long ldb, int kbeg, int nk, double* lds,
                                            d4 (&acc)[4][4], bool cuse = false, const double* Cb = nullptr,
                                            long long ldc = 0, double sc = 0.0) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // SW: the wave index as a scalar (gemm_wave); the fused kernel keeps it in a VGPR (with
+  // SGPR wave math its factor / panel paths spill ~100 more VGPRs)
+  const int tid = threadIdx.x, lane = tid & 63, wave = SW ? gemm_wave() : tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   double fa0[4], fb0[4], fa1[4], fb1[4];
+  const double* Al = glds_lane_base<AK>(Ab, lda, lane, wave);   // stage-load sources (gemm_glds)
+  const double* Bl = glds_lane_base<BK>(Bb, ldb, lane, wave);
   double ct0[8], ct1[8];   // CDEF: C chunks in flight (buffer c & 1)
   CSrc csrc;
   if constexpr (CDEF) csrc = c_src<WIDE>(Cb, ldc, lane, wm, wn);
@@ -921,7 +933,7 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
   gemm_gload<AK, BK>(Ab, Bb, lda, ldb, kbeg, tid, ra, rb);
   gemm_sstore<AK, BK>(lds, 0, tid, ra, rb);
 #else
-  gemm_glds<AK, BK>(Ab, Bb, lda, ldb, kbeg, tid, lds, 0);
+  gemm_glds<AK, BK, SW>(Al, Bl, lda, ldb, kbeg, tid, lds, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   __syncthreads();
@@ -939,7 +951,7 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
 #ifdef GEMM_REGSTAGE
     if (more) gemm_gload<AK, BK>(Ab, Bb, lda, ldb, kbeg + (s + 1) * GK, tid, ra, rb);
 #else
-    if (more) gemm_glds<AK, BK>(Ab, Bb, lda, ldb, kbeg + (s + 1) * GK, tid, lds, (s + 1) & 1);
+    if (more) gemm_glds<AK, BK, SW>(Al, Bl, lda, ldb, kbeg + (s + 1) * GK, tid, lds, (s + 1) & 1);
 #endif
     constexpr bool CLOAD = CDEF && CI >= 0 && CI < C_CHUNKS;
     if constexpr (CLOAD) {
@@ -1015,7 +1027,7 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
 // live values push the factor/panel paths past 256 VGPRs (~150 spilled).
 template <bool WIDE = true>
 __device__ __forceinline__ void gemm_store(double* Cb, long long ldc, double alpha, const d4 (&acc)[4][4]) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = WIDE ? gemm_wave() : (int)(threadIdx.x >> 6);   // narrow: fused
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   if constexpr (!WIDE) {
 #pragma unroll
@@ -1130,7 +1142,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
   if (P.flags & G_KEND_TI) kend = min(kend, (ti + 1) * TILE);
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = FUSED ? (tid >> 6) : gemm_wave();   // as gemm_kloop's SW
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   TTRACE(0);
 #ifdef GEMM_TTRACE
@@ -1193,7 +1205,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
       for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
   }
 
-  if (nk > 0) gemm_kloop<AK, BK, !FUSED, CDEF>(Ab, Bb, P.lda, P.ldb, kbeg, nk, lds, acc, cdefer, Cb, P.ldc,
+  if (nk > 0) gemm_kloop<AK, BK, !FUSED, CDEF, !FUSED>(Ab, Bb, P.lda, P.ldb, kbeg, nk, lds, acc, cdefer, Cb, P.ldc,
                                                P.beta / P.alpha);
   TTRACE(2);
 
@@ -1244,7 +1256,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
-      gemm_kloop<false, false>(Cb, P.X, P.ldc, P.ldx, 0, TILE / GK, lds, acc);
+      gemm_kloop<false, false, true, false, false>(Cb, P.X, P.ldc, P.ldx, 0, TILE / GK, lds, acc);
       gemm_store<false>(Cb, P.ldc, 1.0, acc);
       if (ti == 0) GTRACE(P, 7);
       return;
