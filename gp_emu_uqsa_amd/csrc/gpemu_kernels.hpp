@@ -749,20 +749,19 @@ __device__ __forceinline__ const double* glds_lane_base(const double* P, long lo
   return P + (long long)(8 * wave + (lane >> 3)) * ld + 2 * kp;
 }
 
+// Ast / Bst: this stage's lane sources (lane base + the stage's K offset); piece s adds
+// s * sa (sa = 4 ld for an M-contiguous operand, 32 ld for a K-contiguous one).
 template <bool AK, bool BK, bool SW = true>
-__device__ __forceinline__ void gemm_glds(const double* __restrict__ Al, const double* __restrict__ Bl,
-                                          long long lda, long long ldb, int k0, int tid, double* lds,
-                                          int buf) {
+__device__ __forceinline__ void gemm_glds(const double* __restrict__ Ast, const double* __restrict__ Bst,
+                                          long long sa, long long sb, int tid, double* lds, int buf) {
   double* As = lds + buf * (2 * G_OPND);
   double* Bs = As + G_OPND;
   const int wave = SW ? gemm_wave() : tid >> 6;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int w = wave + 4 * s;   // wave-instruction index 0..15
-    if (!AK) glds16(Al + (long long)(k0 + 4 * s) * lda, As + w * GP);
-    else glds16(Al + (long long)(32 * s) * lda + k0, As + 8 * w * GK);
-    if (!BK) glds16(Bl + (long long)(k0 + 4 * s) * ldb, Bs + w * GP);
-    else glds16(Bl + (long long)(32 * s) * ldb + k0, Bs + 8 * w * GK);
+    glds16(Ast + s * sa, AK ? As + 8 * w * GK : As + w * GP);
+    glds16(Bst + s * sb, BK ? Bs + 8 * w * GK : Bs + w * GP);
   }
 }
 
@@ -818,7 +817,8 @@ __device__ __forceinline__ void gemm_mfmas(d4 (&acc)[4][4], const double (&af)[4
 // one stage of slack the chunks stall the loop by as much.  Chunk indices are template
 // constants (the first ten stages are unrolled): no register is indexed at run time.
 // WIDE: the 16-byte form of gemm_store (DPP exchange at the add).
-template <int V> struct gemm_ic { static constexpr int v = V; };
+// stage tag: v = C chunk index (-1: none), p = the stage's buffer parity (-1: from s)
+template <int V, int P = -1> struct gemm_ic { static constexpr int v = V, p = P < 0 ? (V < 0 ? -1 : (V & 1)) : P; };
 constexpr int C_CHUNKS = 8;
 // host: a launch holding this problem uses the CDEF instance of k_gemm (tiles with fewer
 // than C_CHUNKS + 2 stages still preload C there)
@@ -923,8 +923,11 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
   const int tid = threadIdx.x, lane = tid & 63, wave = SW ? gemm_wave() : tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   double fa0[4], fb0[4], fa1[4], fb1[4];
-  const double* Al = glds_lane_base<AK>(Ab, lda, lane, wave);   // stage-load sources (gemm_glds)
-  const double* Bl = glds_lane_base<BK>(Bb, ldb, lane, wave);
+  // stage-load sources (gemm_glds): lane base at kbeg, advanced by one stage of K per stage
+  const long long sa = AK ? 32 * lda : 4 * lda, sb = BK ? 32 * ldb : 4 * ldb;
+  const long long da = AK ? GK : GK * lda, db = BK ? GK : GK * ldb;
+  const double* Al = glds_lane_base<AK>(Ab, lda, lane, wave) + (AK ? kbeg : kbeg * lda);
+  const double* Bl = glds_lane_base<BK>(Bb, ldb, lane, wave) + (BK ? kbeg : kbeg * ldb);
   double ct0[8], ct1[8];   // CDEF: C chunks in flight (buffer c & 1)
   CSrc csrc;
   if constexpr (CDEF) csrc = c_src<WIDE>(Cb, ldc, lane, wm, wn);
@@ -933,7 +936,7 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
   gemm_gload<AK, BK>(Ab, Bb, lda, ldb, kbeg, tid, ra, rb);
   gemm_sstore<AK, BK>(lds, 0, tid, ra, rb);
 #else
-  gemm_glds<AK, BK, SW>(Al, Bl, lda, ldb, kbeg, tid, lds, 0);
+  gemm_glds<AK, BK, SW>(Al, Bl, sa, sb, tid, lds, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   __syncthreads();
@@ -944,14 +947,19 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
   // parameter, not a branch: two inlined K loops in one kernel push the allocator past
   // 256 VGPRs, and run-time branches around the chunks cost the waitcnt pass its counts.
   auto stage = [&](int s, auto cc) {
-    constexpr int CI = decltype(cc)::v;
+    constexpr int CI = decltype(cc)::v, PAR = decltype(cc)::p;
+    const int cur = PAR >= 0 ? PAR : (s & 1), nxt = cur ^ 1;   // this stage's / the next one's buffer
     const bool more = (CI >= 0 && CI + 2 < C_CHUNKS + 2) || s + 1 < nk;   // prologue: nk >= C_CHUNKS + 2
     if constexpr (CI >= 0) __builtin_amdgcn_sched_barrier(0);   // prologue stages stay apart
     if constexpr (CDEF && CI >= 2) c_chunk_add<CI - 2, WIDE>(acc, lane, cuse, sc, (CI & 1) ? ct1 : ct0);
 #ifdef GEMM_REGSTAGE
     if (more) gemm_gload<AK, BK>(Ab, Bb, lda, ldb, kbeg + (s + 1) * GK, tid, ra, rb);
 #else
-    if (more) gemm_glds<AK, BK, SW>(Al, Bl, lda, ldb, kbeg + (s + 1) * GK, tid, lds, (s + 1) & 1);
+    if (more) {
+      Al += da;
+      Bl += db;
+      gemm_glds<AK, BK, SW>(Al, Bl, sa, sb, tid, lds, nxt);
+    }
 #endif
     constexpr bool CLOAD = CDEF && CI >= 0 && CI < C_CHUNKS;
     if constexpr (CLOAD) {
@@ -959,7 +967,7 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
       c_chunk_load<CI, WIDE>(csrc, (CI & 1) ? ct1 : ct0);
       __builtin_amdgcn_sched_barrier(0);
     }
-    const double* As = lds + (s & 1) * (2 * G_OPND);
+    const double* As = lds + cur * (2 * G_OPND);
     const double* Bs = As + G_OPND;
     gemm_frags<AK, BK>(As, Bs, 1, lane, wm, wn, fa1, fb1);
     gemm_mfmas<0, 16>(acc, fa0, fb0);
@@ -974,7 +982,7 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
     GEMM_SB();
     if (more) {
 #ifdef GEMM_REGSTAGE
-      gemm_sstore<AK, BK>(lds, (s + 1) & 1, tid, ra, rb);
+      gemm_sstore<AK, BK>(lds, nxt, tid, ra, rb);
       __syncthreads();
 #else
       // this wave's stage s+1 pieces landed; a chunk issued after them may stay in flight
@@ -986,7 +994,7 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
       // clobber keeps the compiler from moving LDS accesses across
       asm volatile("s_barrier" ::: "memory");
 #endif
-      const double* An = lds + ((s + 1) & 1) * (2 * G_OPND);
+      const double* An = lds + nxt * (2 * G_OPND);
       gemm_frags<AK, BK>(An, An + G_OPND, 0, lane, wm, wn, fa0, fb0);
     }
     GEMM_SB();
@@ -1014,7 +1022,13 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
       s0 = C_CHUNKS + 2;
     }
   }
-  for (int s = s0; s < nk; ++s) stage(s, gemm_ic<-1>{});
+  // s0 is even: the loop runs stage pairs whose buffers are compile-time constants
+  int s = s0;
+  for (; s + 1 < nk; s += 2) {
+    stage(s, gemm_ic<-1, 0>{});
+    stage(s + 1, gemm_ic<-1, 1>{});
+  }
+  if (s < nk) stage(s, gemm_ic<-1, 0>{});
   __syncthreads();   // callers reuse the staging LDS
 }
 
