@@ -751,12 +751,12 @@ __device__ __forceinline__ const double* glds_lane_base(const double* P, long lo
 
 // Ast / Bst: this stage's lane sources (lane base + the stage's K offset); piece s adds
 // s * sa (sa = 4 ld for an M-contiguous operand, 32 ld for a K-contiguous one).
-template <bool AK, bool BK, bool SW = true>
+template <bool AK, bool BK>
 __device__ __forceinline__ void gemm_glds(const double* __restrict__ Ast, const double* __restrict__ Bst,
-                                          long long sa, long long sb, int tid, double* lds, int buf) {
+                                          long long sa, long long sb, double* lds, int buf) {
   double* As = lds + buf * (2 * G_OPND);
   double* Bs = As + G_OPND;
-  const int wave = SW ? gemm_wave() : tid >> 6;
+  const int wave = gemm_wave();   // the LDS targets (M0) are wave-uniform: scalar math
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int w = wave + 4 * s;   // wave-instruction index 0..15
@@ -936,7 +936,7 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
   gemm_gload<AK, BK>(Ab, Bb, lda, ldb, kbeg, tid, ra, rb);
   gemm_sstore<AK, BK>(lds, 0, tid, ra, rb);
 #else
-  gemm_glds<AK, BK, SW>(Al, Bl, sa, sb, tid, lds, 0);
+  gemm_glds<AK, BK>(Al, Bl, sa, sb, lds, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   __syncthreads();
@@ -958,7 +958,7 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
     if (more) {
       Al += da;
       Bl += db;
-      gemm_glds<AK, BK, SW>(Al, Bl, sa, sb, tid, lds, nxt);
+      gemm_glds<AK, BK>(Al, Bl, sa, sb, lds, nxt);
     }
 #endif
     constexpr bool CLOAD = CDEF && CI >= 0 && CI < C_CHUNKS;
