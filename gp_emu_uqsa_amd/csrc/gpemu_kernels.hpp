@@ -19,6 +19,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #include "gpemu_diag.hpp"
 
@@ -823,8 +824,10 @@ constexpr int C_CHUNKS = 8;
 // host: a launch holding this problem uses the CDEF instance of k_gemm (tiles with fewer
 // than C_CHUNKS + 2 stages still preload C there)
 // (ldc bound: the chunk loads' 32-bit buffer offsets reach 64 columns of C)
+// (GPEMU_NO_CDEF=1: dev A/B switch, every launch preloads C)
 inline bool gemm_cdef(const GemmProb& p) {
-  return p.beta != 0.0 && p.K >= (C_CHUNKS + 2) * GK && p.ldc <= (1ll << 21);
+  static const bool off = std::getenv("GPEMU_NO_CDEF") != nullptr;
+  return !off && p.beta != 0.0 && p.K >= (C_CHUNKS + 2) * GK && p.ldc <= (1ll << 21);
 }
 
 // The chunk loads are buffer loads off one per-wave resource (SGPRs), one per-lane byte
@@ -1029,7 +1032,7 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
     stage(s + 1, gemm_ic<-1, 1>{});
   }
   if (s < nk) stage(s, gemm_ic<-1, 0>{});
-  __syncthreads();   // callers reuse the staging LDS
+  if constexpr (!SW) __syncthreads();   // the fused kernel's factor / panel paths reuse the staging LDS
 }
 
 // Epilogue and C preload move 16 B per lane: in the MFMA layout lanes l and l ^ 1 hold
