@@ -1307,15 +1307,14 @@ __device__ __forceinline__ float4 gld4f(const float* p) {
   return make_float4(v.x, v.y, v.z, v.w);
 }
 
-__device__ __forceinline__ void g32_gload(const float* Ab, const float* Bb, long long lda, long long ldb, int k0,
-                                          int tid, float (&ra)[16], float (&rb)[16]) {
+// pa / pb: this thread's sources for the stage (lane part + the stage's K offset, see
+// k_gemm_f32); piece u adds u * sa (sa = 8 lda: k rows) / u * sb (sb = 32 ldb: n rows)
+__device__ __forceinline__ void g32_gload(const float* pa, const float* pb, long long sa, long long sb,
+                                          float (&ra)[16], float (&rb)[16]) {
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
-    const int c = tid + 256 * u;
-    const int kk = c >> 5, mm = (c & 31) * 4;
-    const float4 a = gld4f(Ab + mm + (long long)(k0 + kk) * lda);
-    const int nn = c >> 3, k2 = (c & 7) * 4;
-    const float4 b = gld4f(Bb + (long long)nn * ldb + k0 + k2);
+    const float4 a = gld4f(pa + u * sa);
+    const float4 b = gld4f(pb + u * sb);
     ra[4 * u] = a.x; ra[4 * u + 1] = a.y; ra[4 * u + 2] = a.z; ra[4 * u + 3] = a.w;
     rb[4 * u] = b.x; rb[4 * u + 1] = b.y; rb[4 * u + 2] = b.z; rb[4 * u + 3] = b.w;
   }
@@ -1381,8 +1380,13 @@ static __global__ void __launch_bounds__(256, 2) k_gemm_f32(const float* A, long
         acc[u >> 2][u & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(bf[u & 3], af[u >> 2], acc[u >> 2][u & 3], 0, 0, 0);
   };
   float fa0[4], fb0[4], fa1[4], fb1[4];
+  // stage-load sources: lane part once per tile (A: k row tid >> 5, m (tid & 31) * 4; B: n row
+  // tid >> 3, k (tid & 7) * 4), then one uniform step of F32_GK per stage
+  const float* pa = Ab + (tid & 31) * 4 + (long long)(tid >> 5) * lda;
+  const float* pb = Bb + (long long)(tid >> 3) * ldb + (tid & 7) * 4;
+  const long long sa = 8 * lda, sb = 32 * ldb, da = F32_GK * lda;
   if (nk > 0) {
-    g32_gload(Ab, Bb, lda, ldb, 0, tid, ra, rb);
+    g32_gload(pa, pb, sa, sb, ra, rb);
     g32_sstore(lds32, tid, ra, rb);
     __syncthreads();
     frags(lds32, lds32 + F32_GK * F32_PA, 0, fa0, fb0);
@@ -1391,10 +1395,16 @@ static __global__ void __launch_bounds__(256, 2) k_gemm_f32(const float* A, long
   // the 16 MFMAs of k-step ks issue, so their LDS latency hides behind them; at the
   // stage boundary the last 4 MFMAs wait until the next stage's first fragments
   // are in flight.  sched_barrier keeps the compiler from regrouping.
-  for (int s = 0; s < nk; ++s) {
+  // stages run in pairs so each stage's buffer is a compile-time constant (as gemm_kloop)
+  auto stage = [&](int s, auto par) {
+    constexpr int cur = decltype(par)::v, nxt = cur ^ 1;
     const bool more = s + 1 < nk;
-    if (more) g32_gload(Ab, Bb, lda, ldb, (s + 1) * F32_GK, tid, ra, rb);
-    const float* As = lds32 + (s & 1) * F32_STAGE;
+    if (more) {
+      pa += da;
+      pb += F32_GK;
+      g32_gload(pa, pb, sa, sb, ra, rb);
+    }
+    const float* As = lds32 + cur * F32_STAGE;
     const float* Bs = As + F32_GK * F32_PA;
 #pragma unroll
     for (int ks = 0; ks < F32_GK / 4; ks += 2) {
@@ -1412,15 +1422,21 @@ static __global__ void __launch_bounds__(256, 2) k_gemm_f32(const float* A, long
     mfmas(0, 12, fa1, fb1);
     __builtin_amdgcn_sched_barrier(0);
     if (more) {
-      g32_sstore(lds32 + ((s + 1) & 1) * F32_STAGE, tid, ra, rb);
+      g32_sstore(lds32 + nxt * F32_STAGE, tid, ra, rb);
       __syncthreads();
-      const float* An = lds32 + ((s + 1) & 1) * F32_STAGE;
+      const float* An = lds32 + nxt * F32_STAGE;
       frags(An, An + F32_GK * F32_PA, 0, fa0, fb0);
     }
     __builtin_amdgcn_sched_barrier(0);
     mfmas(12, 16, fa1, fb1);
     __builtin_amdgcn_sched_barrier(0);
+  };
+  int s = 0;
+  for (; s + 1 < nk; s += 2) {
+    stage(s, gemm_ic<0>{});
+    stage(s + 1, gemm_ic<1>{});
   }
+  if (s < nk) stage(s, gemm_ic<0>{});
   float* Cb = C + (long long)ti * TILE + (long long)tj * TILE * ldc;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
