@@ -819,6 +819,9 @@ __device__ __forceinline__ void gemm_mfmas(d4 (&acc)[4][4], const double (&af)[4
 // constants (the first ten stages are unrolled): no register is indexed at run time.
 // WIDE: the 16-byte form of gemm_store (DPP exchange at the add).
 // stage tag: v = C chunk index (-1: none), p = the stage's buffer parity (-1: from s)
+#ifndef GEMM_HOLD
+#define GEMM_HOLD 12   // MFMAs of a stage's last k-step issued before its barrier (the rest after)
+#endif
 template <int V, int P = -1> struct gemm_ic { static constexpr int v = V, p = P < 0 ? (V < 0 ? -1 : (V & 1)) : P; };
 constexpr int C_CHUNKS = 8;
 // host: a launch holding this problem uses the CDEF instance of k_gemm (tiles with fewer
@@ -981,7 +984,7 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
     gemm_frags<AK, BK>(As, Bs, 3, lane, wm, wn, fa1, fb1);
     gemm_mfmas<0, 16>(acc, fa0, fb0);
     GEMM_SB();
-    gemm_mfmas<0, 12>(acc, fa1, fb1);
+    gemm_mfmas<0, GEMM_HOLD>(acc, fa1, fb1);
     GEMM_SB();
     if (more) {
 #ifdef GEMM_REGSTAGE
@@ -1001,7 +1004,7 @@ __device__ __forceinline__ void gemm_kloop(const double* Ab, const double* Bb,
       gemm_frags<AK, BK>(An, An + G_OPND, 0, lane, wm, wn, fa0, fb0);
     }
     GEMM_SB();
-    gemm_mfmas<12, 16>(acc, fa1, fb1);
+    gemm_mfmas<GEMM_HOLD, 16>(acc, fa1, fb1);
     GEMM_SB();
     if constexpr (CI >= 0) __builtin_amdgcn_sched_barrier(0);
   };
