@@ -16,10 +16,12 @@ and the max over ranks go through gp_emu_uqsa_amd/rendezvous.py, device
 synchronisation through libgpemu.so.  The headline runs one replica per GPU
 (independent multistart evaluations, no data-path collective; value =
 evaluations by all ranks / the slowest rank's time).  With N > 1 the line also
-carries `extra.rowblock`: BASELINE configs[3] (n=65536, d=20) LLH + gradient as
-ONE evaluation spread over the N GPUs by the row-block distributed objective
-over RCCL (include/gpemu_dist.h), its collective time, and a rank-0 parity check
-against the single-GPU objective.
+carries two row-block legs, each ONE LLH + gradient spread over the N GPUs by the
+row-block distributed objective over RCCL (include/gpemu_dist.h), with its
+collective time and a rank-0 parity check against the single-GPU objective:
+`extra.rowblock_metric` at the metric's own configuration (n=16384, d=10: the
+strong-scaling latency of one evaluation against N) and `extra.rowblock` at
+BASELINE configs[3] (n=65536, d=20).
 
 Also reported: the roofline of the dominant kernel (the MFMA GEMM: algorithmic
 flops per launch / mean launch time from HIP events on its own stream, recorded
@@ -72,6 +74,10 @@ def parse(argv=None):
     ap.add_argument("--rowblock-n", type=int, default=C4[0])
     ap.add_argument("--rowblock-d", type=int, default=C4[1])
     ap.add_argument("--rowblock-steps", type=int, default=2)
+    ap.add_argument("--rowblock-metric-steps", type=int, default=5,
+                    help="N > 1: timed evaluations of the metric-config row-block leg (strong scaling)")
+    ap.add_argument("--no-rowblock-metric", dest="rowblock_metric", action="store_false",
+                    help="N > 1: skip the metric-config row-block leg")
     ap.add_argument("--rowblock-timeout", type=float, default=300.0)
     ap.add_argument("--rendezvous-check", action="store_true",
                     help="(test hook) spawn / rendezvous only: no GPU, rank 0 prints the ranks it saw")
@@ -286,13 +292,14 @@ def other_configs(native, synthetic, ctx, args):
     return out
 
 
-def rowblock_leg(native, synthetic, group, rank, world, local, args, sync_all):
-    """configs[3]: one LLH+gradient (and one value-only evaluation) of n x n spread
-    over the `world` GPUs by the row-block distributed objective over RCCL; time =
-    max over ranks; rank 0 then checks value and gradient against the single-GPU
-    objective (tolerances as tests/test_gpu_fullsize.py)."""
+def rowblock_leg(native, synthetic, group, rank, world, local, args, sync_all, n, d, steps, what):
+    """One LLH+gradient (and one value-only evaluation) of n x n spread over the
+    `world` GPUs by the row-block distributed objective over RCCL; time = max over
+    ranks; rank 0 then checks value and gradient against the single-GPU objective
+    (tolerances as tests/test_gpu_fullsize.py).  Run for configs[3] (n=65536, d=20)
+    and for the metric's own configuration (n=16384, d=10: single-evaluation latency
+    against N)."""
     from gp_emu_uqsa_amd import distributed
-    n, d = args.rowblock_n, args.rowblock_d
     X, f, H = synthetic.problem(n, d, seed=0)
     hp = eval_point(d, 0)
     dc = distributed.dist_context(local, group)
@@ -301,11 +308,11 @@ def rowblock_leg(native, synthetic, group, rank, world, local, args, sync_all):
     sync_all()
     t0 = time.perf_counter()
     comm = []
-    for _ in range(args.rowblock_steps):
+    for _ in range(steps):
         llh, g, _ = dc.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=True)
         comm.append(dc.times()["comm_ms"])
     sync_all()
-    t_grad = group.all_reduce_max((time.perf_counter() - t0) / args.rowblock_steps)
+    t_grad = group.all_reduce_max((time.perf_counter() - t0) / steps)
     t0 = time.perf_counter()
     dc.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=False)
     sync_all()
@@ -322,10 +329,11 @@ def rowblock_leg(native, synthetic, group, rank, world, local, args, sync_all):
         rel_llh = abs(llh - ref) / abs(ref)
         rel_g = float(np.max(np.abs(np.asarray(g) - gref)) / np.max(np.abs(gref)))
         flops = float(n) ** 3   # algorithmic: n^3/3 each for POTRF, TRTRI and the A^-1 partials
-        out = {"config": f"BASELINE configs[3]: gp4ml LLH+grad n={n} d={d}, one evaluation over {world} GPUs "
+        out = {"config": f"{what}: gp4ml LLH+grad n={n} d={d}, one evaluation over {world} GPUs "
                          f"(row-block cyclic tile rows, RCCL)",
                "n": n, "d": d, "ranks": world,
-               "llh_grad_ms": 1000.0 * t_grad, "value_only_ms": 1000.0 * t_val,
+               "llh_grad_ms": 1000.0 * t_grad, "llh_grad_evals_per_s": 1.0 / t_grad,
+               "value_only_ms": 1000.0 * t_val,
                "comm_ms_llh_grad": float(np.mean(comm)), "comm_ms_value_only": comm_val,
                "algorithmic_tflops": flops / t_grad / 1e12,
                "per_rank_device_gb": rank_gb,
@@ -346,7 +354,7 @@ def emit(out):
             print(json.dumps(out), flush=True)
 
 
-def guarded_rowblock(native, synthetic, group, rank, world, local, args, sync_all, out):
+def guarded_rowblock(native, synthetic, group, rank, world, local, args, sync_all, out, key, n, d, steps, what):
     """rowblock_leg behind a pre-flight check and a watchdog, so that the headline
     line survives a row-block failure: every rank first reports whether its GPU is
     visible; a failure on any rank makes all skip; an exception is recorded; and if
@@ -364,18 +372,25 @@ def guarded_rowblock(native, synthetic, group, rank, world, local, args, sync_al
         if done.wait(args.rowblock_timeout):
             return
         if rank == 0:
-            out.setdefault("extra", {})["rowblock"] = {"error": f"timed out after {args.rowblock_timeout:.0f} s"}
+            out.setdefault("extra", {})[key] = {"error": f"timed out after {args.rowblock_timeout:.0f} s"}
             emit(out)
         sys.stdout.flush()
         os._exit(0 if rank == 0 else 3)
 
     threading.Thread(target=watchdog, daemon=True).start()
+    from gp_emu_uqsa_amd import rendezvous
     try:
-        res = rowblock_leg(native, synthetic, group, rank, world, local, args, sync_all)
+        res = rowblock_leg(native, synthetic, group, rank, world, local, args, sync_all, n, d, steps, what)
         err = None
+    except rendezvous.RendezvousAborted as e:   # a peer failed: its message
+        res, err = None, str(e)
     except Exception as e:   # recorded in the line; the headline stands
         res, err = None, f"{type(e).__name__}: {e}"
-    errs = [e for e in group.all_gather(err) if e]
+        group.abort(err)     # peers waiting in a file collective raise with this message
+    try:
+        errs = [e for e in group.all_gather(err) if e] if group.aborted is None else [group.aborted]
+    except rendezvous.RendezvousAborted as e:
+        errs = [str(e)]
     done.set()
     if errs:
         return {"error": errs[0]}
@@ -556,9 +571,23 @@ def main(argv=None):
         for c in ctxs:          # the replica workspaces are not needed by the row-block leg
             c.close()
         ctxs = []
-        rb = guarded_rowblock(native, synthetic, group, rank, world, local, args, sync_all, out)
-        if rank == 0:
-            out.setdefault("extra", {})["rowblock"] = rb
+        # strong scaling of the metric's own unit first (one n=16384 evaluation over N
+        # GPUs), then configs[3]; each leg guarded on its own
+        legs = [("rowblock_metric", args.n, args.d, args.rowblock_metric_steps,
+                 "metric configuration (strong scaling of one evaluation)"),
+                ("rowblock", args.rowblock_n, args.rowblock_d, args.rowblock_steps, "BASELINE configs[3]")]
+        for key, n_, d_, steps_, what in legs:
+            if not args.rowblock_metric and key == "rowblock_metric":
+                continue
+            rb = guarded_rowblock(native, synthetic, group, rank, world, local, args, sync_all, out,
+                                  key, n_, d_, steps_, what)
+            if rank == 0:
+                out.setdefault("extra", {})[key] = rb
+                if key == "rowblock_metric" and isinstance(rb, dict) and rb.get("llh_grad_ms"):
+                    rb["single_gpu_single_eval_ms"] = 1000.0 * single_s
+                    rb["speedup_vs_single_gpu"] = 1000.0 * single_s / rb["llh_grad_ms"]
+            if group.aborted is not None:
+                break
     if rank == 0:
         emit(out)
     for c in ctxs:

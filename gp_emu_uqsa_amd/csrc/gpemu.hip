@@ -66,6 +66,7 @@ struct Fact {
   size_t cap = 0;
   double* logdet = nullptr;  // NB per-block log-determinant parts
   int* flags = nullptr;      // NB diagonal-inverse ready flags (fused Cholesky)
+  int* tflags = nullptr;     // NB tile-row flags of the forward substitution (k_trsv_lower)
   int desc_base = 0;         // first slot of its descriptors in the device array
   Plan plan;
 };
@@ -150,6 +151,7 @@ struct gpe_ctx {
 
   // resident factor (gpe_factor)
   bool factor_valid = false;
+  bool linv_valid = false;   // tr.B holds L^-1 (TRTRI of the resident L; run on demand)
   bool ainv_valid = false;   // tr.A holds A^-1 (LAUUM of the resident L^-1)
   int f_kernel = 0;
   std::vector<double> f_delta;
@@ -621,6 +623,7 @@ int ensure_fact(gpe_ctx* c, Fact& F, long long n_pad) {
     F.NB = (int)(n_pad / TILE);
     CHK(dalloc(c, &F.logdet, (size_t)F.NB));
     CHK(dalloc(c, &F.flags, (size_t)F.NB));
+    CHK(dalloc(c, &F.tflags, (size_t)F.NB));
     F.plan = Plan();
   }
   return GPE_OK;
@@ -856,8 +859,13 @@ void ev_rec(gpe_ctx* c, int i) {
   if (c->prof) hipEventRecord(c->ev[i], c->stream);
 }
 
+// K-build and Cholesky of the training matrix; with invert, also X = L^-1 (TRTRI) into
+// tr.B.  Without it tr.B keeps only the diagonal-tile inverses, which is all the forward
+// substitution (trsv_lower) needs: the value-only objective and gpe_beta skip the n^3/3
+// flops of the inverse, and the posterior-side entries run it on demand (ensure_linv).
 int factor_and_invert(gpe_ctx* c, int kernel, const double* delta, double nu, double s2,
-                      double rscale) {
+                      double rscale, bool invert = true) {
+  c->linv_valid = false;
   HIPCHK(c, hipMemsetAsync(c->dinfo, 0, sizeof(int), c->stream));
   CHK(build_plan(c, c->tr));
   ev_rec(c, 0);
@@ -866,8 +874,33 @@ int factor_and_invert(gpe_ctx* c, int kernel, const double* delta, double nu, do
   ev_rec(c, 1);
   CHK(potrf(c, c->tr));
   ev_rec(c, 2);
-  CHK(trtri(c, c->tr));
+  if (invert) {
+    CHK(trtri(c, c->tr));
+    c->linv_valid = true;
+  }
   ev_rec(c, 3);
+  return GPE_OK;
+}
+
+// X = L^-1 of the resident factor into tr.B if the factorisation skipped it
+int ensure_linv(gpe_ctx* c) {
+  if (c->linv_valid) return GPE_OK;
+  CHK(trtri(c, c->tr));
+  c->linv_valid = true;
+  c->x32_valid = false;
+  return GPE_OK;
+}
+
+// Y = L^-1 R (n_pad x P, column-major) from the Cholesky factor in F.A and the diagonal
+// inverses in F.B: k_trsv_lower, one launch per TS_PM columns
+int trsv_lower(gpe_ctx* c, Fact& F, const double* R, long long ldr, int P, double* Y, long long ldy) {
+  for (int c0 = 0; c0 < P; c0 += TS_PM) {
+    const int pc = std::min(TS_PM, P - c0);
+    HIPCHK(c, hipMemsetAsync(F.tflags, 0, (size_t)F.NB * sizeof(int), c->stream));
+    hipLaunchKernelGGL(k_trsv_lower, dim3(F.NB), dim3(512), 0, c->stream, F.A, (long long)F.n_pad, F.B,
+                       R + (long long)c0 * ldr, ldr, Y + (long long)c0 * ldy, ldy, pc, F.tflags, c->dinfo);
+    HIPCHK(c, hipGetLastError());
+  }
   return GPE_OK;
 }
 
@@ -1001,6 +1034,8 @@ void gpe_destroy(gpe_ctx* c) {
   if (c->dK32) hipFree(c->dK32);
   if (c->tr.flags) hipFree(c->tr.flags);
   if (c->aux.flags) hipFree(c->aux.flags);
+  if (c->tr.tflags) hipFree(c->tr.tflags);
+  if (c->aux.tflags) hipFree(c->aux.tflags);
   if (c->dprobs) hipFree(c->dprobs);
   if (c->dtiles) hipFree(c->dtiles);
   if (c->hpin) hipHostFree(c->hpin);
@@ -1118,12 +1153,16 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
     c->gemm_launches = c->gemm_flops = c->gemm_ms = 0.0;
   }
 
-  CHK(factor_and_invert(c, kernel, hp, nu, s2, rscale));
+  // value only: no L^-1 (forward substitution with the diagonal inverses instead)
+  CHK(factor_and_invert(c, kernel, hp, nu, s2, rscale, want_grad != 0));
   // z, w = L^-1 [f H]
   const int P = q + 1;
   const long long np = c->n_pad;
   const int NBt = c->tr.NB;
-  CHK(skinny(c, false, c->tr.B, np, c->NB, c->NB, true, c->dF, np, P, c->dZ, np));
+  if (want_grad)
+    CHK(skinny(c, false, c->tr.B, np, c->NB, c->NB, true, c->dF, np, P, c->dZ, np));
+  else
+    CHK(trsv_lower(c, c->tr, c->dF, np, P, c->dZ, np));
   // Gram, log-determinant parts and the failure flag go to the host behind an event;
   // A^-1 = L^-T L^-1 (22 ms at n=16384, independent of the host algebra) is queued
   // before the host waits, so the GPU does not idle over the round trip
@@ -1238,7 +1277,7 @@ int gpe_factor(gpe_ctx* c, int32_t kernel, const double* delta, double nu, doubl
   c->factor_valid = false;
   c->ainv_valid = false;
   c->x32_valid = false;
-  CHK(factor_and_invert(c, kernel, delta, nu, s2, r_scale));
+  CHK(factor_and_invert(c, kernel, delta, nu, s2, r_scale, false));   // L^-1 on demand
   int info = 0;
   double logdet = 0.0;
   CHK(read_info_logdet(c, c->tr, &info, &logdet));
@@ -1266,6 +1305,7 @@ static int grow(gpe_ctx* c, double** p, size_t* cap, size_t need) {
 // A^-1 = L^-T L^-1 of the resident factor into tr.A (the LAUUM launch of the plan)
 static int ensure_ainv(gpe_ctx* c) {
   if (c->ainv_valid) return GPE_OK;
+  CHK(ensure_linv(c));
   CHK(launch_gemm_range(c, c->tr.plan.launches[c->tr.plan.lauum]));
   c->ainv_valid = true;
   return GPE_OK;
@@ -1275,6 +1315,7 @@ int gpe_solve(gpe_ctx* c, int32_t ncols, const double* B, double* X) {
   CHK(check_ready(c));
   if (!c->factor_valid) return fail(c, GPE_ERR_STATE, "no resident factor (call gpe_factor)");
   if (ncols <= 0 || !B || !X) return fail(c, GPE_ERR_ARG, "bad solve args");
+  CHK(ensure_linv(c));
   const long long np = c->n_pad, n = c->n;
   for (int c0 = 0; c0 < ncols; c0 += SK_PMAX) {
     const int cc = std::min(SK_PMAX, ncols - c0);
@@ -1391,7 +1432,10 @@ int gpe_beta(gpe_ctx* c, double* beta_out) {
   if (!c->factor_valid) return fail(c, GPE_ERR_STATE, "no resident factor (call gpe_factor)");
   const int P = c->q + 1;
   const long long np = c->n_pad;
-  CHK(skinny(c, false, c->tr.B, np, c->NB, c->NB, true, c->dF, np, P, c->dZ, np));
+  if (c->linv_valid)
+    CHK(skinny(c, false, c->tr.B, np, c->NB, c->NB, true, c->dF, np, P, c->dZ, np));
+  else
+    CHK(trsv_lower(c, c->tr, c->dF, np, P, c->dZ, np));
   std::vector<double> G((size_t)P * P);
   CHK(gram(c, c->dZ, np, P, (int)np, G.data()));
   SmallAlgebra sa = small_from_gram(G, P);
@@ -1414,6 +1458,7 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
   if (keep_dev && (!full_var || m > 16384)) return fail(c, GPE_ERR_ARG, "device-resident variance: full, m <= 16384");
   if (precision != 64 && precision != 32) return fail(c, GPE_ERR_ARG, "precision must be 64 or 32");
   if (precision == 32 && full_var) return fail(c, GPE_ERR_UNSUPPORTED, "precision 32 is for the diagonal variance");
+  CHK(ensure_linv(c));
   const bool f32 = precision == 32;
   const int d = c->d, q = c->q, P = q + 1;
   const long long np = c->n_pad;

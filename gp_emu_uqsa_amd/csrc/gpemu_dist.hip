@@ -1154,6 +1154,10 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
   if (variant != GPE_GP4ML && variant != GPE_MUCM) return dfail(h, GPE_ERR_ARG, "bad variant");
   if (kernel != GPE_KERNEL_STD && kernel != GPE_KERNEL_ALT_NUG) return dfail(h, GPE_ERR_ARG, "bad kernel");
   DCHK_HIP(h, hipSetDevice(h->device));
+  // a previous call that failed inside group_sweep may have left chain work queued on the
+  // critical stream, never joined into the compute stream: drain it before this call's
+  // host staging and memsets (idle in the normal case)
+  DCHK_HIP(h, hipStreamSynchronize(h->crit));
   const int d = h->d, q = h->q, Pc = q + 1, P = h->P, NB = h->NB;
   const long long np = h->n_pad;
   const bool gp4ml = variant == GPE_GP4ML;

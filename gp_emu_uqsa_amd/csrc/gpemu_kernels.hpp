@@ -1183,7 +1183,9 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
   double* Cb = P.C + (long long)ti * TILE + (long long)tj * TILE * P.ldc;
   const int nk = (kend - kbeg) / GK;
   // beta != 0 with >= 10 stages: C is added chunk by chunk inside the K loop (c_chunk_load)
-  const bool cdefer = CDEF && P.beta != 0.0 && nk >= C_CHUNKS + 2;
+  // (the ldc bound of gemm_cdef again: the chunk loads' 32-bit buffer offsets; a CDEF
+  // launch may mix problems, and one over the bound preloads C instead)
+  const bool cdefer = CDEF && P.beta != 0.0 && nk >= C_CHUNKS + 2 && P.ldc <= (1ll << 21);
   d4 acc[4][4];
   if (cdefer) {
 #pragma unroll
@@ -1597,6 +1599,139 @@ static __global__ void __launch_bounds__(256) k_trmm_skinny_t(SkinnyArgs a) {
     for (int p = 0; p < PM; ++p)
       if (p < P) out[(long long)p * a.ldp] = acc[p] + red[c * PM + p];
   }
+}
+
+// ---------------------------------------------------------------------------
+// Z = L^-1 F by blocked forward substitution, without forming L^-1: the value-only
+// objective and gpe_beta need only L, L^-1 f and L^-1 H (_emulatoroptimise.py:382-408,
+// :425-442, :497-504).  L lower by 128-row tiles (ld), D_t = L_tt^-1 the diagonal-tile
+// inverses the fused Cholesky leaves in the second buffer (Dinv, ld), F / Z column-major
+// n_pad x P (P <= TS_PM; the host runs wider F in column chunks).
+// One workgroup per tile row i: acc = F_i - sum_{j<i} L_ij Z_j, taking each Z_j as soon
+// as row j published flags[j], then Z_i = D_i acc, published on flags[i].  Rows publish
+// in order, so a set flags[i-1] means every earlier one is set, and every wait is on a
+// workgroup dispatched before the waiting one (no dispatch-order deadlock).
+// Thread (r, h), 512 threads: row r of the tile row, k quarter h of every 128 x 128 x P
+// product (L_ij's 32 values are loaded before the wait; D_i's 32 are held from the
+// start), partial sums combined through LDS.  L is read once (n^2/2 x 8 B, HBM-bound);
+// the chain per tile row is one flag hop, the Z_{i-1} staging, one tile product and the
+// D_i product (~1.7 us each at one CU's fp64 rate).
+// ---------------------------------------------------------------------------
+constexpr int TS_PM = 16;
+constexpr int TS_Q = 4;             // k quarters
+constexpr int TS_KQ = TILE / TS_Q;  // 32
+
+// sum the TS_Q quarters' v[PM] into quarter 0's threads (two tree rounds through LDS
+// buffers b0, b1, each TILE x PM; callers sync before reusing them)
+__device__ __forceinline__ void ts_reduce(double (&v)[TS_PM], double* b0, double* b1, int r, int h) {
+  if (h >= 2) {
+    double* b = (h == 2) ? b0 : b1;
+#pragma unroll
+    for (int p = 0; p < TS_PM; ++p) b[r * TS_PM + p] = v[p];
+  }
+  __syncthreads();
+  if (h < 2) {
+    const double* b = (h == 0) ? b0 : b1;
+#pragma unroll
+    for (int p = 0; p < TS_PM; ++p) v[p] += b[r * TS_PM + p];
+  }
+  __syncthreads();
+  if (h == 1) {
+#pragma unroll
+    for (int p = 0; p < TS_PM; ++p) b0[r * TS_PM + p] = v[p];
+  }
+  __syncthreads();
+  if (h == 0) {
+#pragma unroll
+    for (int p = 0; p < TS_PM; ++p) v[p] += b0[r * TS_PM + p];
+  }
+}
+
+static __global__ void __launch_bounds__(512) k_trsv_lower(const double* __restrict__ L, long long ld,
+                                                   const double* __restrict__ Dinv,
+                                                   const double* __restrict__ F, long long ldf, double* Z,
+                                                   long long ldz, int P, int* flags, int* abort_flag) {
+  constexpr int PM = TS_PM, KQ = TS_KQ;
+  __shared__ double Zs[2][TILE * PM];   // [k][p]; after the loop: reduction buffers
+  __shared__ int st;
+  if (abort_flag && *abort_flag) return;   // set by an earlier launch: every workgroup sees it
+  const int i = blockIdx.x;
+  const int tid = threadIdx.x, r = tid & (TILE - 1), h = tid >> 7;
+  // D_i(r, k) for this thread's k quarter (the upper triangle is stored as zeros)
+  double dv[KQ];
+  {
+    const double* drow = Dinv + (long long)i * TILE + r + (long long)(i * TILE + h * KQ) * ld;
+#pragma unroll
+    for (int k = 0; k < KQ; ++k) dv[k] = drow[(long long)k * ld];
+  }
+  double acc[PM];
+  const double* frow = F + (long long)i * TILE + r;
+#pragma unroll
+  for (int p = 0; p < PM; ++p) acc[p] = (h == 0 && p < P) ? frow[(long long)p * ldf] : 0.0;
+  const double* lrow = L + (long long)i * TILE + r + (long long)(h * KQ) * ld;
+  int ready = -1;   // flags[0..ready] known set
+  for (int j = 0; j < i; ++j) {
+    double lv[KQ];
+    const double* lt = lrow + (long long)j * TILE * ld;
+#pragma unroll
+    for (int k = 0; k < KQ; ++k) lv[k] = lt[(long long)k * ld];
+    if (tid == 0 && j > ready) {
+      int v = gemm_wait_flag(flags + j);
+      if (v == 1) {
+        ready = j;
+        if (j + 1 < i && __hip_atomic_load(flags + i - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          ready = i - 1;
+        }
+      }
+      st = v;
+    }
+    __syncthreads();
+    if (st != 1) {   // a failed or timed-out row: report once, stop
+      if (tid == 0 && st == 0 && abort_flag) atomicCAS(abort_flag, 0, GEMM_WAIT_TIMEOUT);
+      return;
+    }
+    double* zs = Zs[j & 1];
+    for (int e = tid; e < TILE * PM; e += 512) {
+      const int kk = e & (TILE - 1), p = e >> 7;
+      zs[kk * PM + p] = p < P ? Z[(long long)j * TILE + kk + (long long)p * ldz] : 0.0;
+    }
+    __syncthreads();
+    const double* zh = zs + h * KQ * PM;
+#pragma unroll   // lv stays in registers only when every index is a constant
+    for (int k = 0; k < KQ; ++k) {
+      const double x = lv[k];
+#pragma unroll
+      for (int p = 0; p < PM; ++p) acc[p] = fma(-x, zh[k * PM + p], acc[p]);
+    }
+  }
+  __syncthreads();
+  ts_reduce(acc, Zs[0], Zs[1], r, h);   // the full acc in quarter 0
+  double* S = Zs[1];                    // acc as [k][p]
+  if (h == 0) {
+#pragma unroll
+    for (int p = 0; p < PM; ++p) S[r * PM + p] = acc[p];
+  }
+  __syncthreads();
+  // Z_i(r, p) = sum_k D_i(r, k) S(k, p): quarter h takes k in [h KQ, h KQ + KQ)
+  double out[PM];
+#pragma unroll
+  for (int p = 0; p < PM; ++p) out[p] = 0.0;
+  const double* sh = S + h * KQ * PM;
+#pragma unroll
+  for (int k = 0; k < KQ; ++k)
+#pragma unroll
+    for (int p = 0; p < PM; ++p) out[p] = fma(dv[k], sh[k * PM + p], out[p]);
+  __syncthreads();   // every quarter has read S
+  ts_reduce(out, Zs[0], Zs[1], r, h);
+  if (h == 0) {
+#pragma unroll
+    for (int p = 0; p < PM; ++p)
+      if (p < P) Z[(long long)i * TILE + r + (long long)p * ldz] = out[p];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) gemm_publish_flag(flags + i, 1);
 }
 
 // MFMA form of the skinny products (same grid, chunks and partial layout as the

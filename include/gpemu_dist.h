@@ -22,8 +22,9 @@
  * [sqrt(c) alpha, W] and of the d+2 contraction sums.
  *
  * Processes: one per GPU.  Rank 0 calls gpe_dist_unique_id, the host shares the
- * 128 bytes (torch.distributed / gloo in gp_emu_uqsa_amd/distributed.py), every
- * rank calls gpe_dist_create with it.  unique_id == NULL selects the in-process
+ * 128 bytes (by default through the job's native file rendezvous,
+ * gp_emu_uqsa_amd/rendezvous.py init_from_env(); a torch.distributed group is the
+ * alternative, distributed.share_unique_id), every rank calls gpe_dist_create with it.  unique_id == NULL selects the in-process
  * loopback transport: all P logical ranks live in this process on one GPU, each
  * with its own buffers, running the same partition, schedule and device code
  * (pack, all-gather buffer, unpermute, broadcast rows, all-reduced partials);

@@ -8,7 +8,9 @@ compares them.  All ranks may sit on one GPU: the test gives every rank its own
 NCCL_HOSTID, so RCCL treats them as separate hosts (socket transport over the
 loopback interface) instead of refusing a second rank on the same device.
 
-usage: RANK=r WORLD_SIZE=P GPEMU_RDZV_DIR=... python tests/rccl_worker.py n d
+usage: RANK=r WORLD_SIZE=P GPEMU_RDZV_DIR=... python tests/rccl_worker.py n d [one]
+("one": only the gp4ml std case, value + gradient once, and no non-PD case: the
+full-size C4 run)
 """
 import json
 import os
@@ -38,16 +40,22 @@ def cases(d, n):
 
 def main():
     n, d = int(sys.argv[1]), int(sys.argv[2])
-    group = rendezvous.init_from_env(timeout=180.0)
+    one = len(sys.argv) > 3 and sys.argv[3] == "one"
+    group = rendezvous.init_from_env(timeout=600.0)
     rank, world = group.rank, group.world_size
     X, f, H = synthetic.problem(n, d, seed=3)
     dc = distributed.dist_context(0, group)
     out = {"ranks": world, "n": n, "d": d, "cases": {}}
-    for name, variant, kernel, hp, nu, r in cases(d, n):
+    for name, variant, kernel, hp, nu, r in cases(d, n)[:1 if one else None]:
         dc.set_data(X, f, H, r)
         llh_v, s2_v = dc.objective(variant, kernel, hp, nu)
         llh, g, s2 = dc.objective(variant, kernel, hp, nu, want_grad=True)
         rec = {"llh_value_only": llh_v, "llh": llh, "grad": list(map(float, g)), "sigma2": s2}
+        rec["rank_gb"] = group.all_gather(dc.rank_bytes() / 1e9)
+        if one:   # free this rank's rows before rank 0 holds the single-GPU n x n buffers
+            out["comm_ms"] = dc.times()["comm_ms"]
+            dc.close()
+            group.barrier()
         if rank == 0:
             c = native.Context(0)
             c.set_data(X, f, H, r)
@@ -55,20 +63,21 @@ def main():
             c.close()
             rec.update(ref_llh=ref, ref_grad=list(map(float, gref)), ref_sigma2=s2ref)
         out["cases"][name] = rec
-    # a matrix that is not positive definite (a duplicated point, no nugget): every
-    # rank must report it, through the all-reduced failure flag
-    Xd = X.copy()
-    Xd[1] = Xd[0]
-    dc.set_data(Xd, f, H)
-    try:
-        dc.objective(native.GP4ML, native.KERNEL_STD, np.concatenate([np.full(d, 0.5), [1.0]]),
-                     nu_fixed=0.0, want_grad=True)
-        out["not_pd"] = False
-    except native.NotPositiveDefinite:
-        out["not_pd"] = True
-    out["comm_ms"] = dc.times()["comm_ms"]
-    out["not_pd_all"] = group.all_gather(out["not_pd"])
-    dc.close()
+    if not one:
+        # a matrix that is not positive definite (a duplicated point, no nugget): every
+        # rank must report it, through the all-reduced failure flag
+        Xd = X.copy()
+        Xd[1] = Xd[0]
+        dc.set_data(Xd, f, H)
+        try:
+            dc.objective(native.GP4ML, native.KERNEL_STD, np.concatenate([np.full(d, 0.5), [1.0]]),
+                         nu_fixed=0.0, want_grad=True)
+            out["not_pd"] = False
+        except native.NotPositiveDefinite:
+            out["not_pd"] = True
+        out["comm_ms"] = dc.times()["comm_ms"]
+        out["not_pd_all"] = group.all_gather(out["not_pd"])
+        dc.close()
     group.barrier()
     if rank == 0:
         print("RESULT " + json.dumps(out), flush=True)

@@ -35,3 +35,10 @@ def test_bench_three_ranks_rowblock_over_rccl():
     assert rb["ranks"] == 3 and rb["n"] == 3000
     assert rb["parity_vs_single_gpu"]["ok"], rb["parity_vs_single_gpu"]
     assert len(rb["per_rank_device_gb"]) == 3
+    # the metric configuration's strong-scaling leg (here at the bench's --n / --d)
+    rm = line["extra"]["rowblock_metric"]
+    assert "error" not in rm and "skipped" not in rm, rm
+    assert rm["ranks"] == 3 and rm["n"] == 2048 and rm["d"] == 6
+    assert rm["parity_vs_single_gpu"]["ok"], rm["parity_vs_single_gpu"]
+    assert rm["llh_grad_ms"] > 0.0 and rm["comm_ms_llh_grad"] > 0.0
+    assert rm["speedup_vs_single_gpu"] > 0.0

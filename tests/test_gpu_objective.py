@@ -49,7 +49,10 @@ def _grad_ok(g, gref, tol=1e-7):
 @pytest.mark.parametrize("fname", ["objective_n200_d3.npz", "objective_n1024_d10.npz"])
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
 @pytest.mark.parametrize("point", [0, 1])
-def test_objective_golden(ctx, fname, case, point):
+@pytest.mark.parametrize("value_only", [False, True], ids=["grad", "value"])
+def test_objective_golden(ctx, fname, case, point, value_only):
+    """value_only: want_grad=0 runs the forward substitution with the Cholesky's
+    diagonal inverses instead of L^-1 (sigma_analytic_mucm, :382-408)."""
     z = np.load(os.path.join(GOLD, fname))
     tag, kind, variant, fitn, use_r = case
     X, f = z["X"], z["f"]
@@ -57,13 +60,17 @@ def test_objective_golden(ctx, fname, case, point):
     ctx.set_data(X, f, H, z["r"] if use_r else None)
     key = f"{tag}_p{point}"
     hp = z[key + "_hp"]
-    llh, grad, s2 = ctx.objective(variant, kind, hp, nu_fixed=float(z[key + "_nufixed"]))
+    llh, grad, s2 = ctx.objective(variant, kind, hp, nu_fixed=float(z[key + "_nufixed"]),
+                                  want_grad=not value_only)
     ref = float(z[key + "_llh"])
     rtol = max(1e-10, 4 * np.finfo(float).eps * _cond(X, hp, kind, variant, fitn,
                                                       float(z[key + "_nufixed"])))
     assert abs(llh - ref) <= rtol * max(1.0, abs(ref)), (llh, ref, rtol)
-    ok, err = _grad_ok(grad, z[key + "_grad"])
-    assert ok, (err, grad, z[key + "_grad"])
+    if value_only:
+        assert grad is None
+    else:
+        ok, err = _grad_ok(grad, z[key + "_grad"])
+        assert ok, (err, grad, z[key + "_grad"])
     assert abs(s2 - float(z[key + "_sig2"])) <= 1e-10 * abs(float(z[key + "_sig2"]))
 
 
@@ -76,13 +83,36 @@ def test_objective_not_pd(ctx, fname):
         ctx.objective(orc.GP4ML, orc.STD, z["nonpd_hp"], nu_fixed=0.0)
 
 
-def test_objective_value_only_matches(ctx):
-    X, f, H = orc.synthetic_problem(500, 4, seed=9)
+@pytest.mark.parametrize("n,d", [(500, 4), (129, 2), (1000, 20), (3000, 40)])
+def test_objective_value_only_matches(ctx, n, d):
+    """The value-only path (forward substitution, no L^-1) against the gradient path
+    (L^-1 [f H]) and the oracle: ragged n, and [f H] wider than one 16-column pass of
+    k_trsv_lower (d = 20: 22 columns, d = 40: 42)."""
+    X, f, H = orc.synthetic_problem(n, d, seed=9)
     ctx.set_data(X, f, H)
-    hp = np.array([0.5, 0.7, 0.9, 1.1, 1e-3, 1.3])
+    hp = np.concatenate([np.linspace(0.5, 1.1, d), [1e-3, 1.3]])
     a = ctx.objective(orc.GP4ML, orc.STD, hp, want_grad=True)
     b = ctx.objective(orc.GP4ML, orc.STD, hp, want_grad=False)
-    assert a[0] == b[0] and b[1] is None
+    assert b[1] is None
+    assert abs(a[0] - b[0]) <= 1e-12 * abs(a[0]), (a[0], b[0])
+    ref = orc.objective_fast(X, f, H, hp, orc.GP4ML, orc.STD, True)[0]
+    assert abs(b[0] - ref) <= 1e-10 * abs(ref), (b[0], ref)
+    m = ctx.objective(orc.MUCM, orc.STD, hp[:-1], want_grad=False)
+    mg = ctx.objective(orc.MUCM, orc.STD, hp[:-1], want_grad=True)
+    assert abs(m[0] - mg[0]) <= 1e-12 * abs(mg[0]) and abs(m[2] - mg[2]) <= 1e-12 * mg[2]
+
+
+def test_value_only_not_pd(ctx):
+    """A non-positive-definite matrix is reported by the value-only path too, and the
+    context stays usable (the substitution's workgroups stop on the abort flag)."""
+    z = np.load(os.path.join(GOLD, "objective_n1024_d10.npz"))
+    X, f = z["X"], z["f"]
+    ctx.set_data(X, f, orc.linear_basis(X))
+    with pytest.raises(native.NotPositiveDefinite):
+        ctx.objective(orc.GP4ML, orc.STD, z["nonpd_hp"], nu_fixed=0.0, want_grad=False)
+    key = "std_gp4ml_fitnug_p0"
+    llh = ctx.objective(orc.GP4ML, orc.STD, z[key + "_hp"], want_grad=False)[0]
+    assert abs(llh - float(z[key + "_llh"])) <= 1e-10 * abs(float(z[key + "_llh"]))
 
 
 def test_scale_point_4096(ctx):

@@ -24,14 +24,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKER = os.path.join(ROOT, "tests", "rccl_worker.py")
 
 
-def run_ranks(P, n, d, timeout=240):
+def run_ranks(P, n, d, timeout=240, extra=()):
     rdzv = tempfile.mkdtemp(prefix="gpemu-rccl-")
     procs = []
     for r in range(P):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(P), LOCAL_RANK="0", GPEMU_RDZV_DIR=rdzv,
                    NCCL_HOSTID=f"gpemu-test-rank-{r}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        procs.append(subprocess.Popen([sys.executable, WORKER, str(n), str(d)], env=env,
+        procs.append(subprocess.Popen([sys.executable, WORKER, str(n), str(d), *extra], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []
     try:
@@ -63,4 +63,22 @@ def test_rccl_multirank_matches_single_gpu(P, n, d):
         g, gref = np.array(c["grad"]), np.array(c["ref_grad"])
         assert np.max(np.abs(g - gref)) <= 1e-8 * np.max(np.abs(gref)), (name, g, gref)
     assert res["not_pd_all"] == [True] * P
+    assert res["comm_ms"] > 0.0
+
+
+@pytest.mark.timeout(600)
+def test_rccl_c4_fullsize_two_ranks():
+    """BASELINE configs[3] at full size (n = 65536, d = 20) over 2 real RCCL ranks on
+    the one GPU (socket transport: the timing is not xGMI's): value and gradient equal
+    the single-GPU objective, and each rank holds O(n^2 / P) of device memory."""
+    res = run_ranks(2, 65536, 20, timeout=560, extra=("one",))
+    c = res["cases"]["gp4ml_std"]
+    ref = c["ref_llh"]
+    assert abs(c["llh"] - ref) <= 1e-10 * abs(ref), (c["llh"], ref)
+    assert abs(c["llh_value_only"] - c["llh"]) <= 1e-12 * abs(ref)
+    g, gref = np.array(c["grad"]), np.array(c["ref_grad"])
+    assert np.max(np.abs(g - gref)) <= 1e-8 * np.max(np.abs(gref)), (g, gref)
+    # O(n^2 / P): 37.5 GB per rank at P = 2 (rows of L and of L^-1 + panels), against
+    # 2 x 34 GB for the single-GPU pair of n x n buffers
+    assert max(c["rank_gb"]) <= 40.0, c["rank_gb"]
     assert res["comm_ms"] > 0.0

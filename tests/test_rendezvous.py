@@ -68,6 +68,88 @@ def test_file_group(tmp_path, world):
     assert not os.path.exists(path)                # rank 0 removed the directory
 
 
+def _stale_worker(rank, world, path, q):
+    """A first attempt that dies after sharing its RCCL id: rank 1 exits without
+    close(), rank 0 too, so every file of that attempt stays behind."""
+    sys.path.insert(0, ROOT)
+    from gp_emu_uqsa_amd import rendezvous
+    g = rendezvous.FileGroup(rank, world, path, timeout=60)
+    g.barrier()
+    g.broadcast_bytes(b"\xee" * 128 if rank == 0 else None)
+    g.barrier()
+    g.all_gather("stale")
+    q.put(rank)
+
+
+def _run(target, world, path, extra=()):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=target, args=(r, world, path, q) + tuple(extra)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in range(world):
+        item = q.get(timeout=120)
+        res[item[0] if isinstance(item, tuple) else item] = item
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_group_over_leftover_directory(tmp_path, world):
+    """a restarted job (same directory name: same port / parent / run id)
+    must not read the files of the attempt before it: not its sequence files (the old
+    RCCL id, old barrier marks), not its session, not stale hellos."""
+    path = str(tmp_path / "rdzv")
+    _run(_stale_worker, world, path)
+    assert os.listdir(path)                      # the dead attempt's files are there
+    res = _run(_group_worker, world, path)
+    for r in range(world):
+        _, blob, gathered, mx, *_ = res[r]
+        assert blob == b"\x01" * 128               # not the stale id
+        assert gathered == [{"rank": k, "sq": k * k} for k in range(world)]
+        assert mx == 10.0
+
+
+def _abort_worker(rank, world, path, q, mode):
+    sys.path.insert(0, ROOT)
+    import time
+    from gp_emu_uqsa_amd import rendezvous
+    g = rendezvous.FileGroup(rank, world, path, timeout=60)
+    t0 = time.monotonic()
+    try:
+        g.barrier()   # the abort may already be visible here: any pending operation raises
+        if rank == world - 1:
+            if mode == "abort":
+                g.abort("set_data failed: out of memory")
+                raise rendezvous.RendezvousAborted("self")
+            g.all_gather("err")          # the others are in a barrier
+        else:
+            g.barrier()
+        q.put((rank, "none", time.monotonic() - t0))
+    except (rendezvous.RendezvousAborted, rendezvous.RendezvousMismatch) as e:
+        q.put((rank, f"{type(e).__name__}: {e}", time.monotonic() - t0))
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("mode", ["abort", "mismatch"])
+def test_group_fails_fast(tmp_path, mode):
+    """a rank that fails before a collective, or enters another one, makes
+    its peers raise at once with its message (not a hang until the timeout)."""
+    path = str(tmp_path / "rdzv")
+    res = _run(_abort_worker, 3, path, (mode,))
+    for r in range(2):
+        _, err, dt = res[r]
+        assert dt < 20.0
+        if mode == "abort":
+            assert err.startswith("RendezvousAborted") and "out of memory" in err and "rank 2" in err
+        else:
+            assert err.startswith("RendezvousMismatch") and "'ag'" in err
+
+
 def test_single_process_defaults():
     sys.path.insert(0, ROOT)
     from gp_emu_uqsa_amd import rendezvous, replicas

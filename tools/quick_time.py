@@ -19,3 +19,9 @@ ctx.set_profiling(True)
 ctx.objective(0, 0, hp)
 print("phases ms", ctx.phase_times())
 g = ctx.gemm_stats(); print("gemm", g, "TF/s", g['flops'] / g['ms'] / 1e9)
+ctx.set_profiling(False)
+ctx.objective(0, 0, hp, want_grad=False)
+tv = []
+for _ in range(3):
+    t = time.perf_counter(); rv = ctx.objective(0, 0, hp, want_grad=False); tv.append(time.perf_counter() - t)
+print("value-only s", tv, "llh", rv[0], "rel diff vs grad path", abs(rv[0] - r[0]) / abs(r[0]), flush=True)
