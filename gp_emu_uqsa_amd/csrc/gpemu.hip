@@ -1341,9 +1341,10 @@ int gpe_sense_pairs(gpe_ctx* c, int32_t J, const double* w, const double* u, int
   if (J <= 0 || J > 65535 || p <= 0 || !w || !u || !Z || !trace_out || !quad_out)
     return fail(c, GPE_ERR_ARG, "bad sense_pairs args");
   const int d = c->d;
-  if (d > 32) return fail(c, GPE_ERR_UNSUPPORTED, "sense_pairs supports d <= 32 input dimensions");
-  // Z columns in chunks of at most 32 (one launch each; PMAX = the chunk bucket + 2)
+  // Z columns in chunks of at most 32 (one launch each; PMAX = the chunk bucket + 2);
+  // d > 32: k_sense_pairs_wide (coordinates staged through LDS in chunks of 32)
   const int pchunk = std::min(p, 32);
+  const bool wide = d > 32;
   const long long np = c->n_pad, n = c->n;
   const int NB = c->NB;
   CHK(ensure_ainv(c));
@@ -1352,9 +1353,10 @@ int gpe_sense_pairs(gpe_ctx* c, int32_t J, const double* w, const double* u, int
   CHK(grow(c, &c->dSZ, &c->sz_cap, (size_t)np * p));
   CHK(grow(c, &c->dSW, &c->sw_cap, (size_t)J * d));
   // column slices: enough workgroups to fill the chip (>= 2048) when J is small
-  const int nct = (int)((n + SP_CT - 1) / SP_CT);
+  const int ct = wide ? SPW_CT : SP_CT;
+  const int nct = (int)((n + ct - 1) / ct);
   const int CS = std::max(1, std::min(nct, (2048 + NB * J - 1) / (NB * J)));
-  const int cslice = ((nct + CS - 1) / CS) * SP_CT;
+  const int cslice = ((nct + CS - 1) / CS) * ct;
   CHK(grow(c, &c->dSpart, &c->spart_cap, (size_t)NB * CS * 4 * ldp));
   CHK(grow(c, &c->dSout, &c->sout_cap, (size_t)ldp));
   CHK(ensure_pinned(c, std::max<size_t>({(size_t)J * np, (size_t)np * p, (size_t)J * d, (size_t)ldp}) + 64));
@@ -1377,11 +1379,19 @@ int gpe_sense_pairs(gpe_ctx* c, int32_t J, const double* w, const double* u, int
 #define SENSE_LAUNCH(DM, PM)                                                                              \
   hipLaunchKernelGGL((k_sense_pairs<DM, PM>), grid, dim3(256), 0, c->stream, c->tr.A, np, c->dX, d, c->dSW, \
                      c->dSU, np, c->dSZ, np, p, (int)n, cslice, c->dSpart, ldp, zc0, pc)
-    if (need_d <= 4) SENSE_LAUNCH(4, 6);
+#define SENSE_LAUNCH_WIDE(PM)                                                                               \
+  hipLaunchKernelGGL((k_sense_pairs_wide<PM>), grid, dim3(256), 0, c->stream, c->tr.A, np, c->dX, d, c->dSW, \
+                     c->dSU, np, c->dSZ, np, p, (int)n, cslice, c->dSpart, ldp, zc0, pc)
+    if (wide) {
+      if (pc <= 8) SENSE_LAUNCH_WIDE(8);
+      else if (pc <= 16) SENSE_LAUNCH_WIDE(16);
+      else SENSE_LAUNCH_WIDE(32);
+    } else if (need_d <= 4) SENSE_LAUNCH(4, 6);
     else if (need_d <= 8) SENSE_LAUNCH(8, 10);
     else if (need_d <= 16) SENSE_LAUNCH(16, 18);
     else SENSE_LAUNCH(32, 34);
 #undef SENSE_LAUNCH
+#undef SENSE_LAUNCH_WIDE
     HIPCHK(c, hipGetLastError());
   }
   hipLaunchKernelGGL(k_reduce_rows, dim3((unsigned)ldp), dim3(256), 0, c->stream, c->dSpart, NB * CS * 4,
@@ -1445,17 +1455,20 @@ int gpe_beta(gpe_ctx* c, double* beta_out) {
 }
 
 // Posterior mean and variance (gpe_posterior).  With keep_dev the full variance stays
-// on the device in c->dW3 (ld = m rounded up to TILE, identity padding) and var_out
-// is not written; rnew (m, device copy made here) adds s2 * rnew_scale * rnew to its
-// diagonal: Dnew's own r/s2 in Dnew.A (_emulatorclasses.py:572-575, :625).
+// on the device (ld = m rounded up to TILE, identity padding) and var_out is not
+// written: in c->dW3 for m <= 16384 (one chunk), else in dev_full, whose lower
+// triangle of blocks is formed chunk pair by chunk pair; rnew (m, device copy made
+// here) adds s2 * rnew_scale * rnew to its diagonal: Dnew's own r/s2 in Dnew.A
+// (_emulatorclasses.py:572-575, :625).
 static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double* Hs, const double* beta,
                           double sigma, int32_t full_var, int32_t precision, double* mean_out, double* var_out,
-                          const double* rnew, double rnew_scale, bool keep_dev) {
+                          const double* rnew, double rnew_scale, bool keep_dev, double* dev_full = nullptr) {
   CHK(check_ready(c));
   if (!c->factor_valid) return fail(c, GPE_ERR_STATE, "no resident factor (call gpe_factor)");
   if (m <= 0 || !Xs || !Hs || !beta || !mean_out || (!var_out && !keep_dev))
     return fail(c, GPE_ERR_ARG, "bad posterior args");
-  if (keep_dev && (!full_var || m > 16384)) return fail(c, GPE_ERR_ARG, "device-resident variance: full, m <= 16384");
+  if (keep_dev && (!full_var || (m > 16384 && !dev_full)))
+    return fail(c, GPE_ERR_ARG, "device-resident variance: full, and beyond one chunk a device target");
   if (precision != 64 && precision != 32) return fail(c, GPE_ERR_ARG, "precision must be 64 or 32");
   if (precision == 32 && full_var) return fail(c, GPE_ERR_UNSUPPORTED, "precision 32 is for the diagonal variance");
   CHK(ensure_linv(c));
@@ -1715,7 +1728,7 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
     HIPCHK(c, hipMemcpyAsync(c->dTall, Th.data(), Th.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const size_t needc = (size_t)CHUNK * CHUNK;
-    if (needc > c->w3_cap) {
+    if (!keep_dev && needc > c->w3_cap) {
       CHK(dalloc(c, &c->dW3, needc));
       c->w3_cap = needc;
     }
@@ -1728,6 +1741,38 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
         const long long mcb = std::min(CHUNK, m - b0), mpb = ((mcb + TILE - 1) / TILE) * TILE;
         const int mtb = (int)(mpb / TILE);
         const bool dg = a0 == b0;
+        if (keep_dev) {
+          // block (b, a) of the lower triangle straight into dev_full (ld = mtot): rows of
+          // chunk b, columns of chunk a.  Padded rows / columns come out 0 off the
+          // diagonal (zero K*, V and T there) and identity on it (the pair kernel).
+          double* dst = dev_full + b0 + a0 * mtot;
+          PairArgs a;
+          a.xr = c->dXall + b0 * d; a.xc = c->dXall + a0 * d; a.out = dst; a.ld = mtot; a.d = d;
+          a.nr_valid = (int)mcb; a.nc_valid = (int)mca; a.mt = mtb; a.nt = mta; a.mode = dg ? (1 | 2 | 4) : 0;
+          a.s2 = s2; a.coff = coff; a.cdiag = cdiag; a.rscale = 0.0; a.r = nullptr;
+          if (dg && rnew) {
+            CHK(grow(c, &c->dRn, &c->rn_cap, (size_t)mpa));
+            HIPCHK(c, hipMemsetAsync(c->dRn, 0, (size_t)mpa * sizeof(double), c->stream));
+            HIPCHK(c, hipMemcpy(c->dRn, rnew + a0, (size_t)mca * sizeof(double), hipMemcpyHostToDevice));
+            a.r = c->dRn;
+            a.rscale = s2 * rnew_scale;
+          }
+          CHK(launch_pairs(c, a, dg ? mta * (mta + 1) / 2 : mta * mtb));
+          std::vector<GemmProb> p2 = {
+              mkprob(c->dVall + b0 * np, np, c->dVall + a0 * np, np, dst, mtot, mtb, mta, (int)np, 0, -s2, 1.0),
+              mkprob(c->dTall + b0, mtot, c->dTall + a0, mtot, dst, mtot, mtb, mta, kq, 0, s2, 1.0)};
+          p2[0].tile_begin = 0; p2[0].ntiles = mta * mtb;
+          p2[1].tile_begin = 0; p2[1].ntiles = mta * mtb;
+          HIPCHK(c, hipMemcpyAsync(c->dprobs + ADHOC_DESC_BASE + 1, p2.data(), 2 * sizeof(GemmProb),
+                                   hipMemcpyHostToDevice, c->stream));
+          Launch L1{2, ADHOC_DESC_BASE + 1, 1, mta * mtb, 0.0};
+          CHK(launch_gemm_range(c, L1));
+          Launch L2{0, ADHOC_DESC_BASE + 2, 1, mta * mtb, 0.0};
+          CHK(launch_gemm_range(c, L2));
+          // the descriptors are re-uploaded for the next block: drain before overwriting
+          HIPCHK(c, hipStreamSynchronize(c->stream));
+          continue;
+        }
         PairArgs a;   // A** block: the diagonal block as the single-chunk path, else rectangular
         a.xr = c->dXall + a0 * d; a.xc = c->dXall + b0 * d; a.out = dC; a.ld = mpa; a.d = d;
         a.nr_valid = (int)mca; a.nc_valid = (int)mcb; a.mt = mta; a.nt = mtb; a.mode = dg ? (1 | 2 | 4) : 0;
@@ -1776,19 +1821,24 @@ int gpe_noise_sample(gpe_ctx* c, int64_t m, const double* Xs, const double* Hs, 
                      double sigma, const double* r_new, double r_scale, const double* t, int32_t s,
                      const double* U, double* mean_out, double* z_out) {
   CHK(check_ready(c));
-  if (m <= 0 || m > 16384 || s <= 0 || !t || !U || !z_out)
-    return fail(c, GPE_ERR_ARG, "bad noise_sample args (1 <= m <= 16384, s >= 1)");
-  // V = posterior covariance at Xs, left in c->dW3 (mp x mp, identity padding)
-  CHK(posterior_impl(c, m, Xs, Hs, beta, sigma, 1, 64, mean_out, nullptr, r_new, r_scale, true));
+  if (m <= 0 || m > (1LL << 20) || s <= 0 || !t || !U || !z_out)
+    return fail(c, GPE_ERR_ARG, "bad noise_sample args (1 <= m <= 2^20, s >= 1)");
   const long long mp = ((m + TILE - 1) / TILE) * TILE;
   const int mt = (int)(mp / TILE);
   const long long sp = ((s + TILE - 1) / TILE) * TILE;
   const int st = (int)(sp / TILE);
-  // L = chol(V) in the aux workspace (np.linalg.cholesky(post.var), noise_fit.py:131)
+  // V = posterior covariance at Xs (mp x mp, identity padding) into the aux workspace,
+  // then L = chol(V) there (np.linalg.cholesky(post.var), noise_fit.py:131).  One chunk
+  // (m <= 16384): formed in c->dW3 and copied; beyond, formed block by block in place.
   Fact& F = c->aux;
   CHK(ensure_fact(c, F, mp));
   CHK(build_plan(c, F));
-  HIPCHK(c, hipMemcpyAsync(F.A, c->dW3, (size_t)mp * mp * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+  if (m <= 16384) {
+    CHK(posterior_impl(c, m, Xs, Hs, beta, sigma, 1, 64, mean_out, nullptr, r_new, r_scale, true));
+    HIPCHK(c, hipMemcpyAsync(F.A, c->dW3, (size_t)mp * mp * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+  } else {
+    CHK(posterior_impl(c, m, Xs, Hs, beta, sigma, 1, 64, mean_out, nullptr, r_new, r_scale, true, F.A));
+  }
   HIPCHK(c, hipMemsetAsync(c->dinfo, 0, sizeof(int), c->stream));
   CHK(potrf(c, F));
   int info = 0;

@@ -2312,6 +2312,96 @@ static __global__ void __launch_bounds__(256) k_sense_pairs(const double* Ainv, 
   }
 }
 
+// k_sense_pairs for any d (> 32): the slice's columns are staged SPW_CT at a time and
+// their coordinates SPW_DC dimensions at a time (LDS), each thread keeping the running
+// squared distances of its SPW_CT / 2 columns; the distances accumulate dimension by
+// dimension in the same fma order as k_sense_pairs, so the pair values are the same.
+constexpr int SPW_CT = 32, SPW_DC = 32;
+template <int PMAX>
+static __global__ void __launch_bounds__(256) k_sense_pairs_wide(const double* Ainv, long long lda, const double* x,
+                                                                int d, const double* w, const double* u,
+                                                                long long ldu, const double* Z, long long ldz,
+                                                                int p, int n_valid, int cslice, double* part,
+                                                                long long ldp, int zc0, int pc) {
+  __shared__ double xs[SPW_CT * SPW_DC];
+  __shared__ double wsh[SPW_DC];
+  __shared__ double zs[SPW_CT * PMAX];
+  __shared__ double us[SPW_CT];
+  constexpr int CM = SPW_CT / 2;   // columns per thread per stage
+  const int ti = blockIdx.x, j = blockIdx.y, tid = threadIdx.x;
+  const int r = tid & (TILE - 1), h = tid >> 7;
+  const int gi = ti * TILE + r;
+  const bool rv = gi < n_valid;
+  double v[PMAX];
+#pragma unroll
+  for (int q = 0; q < PMAX; ++q) v[q] = 0.0;
+  const double ui = rv ? u[j * ldu + gi] : 0.0;
+  double acc = 0.0;
+  const int cbeg = blockIdx.z * cslice, cfin = min(n_valid, cbeg + cslice);
+  for (int c0 = cbeg; c0 < cfin; c0 += SPW_CT) {
+    double sd[CM];
+#pragma unroll
+    for (int m = 0; m < CM; ++m) sd[m] = 0.0;
+    for (int k0 = 0; k0 < d; k0 += SPW_DC) {
+      __syncthreads();
+      for (int e = tid; e < SPW_CT * SPW_DC; e += 256) {
+        const int c = e / SPW_DC, k = e - c * SPW_DC, g = c0 + c;
+        xs[e] = (k0 + k < d && g < n_valid) ? x[(long long)g * d + k0 + k] : 0.0;
+      }
+      if (tid < SPW_DC) wsh[tid] = (k0 + tid < d) ? w[j * d + k0 + tid] : 0.0;
+      __syncthreads();
+      double xi[SPW_DC];
+#pragma unroll
+      for (int k = 0; k < SPW_DC; ++k) xi[k] = (k0 + k < d && rv) ? x[(long long)gi * d + k0 + k] : 0.0;
+#pragma unroll
+      for (int m = 0; m < CM; ++m) {
+        const int c = h + 2 * m;
+#pragma unroll
+        for (int k = 0; k < SPW_DC; ++k) {
+          const double df = xi[k] - xs[c * SPW_DC + k];
+          sd[m] = fma(wsh[k] * df, df, sd[m]);
+        }
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < SPW_CT * PMAX; e += 256) {   // Z columns zc0 .. zc0 + pc
+      const int c = e % SPW_CT, k = e / SPW_CT, g = c0 + c;
+      zs[c * PMAX + k] = (k < pc && g < n_valid) ? Z[g + (long long)(zc0 + k) * ldz] : 0.0;
+    }
+    if (tid < SPW_CT) us[tid] = (c0 + tid < n_valid) ? u[j * ldu + c0 + tid] : 0.0;
+    __syncthreads();
+    if (rv) {
+#pragma unroll
+      for (int m = 0; m < CM; ++m) {
+        const int c = h + 2 * m, gj = c0 + c;
+        if (gj < cfin) {
+          const double K = ui * us[c] * exp(-sd[m]);
+#pragma unroll
+          for (int q = 0; q < PMAX; ++q) v[q] = fma(K, zs[c * PMAX + q], v[q]);
+          const double av = gj <= gi ? Ainv[gi + (long long)gj * lda] : 0.0;
+          acc = fma(gj < gi ? 2.0 * K : (gj == gi ? K : 0.0), av, acc);
+        }
+      }
+    }
+  }
+  const int lane = tid & 63, wave = tid >> 6;
+  double* out = part + (long long)((ti * gridDim.z + blockIdx.z) * 4 + wave) * ldp + (long long)j * (1 + p * p);
+  double t = acc;
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
+  if (lane == 0) out[0] = t;
+  for (int a = 0; a < p; ++a) {
+    const double za = rv ? Z[gi + (long long)a * ldz] : 0.0;
+#pragma unroll
+    for (int b = 0; b < PMAX; ++b) {
+      if (b < pc) {
+        double s = za * v[b];
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+        if (lane == 0) out[1 + a * p + zc0 + b] = s;
+      }
+    }
+  }
+}
+
 // Gauss transform over the training inputs (main / interaction effects,
 // _sensitivityclasses.py:628-633 Tw summed against e):
 //   out[t] = sum_k a[k] exp(-sum_s c[s] (Y[t,s] - x[k, dims[s]])^2),  one wave per t

@@ -2,18 +2,24 @@
 
 Format (README.md:158-314 of the reference): one ``key value`` per line, split
 at the first space; unknown keys are ignored.  Bounds and ``input_minmax`` are
-Python list literals -- parsed here with ``ast.literal_eval`` instead of
-``eval`` (the reference evals them, _emulatorclasses.py:76-78, :95, :211), after
-unwrapping the ``np.float64(x)`` spellings that NumPy 2 makes the reference
-write into updated beliefs files.
-Error behaviour follows the reference: a message, then ``SystemExit``.
+Python list expressions.  The reference ``eval``s them in a module that imported
+numpy as np (_emulatorclasses.py:76-78, :95, :211), so a file may hold arithmetic
+(``[[0.1, 2*0.5]]``), numpy constants (``np.pi``) and the ``np.float64(x)``
+spellings that NumPy 2 makes the reference write into updated beliefs files
+(SURVEY.md Appendix A).  Here they go through ``literal``: a restricted evaluator
+of the expression tree that computes exactly those forms -- numbers, lists /
+tuples, + - * / // % **, unary +/-, np.pi / np.e / np.inf / np.nan, and the numpy
+scalar constructors and elementary functions (float64, sqrt, exp, log, ...) -- and
+refuses anything else (names, attributes, other calls) with a ValueError instead
+of executing it.  That refusal is the one deliberate difference from ``eval``.
+Error behaviour otherwise follows the reference: a message, then ``SystemExit``.
 """
 from __future__ import annotations
 
 import ast
-import re
+import math
+import operator
 
-_NP_SCALAR = re.compile(r"(?:np|numpy|_np)\.(?:float64|float32|int64|int32|float_|int_)\(([^()]*)\)")
 
 CONFIG_REQUIRED = ("beliefs", "inputs", "outputs", "tv_config", "delta_bounds", "nugget_bounds",
                    "sigma_bounds", "tries", "constraints")
@@ -26,10 +32,48 @@ def _die(msg):
     raise SystemExit(1)
 
 
+_BINOPS = {ast.Add: operator.add, ast.Sub: operator.sub, ast.Mult: operator.mul, ast.Div: operator.truediv,
+           ast.FloorDiv: operator.floordiv, ast.Mod: operator.mod, ast.Pow: operator.pow}
+_UNOPS = {ast.USub: operator.neg, ast.UAdd: operator.pos}
+_NP_CONST = {"pi": math.pi, "e": math.e, "inf": math.inf, "nan": math.nan}
+_NP_FUNCS = {"float64": float, "float32": float, "float_": float, "int64": int, "int32": int, "int_": int,
+             "sqrt": math.sqrt, "exp": math.exp, "log": math.log, "log10": math.log10, "abs": abs,
+             "fabs": math.fabs}
+_NP_NAMES = ("np", "numpy", "_np")
+
+
+def _np_member(node, table):
+    if (isinstance(node, ast.Attribute) and isinstance(node.value, ast.Name)
+            and node.value.id in _NP_NAMES and node.attr in table):
+        return table[node.attr]
+    raise ValueError(f"unsupported expression in a list value: {ast.dump(node)}")
+
+
+def _evaluate(node):
+    if isinstance(node, ast.Expression):
+        return _evaluate(node.body)
+    if isinstance(node, ast.Constant) and isinstance(node.value, (int, float)) and not isinstance(node.value, bool):
+        return node.value
+    if isinstance(node, ast.List):
+        return [_evaluate(e) for e in node.elts]
+    if isinstance(node, ast.Tuple):
+        return tuple(_evaluate(e) for e in node.elts)
+    if isinstance(node, ast.BinOp) and type(node.op) in _BINOPS:
+        return _BINOPS[type(node.op)](_evaluate(node.left), _evaluate(node.right))
+    if isinstance(node, ast.UnaryOp) and type(node.op) in _UNOPS:
+        return _UNOPS[type(node.op)](_evaluate(node.operand))
+    if isinstance(node, ast.Attribute):
+        return _np_member(node, _NP_CONST)
+    if isinstance(node, ast.Call) and not node.keywords:
+        fn = _np_member(node.func, _NP_FUNCS)
+        return fn(*[_evaluate(a) for a in node.args])
+    raise ValueError(f"unsupported expression in a list value: {ast.dump(node)}")
+
+
 def literal(text: str):
-    """Safe replacement for the reference's eval() of list literals."""
-    text = _NP_SCALAR.sub(r"\1", text.strip())
-    return ast.literal_eval(text)
+    """The reference's eval() of a list value (_emulatorclasses.py:76-78, :211),
+    restricted to numbers and arithmetic (see the module docstring)."""
+    return _evaluate(ast.parse(text.strip(), mode="eval"))
 
 
 def read_key_values(path: str, missing_value_exits: bool) -> dict:

@@ -86,7 +86,9 @@ int gpe_set_data(gpe_ctx* ctx, int64_t n, int32_t d, int32_t q,
  * Outputs: *llh_out = the reference's LLH (negative log marginal likelihood);
  * grad_out (n_hp, may be NULL when want_grad == 0) = its gradient w.r.t.
  * x = 2 log(hp), including the MUCM sigma-hat^2 scaling the reference applies;
- * *sigma2_out = sigma^2 (gp4ml) or the analytic sigma-hat^2 (mucm, :324-327). */
+ * *sigma2_out = sigma^2 (gp4ml) or the analytic sigma-hat^2 (mucm, :324-327).
+ * want_grad == 0 (sigma_analytic_mucm, :382-408) runs K-build, Cholesky and a forward
+ * substitution for L^-1 [f H] only: no triangular inverse and no A^-1. */
 int gpe_objective(gpe_ctx* ctx, int32_t variant, int32_t kernel,
                   const double* hp, int32_t n_hp, double nu_fixed, int32_t want_grad,
                   double* llh_out, double* grad_out, double* sigma2_out);
@@ -99,7 +101,9 @@ int gpe_objective(gpe_ctx* ctx, int32_t variant, int32_t kernel,
 int gpe_factor(gpe_ctx* ctx, int32_t kernel, const double* delta, double nu,
                double s2, double r_scale);
 
-/* GLS beta = Q^-1 H^T A^-1 f with the resident factor (optimalbeta, :497-504). */
+/* GLS beta = Q^-1 H^T A^-1 f with the resident factor (optimalbeta, :497-504).  Needs
+ * only L: L^-1 [f H] by forward substitution with the Cholesky's diagonal-tile inverses
+ * (no n^3/3 triangular inverse; that runs on demand for the posterior-side entries). */
 int gpe_beta(gpe_ctx* ctx, double* beta_out);
 
 /* Posterior at m points: replaces Posterior.make_covar/make_mean/make_var
@@ -125,7 +129,9 @@ int gpe_solve(gpe_ctx* ctx, int32_t ncols, const double* B, double* X);
 
 /* J Gaussian pair kernels K_j(k,l) = u[j,k] u[j,l] exp(-sum_i w[j,i] (x_ki - x_li)^2)
  * (w: J x d, u: J x n).  trace_out[j] = sum_kl (A^-1)_kl K_j(k,l) = tr(A^-1 K_j);
- * quad_out[j] = Z^T K_j Z (p x p; Z: n x p, p <= 34, d <= 32). */
+ * quad_out[j] = Z^T K_j Z (p x p; Z: n x p).  Any p (Z columns in chunks of 32, one
+ * launch each) and any d the context holds (d > 32: coordinates staged through LDS in
+ * chunks of 32 dimensions), as the reference's Pw / Rtt loops (:90-102, :599-626). */
 int gpe_sense_pairs(gpe_ctx* ctx, int32_t J, const double* w, const double* u, int32_t p,
                     const double* Z, double* trace_out, double* quad_out);
 
@@ -197,7 +203,10 @@ int gpe_bench_gemm(gpe_ctx* ctx, int32_t trans_a, int32_t trans_b, int32_t mt, i
  * and for the s draws u_j = U[j, :] (U row-major s x m: the reference's successive
  * np.random.randn(m) calls) z_out[i] = sum_j 0.5 (t_i - mean_i - (L u_j)_i)^2
  * (the caller divides by s and applies the log transform).  mean_out (m) is the
- * posterior mean.  Needs the resident factor of gpe_factor.  m <= 16384.
+ * posterior mean.  Needs the resident factor of gpe_factor.  Any m up to 2^20 (the
+ * reference has no bound): m <= 16384 forms V in one chunk, beyond it V is formed
+ * chunk pair by chunk pair straight into the factorisation workspace (V and its
+ * factor take 2 x m_pad^2 x 8 bytes of HBM: 2 x 8.6 GB at m = 32768).
  * GPE_NOT_PD when V is not positive definite (np.linalg.cholesky's LinAlgError). */
 int gpe_noise_sample(gpe_ctx* ctx, int64_t m, const double* Xs, const double* Hs,
                      const double* beta, double sigma, const double* r_new, double r_scale,

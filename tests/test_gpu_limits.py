@@ -7,10 +7,14 @@ m x m posterior covariance for any m, :618-631):
   objective (gp4ml / MUCM / alt-nugget with r), kernel pieces and posterior against the
   oracle; the row-block distributed objective on 2 loopback ranks;
 - d = 3 with a 40-column polynomial basis (many basis columns, few inputs);
-- sensitivity pair sums with p = 45 columns of Z (chunks of 32);
+- sensitivity pair sums with p = 45 columns of Z (chunks of 32), and at d = 40 inputs
+  (coordinates staged through LDS: k_sense_pairs_wide);
 - the full posterior covariance at m = 16384 + 300 points (two chunks: its off-diagonal
   blocks are formed on the device and written to the host), against the oracle on
-  points drawn from both chunks.
+  points drawn from both chunks;
+- noise_fit's estimation step (gpe_noise_sample) at m = 16384 + 500 points: the
+  covariance is formed block by block in the factorisation workspace, factored and
+  drawn from on the device (noise_fit.py:130-150 has no bound on m).
 Tolerances as the small-d tests: LLH 1e-9 relative, gradient 1e-7 of (|g| + max|g|),
 posterior 1e-8 absolute."""
 import numpy as np
@@ -155,3 +159,50 @@ def test_full_covariance_beyond_one_chunk(ctx):
     assert np.max(np.abs(var[np.ix_(sel, sel)] - vref)) < 1e-8
     _, vdiag = ctx.posterior(xs, hs, beta, sigma, full_var=False)
     assert np.max(np.abs(np.diag(var) - vdiag)) < 1e-10
+
+
+@pytest.mark.parametrize("p", [5, 12, 37])
+def test_sense_pairs_d40(ctx, p):
+    """gpe_sense_pairs beyond 32 input dimensions (sensitivity/_sensitivityclasses.py
+    :599-626 takes any d): d = 40, Z widths in each column bucket and over a chunk."""
+    rs = np.random.RandomState(11)
+    n, d = 300, 40
+    X = rs.uniform(size=(n, d))
+    f = np.cos(3 * X[:, 0]) + X[:, 1]
+    ctx.set_data(X, f, orc.linear_basis(X))
+    delta, nu = np.linspace(2.0, 4.0, d), 1e-2
+    ctx.factor(native.KERNEL_STD, delta, nu)
+    Ainv = np.linalg.inv(orc.kernel_var_ref(X, delta, nu, orc.STD)[0])
+    W = rs.uniform(0.0, 0.2, size=(3, d))
+    U = rs.uniform(0.5, 1.5, size=(3, n))
+    Z = rs.normal(size=(n, p))
+    tr, quad = ctx.sense_pairs(W, U, Z)
+    for j in range(3):
+        D = ((X[:, None, :] - X[None, :, :]) ** 2 * W[j]).sum(-1)
+        K = U[j][:, None] * U[j][None, :] * np.exp(-D)
+        assert abs(tr[j] - np.sum(Ainv * K)) <= 1e-9 * np.sum(np.abs(Ainv * K))
+        np.testing.assert_allclose(quad[j], Z.T @ K @ Z, rtol=0, atol=1e-11 * np.abs(Z).sum(0).max() ** 2 * 2.25)
+
+
+def test_noise_sample_beyond_one_chunk(ctx):
+    from oracle import noise_oracle as nor
+    rs = np.random.RandomState(12)
+    n, m, s = 300, 16384 + 500, 6
+    x = rs.uniform(size=(n, 2))
+    f = np.cos(3 * x[:, 0]) + x[:, 1] ** 2 + 0.1 * rs.randn(n)
+    r = 0.01 + 0.05 * x[:, 1]
+    delta, nu, sig, beta = np.array([0.3, 0.4]), 1e-3, 0.8, np.array([0.2])
+    ctx.set_data(x, f, np.ones((n, 1)), r)
+    ctx.factor(native.KERNEL_ALT_NUG, delta, nu, 1.0, 1.0)
+    xs = rs.uniform(size=(m, 2))
+    rn = 0.01 + 0.05 * xs[:, 1]
+    t = rs.randn(m)
+    U = rs.randn(s, m)
+    mean, zsum = ctx.noise_sample(xs, np.ones((m, 1)), beta, sig, t, U, r_new=rn, r_scale=1.0 / sig ** 2)
+    A, _ = orc.kernel_var_ref(x, delta, nu, orc.ALT, True)
+    A[np.diag_indices(n)] += r
+    mref, vref = nor.posterior_ref(x, f, np.ones((n, 1)), A, xs, np.ones((m, 1)), beta, sig, delta, nu,
+                                   orc.ALT, rs_new=rn / sig ** 2)
+    assert np.max(np.abs(mean - mref)) <= 1e-10 * (np.max(np.abs(mref)) + 1.0)
+    zref = np.exp(nor.noise_estimate_ref(mref, vref, t, U)) * s
+    assert np.max(np.abs(zsum - zref) / zref) <= 1e-8, np.max(np.abs(zsum - zref) / zref)

@@ -37,6 +37,30 @@ def test_reconstruct_beliefs_minmax(tmp_path, monkeypatch):
     assert b.fix_nugget == "F"
 
 
+@pytest.mark.parametrize("text", ["[[0.1, 2*0.5]]", "[[1e-3, 1.0/3], [0.5, 2**-1 + 0.25]]",
+                                  "[ [np.float64(0.1), np.pi/2] ]", "[[-1+0.5, np.sqrt(4.0)]]", "[ ]"])
+def test_config_list_arithmetic_as_eval(tmp_path, monkeypatch, text):
+    """Deliberate deviation, documented in files.py: the reference eval()s bound lists
+    with numpy as np in scope (_emulatorclasses.py:76-78), so arithmetic in a config
+    file works there; the restricted evaluator gives exactly eval's values for such
+    files without executing anything else."""
+    monkeypatch.chdir(tmp_path)
+    (tmp_path / "cfg").write_text(f"beliefs b\ninputs i\noutputs o\ntv_config 10 0 2\ndelta_bounds {text}\n"
+                                  "nugget_bounds [ ]\nsigma_bounds [[0.01, 3*1.5]]\ntries 1\nconstraints bounds\n")
+    c = files.Config("cfg")
+    assert c.delta_bounds == eval(text, {"np": np})   # noqa: S307 -- the reference's semantics, test input
+    assert c.sigma_bounds == [[0.01, 4.5]]
+
+
+@pytest.mark.parametrize("text", ["[__import__('os').getcwd()]", "[open('x')]", "[x for x in range(3)]",
+                                  "[np.load('f')]", "['a', 1]"])
+def test_config_list_refuses_code(text):
+    """What eval() would execute (calls, names, comprehensions, strings) is refused with
+    a ValueError naming the expression, instead of being run."""
+    with pytest.raises(ValueError, match="unsupported expression"):
+        files.literal(text)
+
+
 def test_missing_key_exits(tmp_path, monkeypatch):
     monkeypatch.chdir(tmp_path)
     (tmp_path / "cfg").write_text("beliefs b\ninputs i\n")
