@@ -52,6 +52,7 @@ struct Plan {
   std::vector<int> fused;
   std::vector<int> trtri;   // launches in order
   int lauum = -1;
+  bool aug = false;         // the fused launches carry the augmented row
   std::vector<Launch> launches;
   std::vector<GemmProb> probs;
   std::vector<unsigned> tiles;   // concatenated tile lists
@@ -66,7 +67,12 @@ struct Fact {
   size_t cap = 0;
   double* logdet = nullptr;  // NB per-block log-determinant parts
   int* flags = nullptr;      // NB diagonal-inverse ready flags (fused Cholesky)
-  int* tflags = nullptr;     // NB tile-row flags of the forward substitution (k_trsv_lower)
+  int* tflags = nullptr;     // row counter of the forward substitution (k_trsv_lower)
+  // augmented tile row ([f H]^T under the matrix, TILE x n_pad, ld TILE): carried by the
+  // fused Cholesky's panels and trailing updates, it ends as (L^-1 [f H])^T (training
+  // workspace only)
+  bool aug = false;
+  double* Faug = nullptr;
   int desc_base = 0;         // first slot of its descriptors in the device array
   Plan plan;
 };
@@ -431,6 +437,10 @@ int build_plan(gpe_ctx* c, Fact& F) {
   double* A = F.A;
   double* B = F.B;
   auto tile = [&](double* M, int i, int j) { return M + (long long)i * TILE + (long long)j * TILE * ld; };
+  // tile (0, j) of the augmented row (ld TILE)
+  const bool aug = F.aug && F.Faug && !c->potrf_lookahead;
+  pl.aug = aug;
+  auto atile = [&](int j) { return F.Faug + (long long)j * TILE * TILE; };
   // --- Cholesky (right-looking, 128-column steps)
   pl.panel.assign(NB, -1);
   pl.colupd.assign(NB, -1);
@@ -463,7 +473,8 @@ int build_plan(gpe_ctx* c, Fact& F) {
     p.diag_col0 = t * TILE;   // step index for the GEMM_TRACE dev build
     return p;
   };
-  // bulk problems: tiles (i, j), i >= j, j in [a, b), updated by columns [g0, g0 + K/128)
+  // bulk problems: tiles (i, j), i >= j, j in [a, b), updated by columns [g0, g0 + K/128);
+  // with the augmented row also its tiles (aug, j) (not counted as algorithmic flops)
   auto bulk = [&](std::vector<GemmProb>& fp, double& fl, int a, int b, int g0, int K) {
     if (a >= b) return;
     fp.push_back(mkprob(tile(A, a, g0), ld, tile(A, a, g0), ld, tile(A, a, a), ld, b - a, b - a, K,
@@ -474,6 +485,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
                           -1.0, 1.0));
       fl += 2.0 * (NB - b) * T * (double)(b - a) * T * K;
     }
+    if (aug) fp.push_back(mkprob(atile(g0), TILE, tile(A, a, g0), ld, atile(a), TILE, 1, b - a, K, 0, -1.0, 1.0));
   };
   std::vector<int> gs;   // group starts, then NB
   for (int g = 0; g < NB;) {
@@ -516,6 +528,15 @@ int build_plan(gpe_ctx* c, Fact& F) {
       if (m >= 1) {
         fp.push_back(panelprob(t, K ? tile(A, t + 1, p0) : nullptr, K ? tile(A, t, p0) : nullptr, K, al));
         fl += 2.0 * m * T * T * K + (double)m * T * T * T;
+      }
+      if (aug) {   // the augmented row's panel tile (aug, t): pending columns, then x X_t^T
+        GemmProb pa = mkprob(K ? atile(p0) : nullptr, TILE, K ? tile(A, t, p0) : nullptr, ld, atile(t), TILE,
+                             1, 1, K, G_PANEL, al, 1.0);
+        pa.X = tile(B, t, t);
+        pa.ldx = ld;
+        pa.flag = F.flags + t;
+        pa.diag_col0 = -TILE;   // (no GEMM_TRACE slot)
+        fp.push_back(pa);
       }
       if (gi > 0) {
         const int g0 = gs[gi - 1], Kb = (gb - g0) * TILE;
@@ -624,6 +645,7 @@ int ensure_fact(gpe_ctx* c, Fact& F, long long n_pad) {
     CHK(dalloc(c, &F.logdet, (size_t)F.NB));
     CHK(dalloc(c, &F.flags, (size_t)F.NB));
     CHK(dalloc(c, &F.tflags, (size_t)F.NB));
+    if (F.aug) CHK(dalloc(c, &F.Faug, (size_t)n_pad * TILE));
     F.plan = Plan();
   }
   return GPE_OK;
@@ -675,7 +697,11 @@ int kbuild(gpe_ctx* c, int kernel, double nu, double s2, double rscale) {
 //   aux  : wait rest(k-2) | diag(k) | panel(k) | rec ev_panel[k] | wait rest(k-1) | colupd(k)
 //   main : wait ev_panel[k] | rest(k) | rec ev_rest[k]
 // diag/panel/colupd of the next step run while the big trailing update runs.
+// Every launcher of a workspace's schedule first makes sure it is built: growing the
+// tile-list array for one workspace's plan resets the other's (build_plan), e.g. the
+// aux plan of gpe_noise_sample between gpe_factor and a later on-demand TRTRI / LAUUM.
 int potrf(gpe_ctx* c, Fact& F) {
+  CHK(build_plan(c, F));
   const Plan& pl = F.plan;
   const int NB = F.NB;
   if (!c->potrf_lookahead) {
@@ -724,7 +750,14 @@ int potrf(gpe_ctx* c, Fact& F) {
   return GPE_OK;
 }
 
+// A^-1 = X^T X over L (the plan's LAUUM launch)
+int lauum(gpe_ctx* c, Fact& F) {
+  CHK(build_plan(c, F));
+  return launch_gemm_range(c, F.plan.launches[F.plan.lauum]);
+}
+
 int trtri(gpe_ctx* c, Fact& F) {
+  CHK(build_plan(c, F));
   for (int li : F.plan.trtri) CHK(launch_gemm_range(c, F.plan.launches[li]));
   return GPE_OK;
 }
@@ -859,6 +892,9 @@ void ev_rec(gpe_ctx* c, int i) {
   if (c->prof) hipEventRecord(c->ev[i], c->stream);
 }
 
+int z_from_factor(gpe_ctx* c);
+int trsv_lower(gpe_ctx* c, Fact& F, const double* R, long long ldr, int P, double* Y, long long ldy);
+
 // K-build and Cholesky of the training matrix; with invert, also X = L^-1 (TRTRI) into
 // tr.B.  Without it tr.B keeps only the diagonal-tile inverses, which is all the forward
 // substitution (trsv_lower) needs: the value-only objective and gpe_beta skip the n^3/3
@@ -871,8 +907,16 @@ int factor_and_invert(gpe_ctx* c, int kernel, const double* delta, double nu, do
   ev_rec(c, 0);
   CHK(scale_training(c, delta));
   CHK(kbuild(c, kernel, nu, s2, rscale));
+  const int P = c->q + 1;
+  if (c->tr.plan.aug) {   // [f H]^T into the augmented row (the sweep turns it into Z^T)
+    const long long tot = c->n_pad * TILE;
+    hipLaunchKernelGGL(k_aug_init, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, c->dF,
+                       c->n_pad, P, c->n_pad, c->tr.Faug);
+    HIPCHK(c, hipGetLastError());
+  }
   ev_rec(c, 1);
   CHK(potrf(c, c->tr));
+  CHK(z_from_factor(c));
   ev_rec(c, 2);
   if (invert) {
     CHK(trtri(c, c->tr));
@@ -880,6 +924,21 @@ int factor_and_invert(gpe_ctx* c, int kernel, const double* delta, double nu, do
   }
   ev_rec(c, 3);
   return GPE_OK;
+}
+
+// Z = L^-1 [f H] of the resident factor into c->dZ (n_pad x P, column-major): from the
+// augmented row when the fused sweep carried it, else by forward substitution
+int z_from_factor(gpe_ctx* c) {
+  const int P = c->q + 1;
+  const long long np = c->n_pad;
+  if (c->tr.plan.aug) {
+    const long long tot = np * P;
+    hipLaunchKernelGGL(k_aug_to_cols, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
+                       c->tr.Faug, P, np, c->dZ, np);
+    HIPCHK(c, hipGetLastError());
+    return GPE_OK;
+  }
+  return trsv_lower(c, c->tr, c->dF, np, P, c->dZ, np);
 }
 
 // X = L^-1 of the resident factor into tr.B if the factorisation skipped it
@@ -896,7 +955,7 @@ int ensure_linv(gpe_ctx* c) {
 int trsv_lower(gpe_ctx* c, Fact& F, const double* R, long long ldr, int P, double* Y, long long ldy) {
   for (int c0 = 0; c0 < P; c0 += TS_PM) {
     const int pc = std::min(TS_PM, P - c0);
-    HIPCHK(c, hipMemsetAsync(F.tflags, 0, (size_t)F.NB * sizeof(int), c->stream));
+    HIPCHK(c, hipMemsetAsync(F.tflags, 0, sizeof(int), c->stream));   // the row counter
     hipLaunchKernelGGL(k_trsv_lower, dim3(F.NB), dim3(512), 0, c->stream, F.A, (long long)F.n_pad, F.B,
                        R + (long long)c0 * ldr, ldr, Y + (long long)c0 * ldy, ldy, pc, F.tflags, c->dinfo);
     HIPCHK(c, hipGetLastError());
@@ -957,6 +1016,7 @@ gpe_ctx* gpe_create(int32_t device) {
   gpe_ctx* c = new gpe_ctx();
   c->device = device;
   c->aux.desc_base = AUX_DESC_BASE;
+  c->tr.aug = true;   // the training factorisation carries [f H]^T (L^-1 [f H] from the sweep)
   {
     const char* e = std::getenv("GPEMU_DIAG");
     c->diag_rows = e && std::string(e) == "rows";
@@ -1035,6 +1095,7 @@ void gpe_destroy(gpe_ctx* c) {
   if (c->tr.flags) hipFree(c->tr.flags);
   if (c->aux.flags) hipFree(c->aux.flags);
   if (c->tr.tflags) hipFree(c->tr.tflags);
+  if (c->tr.Faug) hipFree(c->tr.Faug);
   if (c->aux.tflags) hipFree(c->aux.tflags);
   if (c->dprobs) hipFree(c->dprobs);
   if (c->dtiles) hipFree(c->dtiles);
@@ -1153,16 +1214,12 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
     c->gemm_launches = c->gemm_flops = c->gemm_ms = 0.0;
   }
 
-  // value only: no L^-1 (forward substitution with the diagonal inverses instead)
+  // z, w = L^-1 [f H] come out of the factorisation (augmented row); value only runs
+  // no L^-1 at all
   CHK(factor_and_invert(c, kernel, hp, nu, s2, rscale, want_grad != 0));
-  // z, w = L^-1 [f H]
   const int P = q + 1;
   const long long np = c->n_pad;
   const int NBt = c->tr.NB;
-  if (want_grad)
-    CHK(skinny(c, false, c->tr.B, np, c->NB, c->NB, true, c->dF, np, P, c->dZ, np));
-  else
-    CHK(trsv_lower(c, c->tr, c->dF, np, P, c->dZ, np));
   // Gram, log-determinant parts and the failure flag go to the host behind an event;
   // A^-1 = L^-T L^-1 (22 ms at n=16384, independent of the host algebra) is queued
   // before the host waits, so the GPU does not idle over the round trip
@@ -1172,7 +1229,7 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
   HIPCHK(c, hipMemcpyAsync(c->hpin + P * P + NBt, c->dinfo, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipEventRecord(c->ev_host, c->stream));
   ev_rec(c, 4);
-  if (want_grad) CHK(launch_gemm_range(c, c->tr.plan.launches[c->tr.plan.lauum]));
+  if (want_grad) CHK(lauum(c, c->tr));
   ev_rec(c, 5);
   HIPCHK(c, hipEventSynchronize(c->ev_host));
   std::vector<double> G(c->hpin, c->hpin + (size_t)P * P);
@@ -1306,7 +1363,7 @@ static int grow(gpe_ctx* c, double** p, size_t* cap, size_t need) {
 static int ensure_ainv(gpe_ctx* c) {
   if (c->ainv_valid) return GPE_OK;
   CHK(ensure_linv(c));
-  CHK(launch_gemm_range(c, c->tr.plan.launches[c->tr.plan.lauum]));
+  CHK(lauum(c, c->tr));
   c->ainv_valid = true;
   return GPE_OK;
 }
@@ -1442,10 +1499,7 @@ int gpe_beta(gpe_ctx* c, double* beta_out) {
   if (!c->factor_valid) return fail(c, GPE_ERR_STATE, "no resident factor (call gpe_factor)");
   const int P = c->q + 1;
   const long long np = c->n_pad;
-  if (c->linv_valid)
-    CHK(skinny(c, false, c->tr.B, np, c->NB, c->NB, true, c->dF, np, P, c->dZ, np));
-  else
-    CHK(trsv_lower(c, c->tr, c->dF, np, P, c->dZ, np));
+  CHK(z_from_factor(c));   // dZ is scratch of other entries: re-formed from the factor
   std::vector<double> G((size_t)P * P);
   CHK(gram(c, c->dZ, np, P, (int)np, G.data()));
   SmallAlgebra sa = small_from_gram(G, P);
@@ -1752,7 +1806,7 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
           a.s2 = s2; a.coff = coff; a.cdiag = cdiag; a.rscale = 0.0; a.r = nullptr;
           if (dg && rnew) {
             CHK(grow(c, &c->dRn, &c->rn_cap, (size_t)mpa));
-            HIPCHK(c, hipMemsetAsync(c->dRn, 0, (size_t)mpa * sizeof(double), c->stream));
+            // (synchronous copy; padded rows do not read r)
             HIPCHK(c, hipMemcpy(c->dRn, rnew + a0, (size_t)mca * sizeof(double), hipMemcpyHostToDevice));
             a.r = c->dRn;
             a.rscale = s2 * rnew_scale;
@@ -2156,7 +2210,7 @@ int gpe_cholesky(gpe_ctx* c, int64_t m, const double* A, double* L_out, double* 
       CHK(fetch_lower(F.B, Linv_out, false));
     }
     if (Ainv_out) {
-      CHK(launch_gemm_range(c, F.plan.launches[F.plan.lauum]));
+      CHK(lauum(c, F));
       HIPCHK(c, hipStreamSynchronize(c->stream));
       CHK(fetch_lower(F.A, Ainv_out, true));
     }

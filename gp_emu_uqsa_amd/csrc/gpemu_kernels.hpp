@@ -1108,7 +1108,7 @@ constexpr int GEMM_WAIT_TIMEOUT = 0x7fffffff;   // info value after a flag wait 
 // flag seen / multiply done (wall_clock64, 100 MHz).
 #ifdef GEMM_TRACE
 __device__ unsigned long long gemm_trace[8 * 4096];
-#define GTRACE(P, slot) do { if (threadIdx.x == 0 && (P).flag) gemm_trace[(P).diag_col0 / TILE * 8 + (slot)] = wall_clock64(); } while (0)
+#define GTRACE(P, slot) do { if (threadIdx.x == 0 && (P).flag && (P).diag_col0 >= 0) gemm_trace[(P).diag_col0 / TILE * 8 + (slot)] = wall_clock64(); } while (0)
 #else
 #define GTRACE(P, slot) do {} while (0)
 #endif
@@ -1608,9 +1608,10 @@ static __global__ void __launch_bounds__(256) k_trmm_skinny_t(SkinnyArgs a) {
 // inverses the fused Cholesky leaves in the second buffer (Dinv, ld), F / Z column-major
 // n_pad x P (P <= TS_PM; the host runs wider F in column chunks).
 // One workgroup per tile row i: acc = F_i - sum_{j<i} L_ij Z_j, taking each Z_j as soon
-// as row j published flags[j], then Z_i = D_i acc, published on flags[i].  Rows publish
-// in order, so a set flags[i-1] means every earlier one is set, and every wait is on a
-// workgroup dispatched before the waiting one (no dispatch-order deadlock).
+// as row j is published, then Z_i = D_i acc, published by raising the row counter
+// *flags to i + 1.  Rows publish in order (row i only after reading *flags >= i), so the
+// counter is monotone, one poll tells a lagging row every tile it may take, and every
+// wait is on a workgroup dispatched before the waiting one (no dispatch-order deadlock).
 // Thread (r, h), 512 threads: row r of the tile row, k quarter h of every 128 x 128 x P
 // product (L_ij's 32 values are loaded before the wait; D_i's 32 are held from the
 // start), partial sums combined through LDS.  L is read once (n^2/2 x 8 B, HBM-bound);
@@ -1669,25 +1670,26 @@ static __global__ void __launch_bounds__(512) k_trsv_lower(const double* __restr
 #pragma unroll
   for (int p = 0; p < PM; ++p) acc[p] = (h == 0 && p < P) ? frow[(long long)p * ldf] : 0.0;
   const double* lrow = L + (long long)i * TILE + r + (long long)(h * KQ) * ld;
-  int ready = -1;   // flags[0..ready] known set
+  int ready = 0;   // rows [0, ready) known published (lane 0 of wave 0 only)
   for (int j = 0; j < i; ++j) {
     double lv[KQ];
     const double* lt = lrow + (long long)j * TILE * ld;
 #pragma unroll
     for (int k = 0; k < KQ; ++k) lv[k] = lt[(long long)k * ld];
-    if (tid == 0 && j > ready) {
-      int v = gemm_wait_flag(flags + j);
-      if (v == 1) {
-        ready = j;
-        if (j + 1 < i && __hip_atomic_load(flags + i - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          ready = i - 1;
-        }
+    if (tid == 0 && j >= ready) {   // one poll and one acquire per batch of published rows
+      int v = 0;
+      for (long it = 0; it < (1l << 22); ++it) {
+        v = __hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v > j) break;
+        __builtin_amdgcn_s_sleep(4);
       }
-      st = v;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ready = v;
+      st = v > j ? 1 : 0;
     }
     __syncthreads();
-    if (st != 1) {   // a failed or timed-out row: report once, stop
+    if (st != 1) {   // timed out (never expected): report once, stop
       if (tid == 0 && st == 0 && abort_flag) atomicCAS(abort_flag, 0, GEMM_WAIT_TIMEOUT);
       return;
     }
@@ -1724,14 +1726,19 @@ static __global__ void __launch_bounds__(512) k_trsv_lower(const double* __restr
     for (int p = 0; p < PM; ++p) out[p] = fma(dv[k], sh[k * PM + p], out[p]);
   __syncthreads();   // every quarter has read S
   ts_reduce(out, Zs[0], Zs[1], r, h);
+  // Z_i leaves through sc1 (write-through) stores, so the flag needs no L2 write-back
+  // (MI355X guide, valid hand-off forms: sc1 payload, every storing wave's vmcnt(0),
+  // a barrier, then one lane's flag store; the consumer keeps its agent acquire)
   if (h == 0) {
 #pragma unroll
     for (int p = 0; p < PM; ++p)
-      if (p < P) Z[(long long)i * TILE + r + (long long)p * ldz] = out[p];
+      if (p < P)
+        __hip_atomic_store(Z + (long long)i * TILE + r + (long long)p * ldz, out[p], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) gemm_publish_flag(flags + i, 1);
+  if (tid == 0) __hip_atomic_store(flags, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // MFMA form of the skinny products (same grid, chunks and partial layout as the
@@ -2444,6 +2451,26 @@ static __global__ void k_scale_points(const double* X, const double* inv_delta, 
   if (e >= (long long)n_pad * d) return;
   int i = (int)(e / d), k = (int)(e % d);
   xw[e] = (i < n) ? X[e] * inv_delta[k] : 0.0;
+}
+
+// The augmented tile row of the fused Cholesky: [f H]^T as rows under the matrix
+// (TILE x n_pad, ld = TILE): Faug(p, i) = F(i, p) for p < P, rows P..127 zero.  The
+// sweep leaves (L^-1 [f H])^T there (build_plan).
+static __global__ void k_aug_init(const double* F, long long ldf, int P, long long n_pad, double* Faug) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_pad * TILE) return;
+  const int p = (int)(e & (TILE - 1));
+  const long long i = e >> 7;
+  Faug[e] = p < P ? F[i + (long long)p * ldf] : 0.0;
+}
+
+// Z(i, p) = Faug(p, i): the augmented row back as a column-major n_pad x P block
+static __global__ void k_aug_to_cols(const double* Faug, int P, long long n_pad, double* Z, long long ldz) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_pad * P) return;
+  const long long i = e % n_pad;
+  const int p = (int)(e / n_pad);
+  Z[i + (long long)p * ldz] = Faug[p + i * TILE];
 }
 
 // set tile (t,t) of M to the identity for t >= t0 (padding blocks of the inverse)

@@ -138,3 +138,29 @@ def test_objective_vs_oracle_ragged(ctx, n, d):
     assert abs(llh - ref[0]) <= 1e-10 * abs(ref[0])
     ok, err = _grad_ok(grad, ref[1])
     assert ok, err
+
+
+def test_forward_substitution_fallback(monkeypatch):
+    """With the two-stream look-ahead Cholesky (GPEMU_POTRF=lookahead, an A/B switch)
+    the sweep carries no augmented row: L^-1 [f H] then comes from the flag-chained
+    forward substitution (k_trsv_lower) over the diagonal-tile inverses.  Value, gradient
+    and beta against the oracle, ragged n over 11 tile rows."""
+    monkeypatch.setenv("GPEMU_POTRF", "lookahead")
+    c = native.Context(0)
+    try:
+        X, f, H = orc.synthetic_problem(1300, 5, seed=4)
+        c.set_data(X, f, H)
+        hp = np.array([0.6, 0.7, 0.8, 0.9, 1.0, 2e-3, 1.2])
+        llh_v = c.objective(orc.GP4ML, orc.STD, hp, want_grad=False)[0]
+        llh, g, _ = c.objective(orc.GP4ML, orc.STD, hp)
+        ref = orc.objective_fast(X, f, H, hp, orc.GP4ML, orc.STD, True)
+        assert abs(llh_v - ref[0]) <= 1e-10 * abs(ref[0]) and abs(llh - ref[0]) <= 1e-10 * abs(ref[0])
+        ok, err = _grad_ok(g, ref[1])
+        assert ok, err
+        c.factor(native.KERNEL_STD, hp[:5], hp[5], 1.0, 0.0)
+        A, _ = orc.kernel_var_ref(X, hp[:5], hp[5], orc.STD, True)
+        beta = c.beta()
+        bref = orc.optimal_beta_ref(A, H, f)
+        assert np.max(np.abs(beta - bref)) <= 1e-8 * (1 + np.max(np.abs(bref)))
+    finally:
+        c.close()
