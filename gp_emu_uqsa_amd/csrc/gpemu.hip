@@ -169,6 +169,7 @@ struct gpe_ctx {
   // with the standalone diagonal kernel instead of the fused one
   bool potrf_lookahead = false;
   bool skinny_valu = false;   // GPEMU_SKINNY=valu: the VALU skinny kernels (A/B)
+  bool kpairs_shfl = false;   // GPEMU_KPAIRS=shuffle: the lane-shuffle d-reduction K-build (A/B)
   // column-group widths of the fused Cholesky: {width, min remaining columns}, first
   // match wins, else 1 (GPEMU_POTRF_W="4:64,2:32" style)
   std::vector<std::pair<int, int>> potrf_groups = {{4, 80}, {2, 40}};
@@ -690,6 +691,14 @@ int kbuild(gpe_ctx* c, int kernel, double nu, double s2, double rscale) {
   kernel_consts(kernel, nu, true, &coff, &cdiag);
   a.s2 = s2; a.coff = coff; a.cdiag = cdiag;
   a.rscale = rscale; a.r = (c->has_r && rscale != 0.0) ? c->dr : nullptr;
+  if (c->kpairs_shfl && a.d <= 32) {   // A/B: the d-reduction as a lane-shuffle tree
+    const dim3 g(c->NB * (c->NB + 1) / 2), b(256);
+    if (a.d <= 8) hipLaunchKernelGGL(k_pairs_shfl<8>, g, b, 0, c->stream, a);
+    else if (a.d <= 16) hipLaunchKernelGGL(k_pairs_shfl<16>, g, b, 0, c->stream, a);
+    else hipLaunchKernelGGL(k_pairs_shfl<32>, g, b, 0, c->stream, a);
+    HIPCHK(c, hipGetLastError());
+    return GPE_OK;
+  }
   return launch_pairs(c, a, c->NB * (c->NB + 1) / 2);
 }
 
@@ -1022,6 +1031,8 @@ gpe_ctx* gpe_create(int32_t device) {
     c->diag_rows = e && std::string(e) == "rows";
     const char* es = std::getenv("GPEMU_SKINNY");
     c->skinny_valu = es && std::string(es) == "valu";
+    const char* ek = std::getenv("GPEMU_KPAIRS");
+    c->kpairs_shfl = ek && std::string(ek) == "shuffle";
     const char* e2 = std::getenv("GPEMU_POTRF");
     c->potrf_lookahead = e2 && std::string(e2) == "lookahead";
     if (const char* e3 = std::getenv("GPEMU_POTRF_W")) {

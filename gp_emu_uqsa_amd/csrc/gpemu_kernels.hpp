@@ -112,6 +112,55 @@ static __global__ void __launch_bounds__(256) k_pairs(PairArgs a) {
   }
 }
 
+// A/B variant of the training K-build (GPEMU_KPAIRS=shuffle):
+// north_star's "wavefront shuffle reductions over d" taken literally.  Each pair's squared
+// distance is split over 8 lanes (dimensions l, l + 8, ...), summed by a 3-step xor
+// shuffle tree, and lane 0 of the group evaluates exp and stores.  Same values up to the
+// order of the sum over d (<= 1 ulp of s).  k_pairs instead keeps a whole pair in one
+// lane: the d FMAs are serial in registers and every lane evaluates its own exp, which
+// is where the time goes (one fp64 exp per pair); this variant is kept only to measure.
+template <int DMAX>
+static __global__ void __launch_bounds__(256) k_pairs_shfl(PairArgs a) {
+  __shared__ double xs_col[TILE * DMAX];
+  __shared__ double xs_row[TILE * DMAX];
+  int ti, tj;
+  if (a.mode & 1) tri_decode(blockIdx.x, ti, tj);
+  else { ti = blockIdx.x % a.mt; tj = blockIdx.x / a.mt; }
+  const int tid = threadIdx.x, d = a.d;
+  for (int e = tid; e < TILE * DMAX; e += 256) {
+    const int c = e / DMAX, k = e - c * DMAX;
+    xs_col[e] = k < d ? a.xc[(long long)(tj * TILE + c) * d + k] : 0.0;
+    xs_row[e] = k < d ? a.xr[(long long)(ti * TILE + c) * d + k] : 0.0;
+  }
+  __syncthreads();
+  const int lane = tid & 63, g = lane >> 3, l = lane & 7, wave = tid >> 6;
+  const double pre = a.s2 * a.coff;
+  const bool train = (a.mode & 2) != 0;
+  for (int e = wave * 8 + g; e < TILE * TILE; e += 32) {
+    const int r = e & (TILE - 1), c = e >> 7;
+    double s = 0.0;
+#pragma unroll
+    for (int k = l; k < DMAX; k += 8) {
+      const double df = xs_row[r * DMAX + k] - xs_col[c * DMAX + k];
+      s = fma(df, df, s);
+    }
+    s += __shfl_xor(s, 1, 8);
+    s += __shfl_xor(s, 2, 8);
+    s += __shfl_xor(s, 4, 8);
+    if (l == 0) {
+      const int gi = ti * TILE + r, gj = tj * TILE + c;
+      double v = pre * exp(-s);
+      const bool pad = gi >= a.nr_valid || gj >= a.nc_valid;
+      const bool diag = gi == gj;
+      double vdiag = a.s2 * a.cdiag;
+      if (train && a.r && diag && !pad) vdiag += a.rscale * a.r[gi];
+      if (train) v = pad ? (diag ? 1.0 : 0.0) : (diag ? vdiag : v);
+      else v = pad ? 0.0 : v;
+      a.out[gi + (long long)gj * a.ld] = v;
+    }
+  }
+}
+
 // k_pairs for any d (the reference's kernel takes any number of inputs,
 // _emulatorkernels.py:39-50): coordinates staged through LDS 32 dimensions at a
 // time, each thread keeping the running squared distances of its 64 columns.  The
