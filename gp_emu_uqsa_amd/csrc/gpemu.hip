@@ -48,11 +48,12 @@ struct Plan {
   // potrf with depth-1 look-ahead: per step kt the panel launch, the update of
   // column block kt+1 (critical path) and the rest of the trailing update
   std::vector<int> panel, colupd, rest;
-  // fused schedule (default): one launch per column block (see build_plan)
-  std::vector<int> fused;
+  // fused schedule (default): one launch per column block (see build_plan); fused_aug:
+  // the same launches also carrying the augmented row (when the workspace has one)
+  std::vector<int> fused, fused_aug;
   std::vector<int> trtri;   // launches in order
   int lauum = -1;
-  bool aug = false;         // the fused launches carry the augmented row
+  bool aug = false;         // fused_aug is built
   std::vector<Launch> launches;
   std::vector<GemmProb> probs;
   std::vector<unsigned> tiles;   // concatenated tile lists
@@ -158,6 +159,7 @@ struct gpe_ctx {
   // resident factor (gpe_factor)
   bool factor_valid = false;
   bool linv_valid = false;   // tr.B holds L^-1 (TRTRI of the resident L; run on demand)
+  bool zaug_valid = false;   // tr.Faug holds (L^-1 [f H])^T from the last factorisation
   bool ainv_valid = false;   // tr.A holds A^-1 (LAUUM of the resident L^-1)
   int f_kernel = 0;
   std::vector<double> f_delta;
@@ -438,15 +440,17 @@ int build_plan(gpe_ctx* c, Fact& F) {
   double* A = F.A;
   double* B = F.B;
   auto tile = [&](double* M, int i, int j) { return M + (long long)i * TILE + (long long)j * TILE * ld; };
-  // tile (0, j) of the augmented row (ld TILE)
-  const bool aug = F.aug && F.Faug && !c->potrf_lookahead;
-  pl.aug = aug;
+  // tile (0, j) of the augmented row (ld TILE); the fused schedule is built without it
+  // and, when the workspace has one, a second time with it (aug in the lambdas below)
+  pl.aug = F.aug && F.Faug && !c->potrf_lookahead;
+  bool aug = false;
   auto atile = [&](int j) { return F.Faug + (long long)j * TILE * TILE; };
   // --- Cholesky (right-looking, 128-column steps)
   pl.panel.assign(NB, -1);
   pl.colupd.assign(NB, -1);
   pl.rest.assign(NB, -1);
   pl.fused.assign(NB, -1);
+  pl.fused_aug.assign(NB, -1);
   // Fused schedule, one launch per column block t.  Columns are grouped (widths from
   // potrf_groups: wide groups while the trailing matrix is large, width 1 at the end).
   // Launch t, t at position h of group g:
@@ -497,6 +501,9 @@ int build_plan(gpe_ctx* c, Fact& F) {
     g += std::max(1, std::min(w, NB - g));
   }
   gs.push_back(NB);
+  for (int va = 0; va < (pl.aug ? 2 : 1); ++va) {
+  aug = va == 1;
+  std::vector<int>& fidx = aug ? pl.fused_aug : pl.fused;
   for (int gi = 0; gi + 1 < (int)gs.size() && !c->potrf_lookahead; ++gi) {
     const int gb = gs[gi], ge = gs[gi + 1], W1 = ge - gb;
     // previous group's bulk: columns [gb+1, NB) split into W1 parts
@@ -544,9 +551,10 @@ int build_plan(gpe_ctx* c, Fact& F) {
         if (h + 1 < W1) bulk(fp, fl, t + 1, t + 2, g0, Kb);   // the column factored next
         bulk(fp, fl, rng[h].first, rng[h].second, g0, Kb);
       }
-      pl.fused[t] = (int)pl.launches.size();
+      fidx[t] = (int)pl.launches.size();
       add_launch(pl, 4, fp, fl);
     }
+  }
   }
   for (int kt = 0; kt + 1 < NB; ++kt) {
     if (!c->potrf_lookahead) break;
@@ -709,7 +717,7 @@ int kbuild(gpe_ctx* c, int kernel, double nu, double s2, double rscale) {
 // Every launcher of a workspace's schedule first makes sure it is built: growing the
 // tile-list array for one workspace's plan resets the other's (build_plan), e.g. the
 // aux plan of gpe_noise_sample between gpe_factor and a later on-demand TRTRI / LAUUM.
-int potrf(gpe_ctx* c, Fact& F) {
+int potrf(gpe_ctx* c, Fact& F, bool with_aug = false) {
   CHK(build_plan(c, F));
   const Plan& pl = F.plan;
   const int NB = F.NB;
@@ -717,7 +725,8 @@ int potrf(gpe_ctx* c, Fact& F) {
     // fused: one launch per step; the diagonal tile kt+1 is factored by the first
     // workgroup of the trailing-update launch kt and its panel follows in-launch
     HIPCHK(c, hipMemsetAsync(F.flags, 0, (size_t)NB * sizeof(int), c->stream));
-    for (int t = 0; t < NB; ++t) CHK(launch_gemm_range(c, pl.launches[pl.fused[t]]));
+    const std::vector<int>& fidx = (with_aug && pl.aug) ? pl.fused_aug : pl.fused;
+    for (int t = 0; t < NB; ++t) CHK(launch_gemm_range(c, pl.launches[fidx[t]]));
     return GPE_OK;
   }
   if ((int)c->ev_panel.size() < NB) {
@@ -917,36 +926,42 @@ int factor_and_invert(gpe_ctx* c, int kernel, const double* delta, double nu, do
   CHK(scale_training(c, delta));
   CHK(kbuild(c, kernel, nu, s2, rscale));
   const int P = c->q + 1;
-  if (c->tr.plan.aug) {   // [f H]^T into the augmented row (the sweep turns it into Z^T)
+  // without the inverse (value only, gpe_factor) the sweep carries [f H]^T in the
+  // augmented row and leaves L^-1 [f H] there; with it, L^-1 [f H] is one skinny product
+  // with L^-1 and the sweep stays lean
+  c->zaug_valid = !invert && c->tr.plan.aug;
+  if (c->zaug_valid) {
     const long long tot = c->n_pad * TILE;
     hipLaunchKernelGGL(k_aug_init, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, c->dF,
                        c->n_pad, P, c->n_pad, c->tr.Faug);
     HIPCHK(c, hipGetLastError());
   }
   ev_rec(c, 1);
-  CHK(potrf(c, c->tr));
-  CHK(z_from_factor(c));
+  CHK(potrf(c, c->tr, c->zaug_valid));
   ev_rec(c, 2);
   if (invert) {
     CHK(trtri(c, c->tr));
     c->linv_valid = true;
   }
+  CHK(z_from_factor(c));
   ev_rec(c, 3);
   return GPE_OK;
 }
 
 // Z = L^-1 [f H] of the resident factor into c->dZ (n_pad x P, column-major): from the
-// augmented row when the fused sweep carried it, else by forward substitution
+// augmented row when the fused sweep carried it, else as L^-1 times [f H] when L^-1 is
+// resident, else by forward substitution
 int z_from_factor(gpe_ctx* c) {
   const int P = c->q + 1;
   const long long np = c->n_pad;
-  if (c->tr.plan.aug) {
+  if (c->zaug_valid) {
     const long long tot = np * P;
     hipLaunchKernelGGL(k_aug_to_cols, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
                        c->tr.Faug, P, np, c->dZ, np);
     HIPCHK(c, hipGetLastError());
     return GPE_OK;
   }
+  if (c->linv_valid) return skinny(c, false, c->tr.B, np, c->NB, c->NB, true, c->dF, np, P, c->dZ, np);
   return trsv_lower(c, c->tr, c->dF, np, P, c->dZ, np);
 }
 
@@ -1025,7 +1040,12 @@ gpe_ctx* gpe_create(int32_t device) {
   gpe_ctx* c = new gpe_ctx();
   c->device = device;
   c->aux.desc_base = AUX_DESC_BASE;
-  c->tr.aug = true;   // the training factorisation carries [f H]^T (L^-1 [f H] from the sweep)
+  // the training factorisation carries [f H]^T (L^-1 [f H] from the sweep); GPEMU_AUG=0
+  // (A/B switch) takes L^-1 [f H] from the forward substitution instead
+  {
+    const char* ea = std::getenv("GPEMU_AUG");
+    c->tr.aug = !(ea && std::string(ea) == "0");
+  }
   {
     const char* e = std::getenv("GPEMU_DIAG");
     c->diag_rows = e && std::string(e) == "rows";
@@ -1147,6 +1167,8 @@ int gpe_set_data(gpe_ctx* c, int64_t n, int32_t d, int32_t q, const double* X, c
   c->factor_valid = false;
   c->ainv_valid = false;
   c->x32_valid = false;
+  c->zaug_valid = false;
+  c->linv_valid = false;
   if (resize) {
     CHK(ensure_fact(c, c->tr, n_pad));
     CHK(dalloc(c, &c->dX, (size_t)n_pad * d));
