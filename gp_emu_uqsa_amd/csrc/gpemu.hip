@@ -52,6 +52,11 @@ struct Plan {
   // the same launches also carrying the augmented row (when the workspace has one)
   std::vector<int> fused, fused_aug;
   std::vector<int> trtri;   // launches in order
+  // the same triangular inverse split for the overlapped tail (potrf_overlap): the pairs
+  // inside the leading block [0, split) (their L is final once the Cholesky reaches the
+  // tail), then the rest; split = 0: not built
+  int split = 0;
+  std::vector<int> trtri_lead, trtri_rest;
   int lauum = -1;
   bool aug = false;         // fused_aug is built
   std::vector<Launch> launches;
@@ -176,6 +181,14 @@ struct gpe_ctx {
   // match wins, else 1 (GPEMU_POTRF_W="4:64,2:32" style)
   std::vector<std::pair<int, int>> potrf_groups = {{4, 80}, {2, 40}};
 
+  // overlapped Cholesky tail (potrf_trtri_overlap): the width-1 tail steps on one half of
+  // the CUs, the triangular inverse of the leading block on the other half (CU-masked
+  // streams, created on first use).  A/B switch GPEMU_TAIL_OVERLAP=1; off by default: it
+  // measured slower
+  bool tail_overlap = false;
+  bool tail_streams_ok = false, tail_streams_tried = false;
+  hipStream_t st_tail = nullptr, st_fill = nullptr;
+  hipEvent_t ev_split = nullptr, ev_tail = nullptr, ev_fill = nullptr;
   // look-ahead stream and events
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -580,7 +593,9 @@ int build_plan(gpe_ctx* c, Fact& F) {
                  (double)(m - 1) * T * ((double)(m - 1) * T + 1.0) * T);
     }
   }
-  // --- triangular inverse X = L^-1 in B (diagonal tiles already hold Dinv)
+  // --- triangular inverse X = L^-1 in B (diagonal tiles already hold Dinv); sel: 0 all
+  // pairs, 1 the pairs inside [0, split), 2 the others
+  auto build_trtri = [&](int sel, int split, std::vector<int>& out) {
   for (int s = 2; s / 2 < NB; s *= 2) {
     std::vector<GemmProb> pa, pb;
     double fa = 0.0, fb = 0.0;
@@ -588,6 +603,8 @@ int build_plan(gpe_ctx* c, Fact& F) {
       const int h = t0 + s / 2;
       if (h >= NB) continue;
       const int t1 = std::min(t0 + s, NB);
+      if (sel == 1 && t1 > split) continue;
+      if (sel == 2 && t1 <= split) continue;
       const int a = h - t0, b = t1 - h;
       // T^T (a x b tiles, stored in the upper block rows t0:h, cols h:t1 of B)
       //   = X11^T L21^T ;  opA(m,k) = X11(k,m): K-contiguous, upper -> kbeg = ti*128
@@ -600,10 +617,23 @@ int build_plan(gpe_ctx* c, Fact& F) {
       fb += (double)b * T * b * T * a * T;
     }
     if (pa.empty()) continue;
-    pl.trtri.push_back((int)pl.launches.size());
+    out.push_back((int)pl.launches.size());
     add_launch(pl, 1, pa, fa);
-    pl.trtri.push_back((int)pl.launches.size());
+    out.push_back((int)pl.launches.size());
     add_launch(pl, 0, pb, fb);
+  }
+  };
+  build_trtri(0, 0, pl.trtri);
+  // the overlapped tail: the width-1 steps of the fused Cholesky (the chain-bound end)
+  if (!c->potrf_lookahead && F.aug && NB >= 64) {
+    int split = 0;
+    for (size_t gi = 0; gi + 1 < gs.size(); ++gi)
+      if (gs[gi + 1] - gs[gi] == 1) { split = gs[gi]; break; }
+    if (split >= 16 && split < NB) {
+      pl.split = split;
+      build_trtri(1, split, pl.trtri_lead);
+      build_trtri(2, split, pl.trtri_rest);
+    }
   }
   // --- A^-1 = X^T X (lower tiles), written over L in A
   pl.lauum = (int)pl.launches.size();
@@ -769,6 +799,52 @@ int potrf(gpe_ctx* c, Fact& F, bool with_aug = false) {
 }
 
 // A^-1 = X^T X over L (the plan's LAUUM launch)
+void ev_rec(gpe_ctx* c, int i);
+
+// CU-masked streams for potrf_overlap: bits [0, 128) and [128, 256) of the mask are
+// disjoint halves, 16 CUs of every XCD each (tools/hip/cumask_probe.hip on gfx950)
+bool ensure_tail_streams(gpe_ctx* c) {
+  if (c->tail_streams_tried) return c->tail_streams_ok;
+  c->tail_streams_tried = true;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, c->device) != hipSuccess || prop.multiProcessorCount < 64) return false;
+  const int ncu = prop.multiProcessorCount, words = (ncu + 31) / 32;
+  std::vector<unsigned> lo(words, 0u), hi(words, 0u);
+  for (int b = 0; b < ncu; ++b) (b < ncu / 2 ? lo : hi)[b >> 5] |= 1u << (b & 31);
+  c->tail_streams_ok = hipExtStreamCreateWithCUMask(&c->st_tail, words, lo.data()) == hipSuccess &&
+                       hipExtStreamCreateWithCUMask(&c->st_fill, words, hi.data()) == hipSuccess &&
+                       hipEventCreateWithFlags(&c->ev_split, hipEventDisableTiming) == hipSuccess &&
+                       hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming) == hipSuccess &&
+                       hipEventCreateWithFlags(&c->ev_fill, hipEventDisableTiming) == hipSuccess;
+  return c->tail_streams_ok;
+}
+
+// Cholesky + triangular inverse with the chain-bound tail overlapped: steps [0, split)
+// on the context stream (every CU); then, on two disjoint halves of the CUs at once, the
+// width-1 tail steps [split, NB) and the inverse of the leading block [0, split) (its L
+// is final: DESIGN.md section 6.3); then the rest of the inverse on the context stream.
+// A plain stream beside the tail slowed its chain (the factorisation shares a CU with a
+// long inverse tile); the masks keep the chain's CUs free of them.
+int potrf_trtri_overlap(gpe_ctx* c, Fact& F) {
+  CHK(build_plan(c, F));
+  const Plan& pl = F.plan;
+  const int NB = F.NB, split = pl.split;
+  HIPCHK(c, hipMemsetAsync(F.flags, 0, (size_t)NB * sizeof(int), c->stream));
+  for (int t = 0; t < split; ++t) CHK(launch_gemm_range(c, pl.launches[pl.fused[t]]));
+  HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->st_tail, c->ev_split, 0));
+  HIPCHK(c, hipStreamWaitEvent(c->st_fill, c->ev_split, 0));
+  for (int t = split; t < NB; ++t) CHK(launch_gemm_range(c, pl.launches[pl.fused[t]], c->st_tail));
+  for (int li : pl.trtri_lead) CHK(launch_gemm_range(c, pl.launches[li], c->st_fill));
+  HIPCHK(c, hipEventRecord(c->ev_tail, c->st_tail));
+  HIPCHK(c, hipEventRecord(c->ev_fill, c->st_fill));
+  HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_tail, 0));
+  HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_fill, 0));
+  ev_rec(c, 2);
+  for (int li : pl.trtri_rest) CHK(launch_gemm_range(c, pl.launches[li]));
+  return GPE_OK;
+}
+
 int lauum(gpe_ctx* c, Fact& F) {
   CHK(build_plan(c, F));
   return launch_gemm_range(c, F.plan.launches[F.plan.lauum]);
@@ -920,6 +996,10 @@ int trsv_lower(gpe_ctx* c, Fact& F, const double* R, long long ldr, int P, doubl
 int factor_and_invert(gpe_ctx* c, int kernel, const double* delta, double nu, double s2,
                       double rscale, bool invert = true) {
   c->linv_valid = false;
+  if (c->tail_streams_ok) {   // a failed earlier call may have left work on the tail streams
+    HIPCHK(c, hipStreamSynchronize(c->st_tail));
+    HIPCHK(c, hipStreamSynchronize(c->st_fill));
+  }
   HIPCHK(c, hipMemsetAsync(c->dinfo, 0, sizeof(int), c->stream));
   CHK(build_plan(c, c->tr));
   ev_rec(c, 0);
@@ -937,11 +1017,17 @@ int factor_and_invert(gpe_ctx* c, int kernel, const double* delta, double nu, do
     HIPCHK(c, hipGetLastError());
   }
   ev_rec(c, 1);
-  CHK(potrf(c, c->tr, c->zaug_valid));
-  ev_rec(c, 2);
-  if (invert) {
-    CHK(trtri(c, c->tr));
+  CHK(build_plan(c, c->tr));
+  if (invert && c->tail_overlap && c->tr.plan.split > 0 && ensure_tail_streams(c)) {
+    CHK(potrf_trtri_overlap(c, c->tr));   // records phase event 2 at the join
     c->linv_valid = true;
+  } else {
+    CHK(potrf(c, c->tr, c->zaug_valid));
+    ev_rec(c, 2);
+    if (invert) {
+      CHK(trtri(c, c->tr));
+      c->linv_valid = true;
+    }
   }
   CHK(z_from_factor(c));
   ev_rec(c, 3);
@@ -1051,6 +1137,8 @@ gpe_ctx* gpe_create(int32_t device) {
     c->diag_rows = e && std::string(e) == "rows";
     const char* es = std::getenv("GPEMU_SKINNY");
     c->skinny_valu = es && std::string(es) == "valu";
+    const char* et = std::getenv("GPEMU_TAIL_OVERLAP");
+    c->tail_overlap = et && std::string(et) == "1";
     const char* ek = std::getenv("GPEMU_KPAIRS");
     c->kpairs_shfl = ek && std::string(ek) == "shuffle";
     const char* e2 = std::getenv("GPEMU_POTRF");
@@ -1143,6 +1231,13 @@ void gpe_destroy(gpe_ctx* c) {
     (void)hipStreamSynchronize(c->stream2);
     (void)hipStreamDestroy(c->stream2);
   }
+  for (hipStream_t st : {c->st_tail, c->st_fill})
+    if (st) {
+      (void)hipStreamSynchronize(st);
+      (void)hipStreamDestroy(st);
+    }
+  for (hipEvent_t e : {c->ev_split, c->ev_tail, c->ev_fill})
+    if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }

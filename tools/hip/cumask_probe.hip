@@ -58,6 +58,31 @@ int main() {
   run("bits 0-31", first32);
   std::vector<unsigned> every4(words, 0x11111111u);
   run("every 4th bit", every4);
+  // halves: are bits [0, 128) and [128, 256) disjoint CU sets?
+  std::vector<unsigned> lo(words, 0u), hi(words, 0u);
+  for (int w = 0; w < words; ++w) (w < words / 2 ? lo : hi)[w] = 0xffffffffu;
+  run("bits 0-127", lo);
+  run("bits 128-255", hi);
+  {
+    auto cus = [&](std::vector<unsigned> mask) {
+      std::set<std::tuple<int, int, int>> used;
+      hipStream_t s;
+      if (hipExtStreamCreateWithCUMask(&s, words, mask.data()) != hipSuccess) return used;
+      hipLaunchKernelGGL(probe, dim3(nwg), dim3(64), 0, s, d, 20000);
+      (void)hipStreamSynchronize(s);
+      (void)hipMemcpy(h.data(), d, h.size() * 4, hipMemcpyDeviceToHost);
+      for (int i = 0; i < nwg; ++i) {
+        unsigned hw = h[2 * i], xcc = h[2 * i + 1] & 0xf;
+        used.insert({(int)xcc, (int)(((hw >> 13) & 3) * 2 + ((hw >> 12) & 1)), (int)((hw >> 8) & 0xf)});
+      }
+      (void)hipStreamDestroy(s);
+      return used;
+    };
+    auto a = cus(lo), b = cus(hi);
+    int both = 0;
+    for (auto& u : a) both += b.count(u);
+    printf("halves: %zu + %zu CUs, %d in both\n", a.size(), b.size(), both);
+  }
   std::vector<unsigned> low8(words, 0u); low8[0] = 0xffu;
   run("bits 0-7", low8);
   std::vector<unsigned> not4(words, 0xeeeeeeeeu);
