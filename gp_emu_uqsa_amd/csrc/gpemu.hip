@@ -186,6 +186,11 @@ struct gpe_ctx {
   // streams, created on first use).  A/B switch GPEMU_TAIL_OVERLAP=1; off by default: it
   // measured slower
   bool tail_overlap = false;
+  // GPEMU_TAIL_OVERLAP=2: the leading block's inverse on a plain second stream (no CU
+  // mask) from Cholesky step tail_split on (GPEMU_TAIL_SPLIT, default 64), the Cholesky
+  // staying on the context stream: the bulk-bound middle of the sweep absorbs it
+  int tail_mode = 0, tail_split = 64;
+  hipStream_t st_plain = nullptr;
   bool tail_streams_ok = false, tail_streams_tried = false;
   hipStream_t st_tail = nullptr, st_fill = nullptr;
   hipEvent_t ev_split = nullptr, ev_tail = nullptr, ev_fill = nullptr;
@@ -627,8 +632,12 @@ int build_plan(gpe_ctx* c, Fact& F) {
   // the overlapped tail: the width-1 steps of the fused Cholesky (the chain-bound end)
   if (!c->potrf_lookahead && F.aug && NB >= 64) {
     int split = 0;
-    for (size_t gi = 0; gi + 1 < gs.size(); ++gi)
-      if (gs[gi + 1] - gs[gi] == 1) { split = gs[gi]; break; }
+    if (c->tail_mode == 2) {
+      split = std::min(c->tail_split, NB - 1);
+    } else {
+      for (size_t gi = 0; gi + 1 < gs.size(); ++gi)
+        if (gs[gi + 1] - gs[gi] == 1) { split = gs[gi]; break; }
+    }
     if (split >= 16 && split < NB) {
       pl.split = split;
       build_trtri(1, split, pl.trtri_lead);
@@ -811,7 +820,8 @@ bool ensure_tail_streams(gpe_ctx* c) {
   const int ncu = prop.multiProcessorCount, words = (ncu + 31) / 32;
   std::vector<unsigned> lo(words, 0u), hi(words, 0u);
   for (int b = 0; b < ncu; ++b) (b < ncu / 2 ? lo : hi)[b >> 5] |= 1u << (b & 31);
-  c->tail_streams_ok = hipExtStreamCreateWithCUMask(&c->st_tail, words, lo.data()) == hipSuccess &&
+  c->tail_streams_ok = hipStreamCreateWithFlags(&c->st_plain, hipStreamNonBlocking) == hipSuccess &&
+                       hipExtStreamCreateWithCUMask(&c->st_tail, words, lo.data()) == hipSuccess &&
                        hipExtStreamCreateWithCUMask(&c->st_fill, words, hi.data()) == hipSuccess &&
                        hipEventCreateWithFlags(&c->ev_split, hipEventDisableTiming) == hipSuccess &&
                        hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming) == hipSuccess &&
@@ -832,6 +842,16 @@ int potrf_trtri_overlap(gpe_ctx* c, Fact& F) {
   HIPCHK(c, hipMemsetAsync(F.flags, 0, (size_t)NB * sizeof(int), c->stream));
   for (int t = 0; t < split; ++t) CHK(launch_gemm_range(c, pl.launches[pl.fused[t]]));
   HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
+  if (c->tail_mode == 2) {   // plain second stream beside the rest of the sweep
+    HIPCHK(c, hipStreamWaitEvent(c->st_plain, c->ev_split, 0));
+    for (int li : pl.trtri_lead) CHK(launch_gemm_range(c, pl.launches[li], c->st_plain));
+    HIPCHK(c, hipEventRecord(c->ev_fill, c->st_plain));
+    for (int t = split; t < NB; ++t) CHK(launch_gemm_range(c, pl.launches[pl.fused[t]]));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_fill, 0));
+    ev_rec(c, 2);
+    for (int li : pl.trtri_rest) CHK(launch_gemm_range(c, pl.launches[li]));
+    return GPE_OK;
+  }
   HIPCHK(c, hipStreamWaitEvent(c->st_tail, c->ev_split, 0));
   HIPCHK(c, hipStreamWaitEvent(c->st_fill, c->ev_split, 0));
   for (int t = split; t < NB; ++t) CHK(launch_gemm_range(c, pl.launches[pl.fused[t]], c->st_tail));
@@ -999,6 +1019,7 @@ int factor_and_invert(gpe_ctx* c, int kernel, const double* delta, double nu, do
   if (c->tail_streams_ok) {   // a failed earlier call may have left work on the tail streams
     HIPCHK(c, hipStreamSynchronize(c->st_tail));
     HIPCHK(c, hipStreamSynchronize(c->st_fill));
+    HIPCHK(c, hipStreamSynchronize(c->st_plain));
   }
   HIPCHK(c, hipMemsetAsync(c->dinfo, 0, sizeof(int), c->stream));
   CHK(build_plan(c, c->tr));
@@ -1138,7 +1159,9 @@ gpe_ctx* gpe_create(int32_t device) {
     const char* es = std::getenv("GPEMU_SKINNY");
     c->skinny_valu = es && std::string(es) == "valu";
     const char* et = std::getenv("GPEMU_TAIL_OVERLAP");
-    c->tail_overlap = et && std::string(et) == "1";
+    c->tail_mode = et ? std::atoi(et) : 0;
+    c->tail_overlap = c->tail_mode == 1 || c->tail_mode == 2;
+    if (const char* es = std::getenv("GPEMU_TAIL_SPLIT")) c->tail_split = std::atoi(es);
     const char* ek = std::getenv("GPEMU_KPAIRS");
     c->kpairs_shfl = ek && std::string(ek) == "shuffle";
     const char* e2 = std::getenv("GPEMU_POTRF");
@@ -1231,7 +1254,7 @@ void gpe_destroy(gpe_ctx* c) {
     (void)hipStreamSynchronize(c->stream2);
     (void)hipStreamDestroy(c->stream2);
   }
-  for (hipStream_t st : {c->st_tail, c->st_fill})
+  for (hipStream_t st : {c->st_tail, c->st_fill, c->st_plain})
     if (st) {
       (void)hipStreamSynchronize(st);
       (void)hipStreamDestroy(st);
