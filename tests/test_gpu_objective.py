@@ -162,6 +162,13 @@ def test_forward_substitution_fallback(monkeypatch):
         beta = c.beta()
         bref = orc.optimal_beta_ref(A, H, f)
         assert np.max(np.abs(beta - bref)) <= 1e-8 * (1 + np.max(np.abs(bref)))
+        # [f H] wider than one 16-column pass of the substitution (d = 20: 22 columns)
+        X2, f2, H2 = orc.synthetic_problem(700, 20, seed=6)
+        c.set_data(X2, f2, H2)
+        hp2 = np.concatenate([np.linspace(1.5, 3.0, 20), [2e-3, 0.9]])
+        v2 = c.objective(orc.GP4ML, orc.STD, hp2, want_grad=False)[0]
+        r2 = orc.objective_fast(X2, f2, H2, hp2, orc.GP4ML, orc.STD, True)[0]
+        assert abs(v2 - r2) <= 1e-10 * abs(r2), (v2, r2)
     finally:
         c.close()
 
