@@ -59,6 +59,13 @@ struct Plan {
   std::vector<int> trtri_lead, trtri_rest;
   int lauum = -1;
   bool aug = false;         // fused_aug is built
+  // two-stream group schedule (potrf_g2s, GPEMU_POTRF=g2s): for groups of width >= 2 a
+  // chain launch per step (diagonal, panels, the next column's update) and ONE trailing-
+  // update launch per group on the other stream; width-1 groups run their fused launches
+  bool g2s = false;
+  std::vector<int> g2s_gs;                    // group starts, then NB
+  std::vector<int> g2s_step, g2s_step_aug;    // per step: launch index
+  std::vector<int> g2s_bulk, g2s_bulk_aug;    // per group: trailing-update launch, or -1
   std::vector<Launch> launches;
   std::vector<GemmProb> probs;
   std::vector<unsigned> tiles;   // concatenated tile lists
@@ -175,6 +182,8 @@ struct gpe_ctx {
   // A/B switch: GPEMU_POTRF=lookahead selects the two-stream look-ahead schedule
   // with the standalone diagonal kernel instead of the fused one
   bool potrf_lookahead = false;
+  bool potrf_g2s = false;   // GPEMU_POTRF=g2s: the two-stream group schedule (potrf_g2s)
+  std::vector<hipEvent_t> ev_gbulk, ev_gchain;
   bool skinny_valu = false;   // GPEMU_SKINNY=valu: the VALU skinny kernels (A/B)
   bool kpairs_shfl = false;   // GPEMU_KPAIRS=shuffle: the lane-shuffle d-reduction K-build (A/B)
   // column-group widths of the fused Cholesky: {width, min remaining columns}, first
@@ -573,6 +582,55 @@ int build_plan(gpe_ctx* c, Fact& F) {
       add_launch(pl, 4, fp, fl);
     }
   }
+  // the two-stream group schedule: the same chain tiles without the trailing-update
+  // shares, which form one plain launch per group (columns [ge, NB) by the previous group)
+  if (c->potrf_g2s && !c->potrf_lookahead) {
+    pl.g2s = true;
+    pl.g2s_gs = gs;
+    std::vector<int>& sidx = aug ? pl.g2s_step_aug : pl.g2s_step;
+    std::vector<int>& bidx = aug ? pl.g2s_bulk_aug : pl.g2s_bulk;
+    sidx.assign(NB, -1);
+    bidx.assign(gs.size(), -1);
+    for (int gi = 0; gi + 1 < (int)gs.size(); ++gi) {
+      const int gb = gs[gi], ge = gs[gi + 1], W1 = ge - gb;
+      if (W1 < 2) {   // width 1: the fused launch as it is (its own trailing update)
+        sidx[gb] = fidx[gb];
+        continue;
+      }
+      for (int h = 0; h < W1; ++h) {
+        const int t = gb + h;
+        const int p0 = (h == 0) ? (gi > 0 ? gs[gi - 1] : 0) : gb;
+        const int K = (t - p0) * TILE;
+        const double al = K ? -1.0 : 1.0;
+        const int m = NB - t - 1;
+        std::vector<GemmProb> fp = {diagprob(t, K ? tile(A, t, p0) : nullptr, K, al)};
+        double fl = T * (T + 1.0) * K;
+        if (m >= 1) {
+          fp.push_back(panelprob(t, K ? tile(A, t + 1, p0) : nullptr, K ? tile(A, t, p0) : nullptr, K, al));
+          fl += 2.0 * m * T * T * K + (double)m * T * T * T;
+        }
+        if (aug) {
+          GemmProb pa = mkprob(K ? atile(p0) : nullptr, TILE, K ? tile(A, t, p0) : nullptr, ld, atile(t), TILE,
+                               1, 1, K, G_PANEL, al, 1.0);
+          pa.X = tile(B, t, t);
+          pa.ldx = ld;
+          pa.flag = F.flags + t;
+          pa.diag_col0 = -TILE;
+          fp.push_back(pa);
+        }
+        if (gi > 0 && h + 1 < W1) bulk(fp, fl, t + 1, t + 2, gs[gi - 1], (gb - gs[gi - 1]) * TILE);
+        sidx[t] = (int)pl.launches.size();
+        add_launch(pl, 4, fp, fl);
+      }
+      if (gi > 0 && ge < NB) {
+        std::vector<GemmProb> fp;
+        double fl = 0.0;
+        bulk(fp, fl, ge, NB, gs[gi - 1], (gb - gs[gi - 1]) * TILE);
+        bidx[gi] = (int)pl.launches.size();
+        add_launch(pl, 0, fp, fl);
+      }
+    }
+  }
   }
   for (int kt = 0; kt + 1 < NB; ++kt) {
     if (!c->potrf_lookahead) break;
@@ -756,10 +814,63 @@ int kbuild(gpe_ctx* c, int kernel, double nu, double s2, double rscale) {
 // Every launcher of a workspace's schedule first makes sure it is built: growing the
 // tile-list array for one workspace's plan resets the other's (build_plan), e.g. the
 // aux plan of gpe_noise_sample between gpe_factor and a later on-demand TRTRI / LAUUM.
+// Two-stream group schedule.  Groups of width >= 2: the chain launches of group g (their
+// diagonal factorisations, panels and the next column's update) on the high-priority
+// stream2 and, beside them on the context stream, ONE launch updating the columns beyond
+// g by group g - 1: its tiles no longer drain at every step's launch boundary.  B(g) waits
+// for the chain of g - 1 (its panels); the chain of g + 1 waits for B(g) (its columns'
+// update by g - 1).  Width-1 groups (the chain-bound tail) run their fused launches on the
+// context stream after the join.  Writes are disjoint: B(g) touches columns >= end(g), the
+// chain of g only the columns of g.
+int potrf_g2s(gpe_ctx* c, Fact& F, bool with_aug) {
+  const Plan& pl = F.plan;
+  const int NB = F.NB;
+  const std::vector<int>& gs = pl.g2s_gs;
+  const std::vector<int>& sidx = with_aug ? pl.g2s_step_aug : pl.g2s_step;
+  const std::vector<int>& bidx = with_aug ? pl.g2s_bulk_aug : pl.g2s_bulk;
+  const int ng = (int)gs.size() - 1;
+  if ((int)c->ev_gbulk.size() < ng) {
+    for (auto& e : c->ev_gbulk) (void)hipEventDestroy(e);
+    for (auto& e : c->ev_gchain) (void)hipEventDestroy(e);
+    c->ev_gbulk.assign(ng, nullptr);
+    c->ev_gchain.assign(ng, nullptr);
+    for (int i = 0; i < ng; ++i) {
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_gbulk[i], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_gchain[i], hipEventDisableTiming));
+    }
+  }
+  hipStream_t mainst = c->stream, chain = c->stream2;
+  HIPCHK(c, hipMemsetAsync(F.flags, 0, (size_t)NB * sizeof(int), mainst));
+  HIPCHK(c, hipEventRecord(c->ev_fork, mainst));
+  HIPCHK(c, hipStreamWaitEvent(chain, c->ev_fork, 0));
+  int last_two = -1;   // the last group of width >= 2 so far
+  for (int gi = 0; gi < ng; ++gi) {
+    const int gb = gs[gi], ge = gs[gi + 1];
+    if (ge - gb >= 2) {
+      if (bidx[gi] >= 0) {
+        HIPCHK(c, hipStreamWaitEvent(mainst, c->ev_gchain[gi - 1], 0));
+        CHK(launch_gemm_range(c, pl.launches[bidx[gi]], mainst));
+        HIPCHK(c, hipEventRecord(c->ev_gbulk[gi], mainst));
+      }
+      if (gi > 0 && bidx[gi - 1] >= 0) HIPCHK(c, hipStreamWaitEvent(chain, c->ev_gbulk[gi - 1], 0));
+      for (int t = gb; t < ge; ++t) CHK(launch_gemm_range(c, pl.launches[sidx[t]], chain));
+      HIPCHK(c, hipEventRecord(c->ev_gchain[gi], chain));
+      last_two = gi;
+    } else {
+      if (last_two == gi - 1 && last_two >= 0)   // join: the tail runs on the context stream
+        HIPCHK(c, hipStreamWaitEvent(mainst, c->ev_gchain[last_two], 0));
+      CHK(launch_gemm_range(c, pl.launches[sidx[gb]], mainst));
+    }
+  }
+  if (last_two == ng - 1) HIPCHK(c, hipStreamWaitEvent(mainst, c->ev_gchain[last_two], 0));
+  return GPE_OK;
+}
+
 int potrf(gpe_ctx* c, Fact& F, bool with_aug = false) {
   CHK(build_plan(c, F));
   const Plan& pl = F.plan;
   const int NB = F.NB;
+  if (pl.g2s) return potrf_g2s(c, F, with_aug && pl.aug);
   if (!c->potrf_lookahead) {
     // fused: one launch per step; the diagonal tile kt+1 is factored by the first
     // workgroup of the trailing-update launch kt and its panel follows in-launch
@@ -1166,6 +1277,7 @@ gpe_ctx* gpe_create(int32_t device) {
     c->kpairs_shfl = ek && std::string(ek) == "shuffle";
     const char* e2 = std::getenv("GPEMU_POTRF");
     c->potrf_lookahead = e2 && std::string(e2) == "lookahead";
+    c->potrf_g2s = e2 && std::string(e2) == "g2s";
     if (const char* e3 = std::getenv("GPEMU_POTRF_W")) {
       c->potrf_groups.clear();
       std::string spec(e3);
@@ -1247,6 +1359,8 @@ void gpe_destroy(gpe_ctx* c) {
   for (auto& e : c->gev) (void)hipEventDestroy(e);
   for (auto& e : c->ev_panel) (void)hipEventDestroy(e);
   for (auto& e : c->ev_rest) (void)hipEventDestroy(e);
+  for (auto& e : c->ev_gbulk) (void)hipEventDestroy(e);
+  for (auto& e : c->ev_gchain) (void)hipEventDestroy(e);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->ev_host) (void)hipEventDestroy(c->ev_host);
