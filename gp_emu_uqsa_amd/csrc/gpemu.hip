@@ -189,6 +189,7 @@ struct gpe_ctx {
   // column-group widths of the fused Cholesky: {width, min remaining columns}, first
   // match wins, else 1 (GPEMU_POTRF_W="4:64,2:32" style)
   std::vector<std::pair<int, int>> potrf_groups = {{4, 80}, {2, 40}};
+  int potrf_first = 0;   // width of the first column group (0: as potrf_groups)
 
   // overlapped Cholesky tail (potrf_trtri_overlap): the width-1 tail steps on one half of
   // the CUs, the triangular inverse of the leading block on the other half (CU-masked
@@ -525,6 +526,9 @@ int build_plan(gpe_ctx* c, Fact& F) {
     int w = 1;
     for (const auto& r : c->potrf_groups)
       if (NB - g > r.second) { w = r.first; break; }
+    // the first group has no trailing update to carry (nothing precedes it): a narrower
+    // first group starts the first update sooner (GPEMU_POTRF_FIRST)
+    if (g == 0 && c->potrf_first > 0) w = c->potrf_first;
     g += std::max(1, std::min(w, NB - g));
   }
   gs.push_back(NB);
@@ -1278,6 +1282,7 @@ gpe_ctx* gpe_create(int32_t device) {
     const char* e2 = std::getenv("GPEMU_POTRF");
     c->potrf_lookahead = e2 && std::string(e2) == "lookahead";
     c->potrf_g2s = e2 && std::string(e2) == "g2s";
+    if (const char* ef = std::getenv("GPEMU_POTRF_FIRST")) c->potrf_first = std::max(0, std::min(8, std::atoi(ef)));
     if (const char* e3 = std::getenv("GPEMU_POTRF_W")) {
       c->potrf_groups.clear();
       std::string spec(e3);

@@ -11,8 +11,9 @@ import os
 import subprocess
 import sys
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
-d = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+n = int(args[0]) if len(args) > 0 else 16384
+d = int(args[1]) if len(args) > 1 else 10
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 passes = [["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS",
            "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_VALU"],
@@ -20,13 +21,15 @@ passes = [["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY"
            "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INST_LEVEL_VMEM", "SQ_INSTS_SALU", "GRBM_GUI_ACTIVE"],
           ["TA_TA_BUSY_sum", "TA_ADDR_STALLED_BY_TC_CYCLES_sum", "TCP_PENDING_STALL_CYCLES_sum",
            "TCP_TCC_READ_REQ_LATENCY_sum", "TCP_TCC_READ_REQ_sum", "TCP_TCC_WRITE_REQ_sum", "GRBM_GUI_ACTIVE"]]
+analyze_only = "--analyze" in sys.argv   # re-read gpurun_out/pmc_stall*/ without collecting
 launches = None
 for i, counters in enumerate(passes):
     odir = os.path.join(root, "gpurun_out", f"pmc_stall{i}")
     cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", *counters, "-d", odir, "-o", "run",
            "--output-format", "csv", "--", sys.executable, os.path.join(root, "tools", "prof_objective.py"),
            str(n), str(d), "1"]
-    subprocess.run(cmd, check=True, cwd=root, env=dict(os.environ, TMPDIR="/tmp"))
+    if not analyze_only:
+        subprocess.run(cmd, check=True, cwd=root, env=dict(os.environ, TMPDIR="/tmp"))
     rows = {}
     for f in glob.glob(os.path.join(odir, "**", "*counter_collection*.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
