@@ -189,6 +189,7 @@ struct gpe_ctx {
   // column-group widths of the fused Cholesky: {width, min remaining columns}, first
   // match wins, else 1 (GPEMU_POTRF_W="4:64,2:32" style)
   std::vector<std::pair<int, int>> potrf_groups = {{4, 80}, {2, 40}};
+  int chol_prio = 1;   // fused Cholesky (1), and the TRTRI levels (2), on the high-priority stream
   int potrf_first = 0;   // width of the first column group (0: as potrf_groups)
 
   // overlapped Cholesky tail (potrf_trtri_overlap): the width-1 tail steps on one half of
@@ -880,6 +881,16 @@ int potrf(gpe_ctx* c, Fact& F, bool with_aug = false) {
     // workgroup of the trailing-update launch kt and its panel follows in-launch
     HIPCHK(c, hipMemsetAsync(F.flags, 0, (size_t)NB * sizeof(int), c->stream));
     const std::vector<int>& fidx = (with_aug && pl.aug) ? pl.fused_aug : pl.fused;
+    if (c->chol_prio) {
+      // the whole sweep on the context's high-priority stream: with two tries in flight
+      // its chain workgroups are dispatched ahead of the other try's inverse tiles
+      HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+      HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+      for (int t = 0; t < NB; ++t) CHK(launch_gemm_range(c, pl.launches[fidx[t]], c->stream2));
+      HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+      return GPE_OK;
+    }
     for (int t = 0; t < NB; ++t) CHK(launch_gemm_range(c, pl.launches[fidx[t]]));
     return GPE_OK;
   }
@@ -955,6 +966,22 @@ int potrf_trtri_overlap(gpe_ctx* c, Fact& F) {
   const Plan& pl = F.plan;
   const int NB = F.NB, split = pl.split;
   HIPCHK(c, hipMemsetAsync(F.flags, 0, (size_t)NB * sizeof(int), c->stream));
+  if (c->tail_mode == 2 && c->chol_prio) {
+    // the sweep on the high-priority stream, the leading block's inverse on the context
+    // stream beside its second part: the chain's workgroups are dispatched first
+    HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+    for (int t = 0; t < split; ++t) CHK(launch_gemm_range(c, pl.launches[pl.fused[t]], c->stream2));
+    HIPCHK(c, hipEventRecord(c->ev_split, c->stream2));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_split, 0));
+    for (int li : pl.trtri_lead) CHK(launch_gemm_range(c, pl.launches[li]));
+    for (int t = split; t < NB; ++t) CHK(launch_gemm_range(c, pl.launches[pl.fused[t]], c->stream2));
+    HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    ev_rec(c, 2);
+    for (int li : pl.trtri_rest) CHK(launch_gemm_range(c, pl.launches[li]));
+    return GPE_OK;
+  }
   for (int t = 0; t < split; ++t) CHK(launch_gemm_range(c, pl.launches[pl.fused[t]]));
   HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
   if (c->tail_mode == 2) {   // plain second stream beside the rest of the sweep
@@ -987,6 +1014,14 @@ int lauum(gpe_ctx* c, Fact& F) {
 
 int trtri(gpe_ctx* c, Fact& F) {
   CHK(build_plan(c, F));
+  if (c->chol_prio >= 2) {   // the level launches on the high-priority stream too
+    HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+    for (int li : F.plan.trtri) CHK(launch_gemm_range(c, F.plan.launches[li], c->stream2));
+    HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    return GPE_OK;
+  }
   for (int li : F.plan.trtri) CHK(launch_gemm_range(c, F.plan.launches[li]));
   return GPE_OK;
 }
@@ -1282,6 +1317,7 @@ gpe_ctx* gpe_create(int32_t device) {
     const char* e2 = std::getenv("GPEMU_POTRF");
     c->potrf_lookahead = e2 && std::string(e2) == "lookahead";
     c->potrf_g2s = e2 && std::string(e2) == "g2s";
+    if (const char* ep = std::getenv("GPEMU_CHOL_PRIO")) c->chol_prio = std::max(0, std::min(2, std::atoi(ep)));
     if (const char* ef = std::getenv("GPEMU_POTRF_FIRST")) c->potrf_first = std::max(0, std::min(8, std::atoi(ef)));
     if (const char* e3 = std::getenv("GPEMU_POTRF_W")) {
       c->potrf_groups.clear();
