@@ -193,3 +193,56 @@ def test_kbuild_shuffle_reduction_variant(monkeypatch):
     assert abs(llh - ref) <= 1e-10 * abs(ref), (llh, ref)
     ok, err = _grad_ok(g, z[key + "_grad"])
     assert ok, err
+
+
+_SCHEDULES = [
+    {"GPEMU_CHOL_PRIO": "0"},
+    {"GPEMU_CHOL_PRIO": "2"},
+    {"GPEMU_POTRF": "g2s"},
+    {"GPEMU_POTRF_FIRST": "1"},
+    {"GPEMU_TAIL_OVERLAP": "1"},
+    {"GPEMU_TAIL_OVERLAP": "2", "GPEMU_TAIL_SPLIT": "48"},
+    {"GPEMU_TAIL_OVERLAP": "2", "GPEMU_TAIL_SPLIT": "48", "GPEMU_CHOL_PRIO": "0"},
+]
+
+
+@pytest.fixture(scope="module")
+def schedule_problem():
+    """n = 8448 (66 tile columns: groups of width 4, 2 and 1, and a tail long enough for
+    the overlapped schedules), d = 10, with the default schedule's results."""
+    X, f, H = orc.synthetic_problem(8448, 10, seed=12)
+    hp = np.concatenate([np.linspace(0.8, 1.6, 10), [3e-3, 0.9]])
+    c = native.Context(0)
+    try:
+        c.set_data(X, f, H)
+        v = c.objective(orc.GP4ML, orc.STD, hp, want_grad=False)[0]
+        llh, g, s2 = c.objective(orc.GP4ML, orc.STD, hp)
+    finally:
+        c.close()
+    ref = orc.objective_fast(X, f, H, hp, orc.GP4ML, orc.STD, True)   # the default, pinned
+    assert abs(llh - ref[0]) <= 1e-10 * abs(ref[0]) and abs(v - ref[0]) <= 1e-10 * abs(ref[0])
+    ok, err = _grad_ok(g, ref[1])
+    assert ok, err
+    return X, f, H, hp, v, llh, g, s2
+
+
+@pytest.mark.parametrize("env", _SCHEDULES, ids=lambda e: ",".join(f"{k[6:]}={v}" for k, v in e.items()))
+def test_schedule_switches_match_default(monkeypatch, schedule_problem, env):
+    """Every A/B schedule switch (the Cholesky's stream priority,
+    the two-stream group schedule, the first group's width, the overlapped tail on
+    CU-masked halves or a plain stream) computes the default schedule's value, gradient
+    and sigma^2: the same tiles in another order or on other streams."""
+    X, f, H, hp, v0, llh0, g0, s20 = schedule_problem
+    for k, val in env.items():
+        monkeypatch.setenv(k, val)
+    c = native.Context(0)
+    try:
+        c.set_data(X, f, H)
+        v = c.objective(orc.GP4ML, orc.STD, hp, want_grad=False)[0]
+        llh, g, s2 = c.objective(orc.GP4ML, orc.STD, hp)
+    finally:
+        c.close()
+    assert abs(v - v0) <= 1e-11 * abs(v0), (v, v0)
+    assert abs(llh - llh0) <= 1e-11 * abs(llh0), (llh, llh0)
+    assert abs(s2 - s20) <= 1e-11 * abs(s20)
+    assert np.max(np.abs(g - g0)) <= 1e-9 * (1.0 + np.max(np.abs(g0))), (g, g0)
