@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -66,6 +67,11 @@ struct Plan {
   std::vector<int> g2s_gs;                    // group starts, then NB
   std::vector<int> g2s_step, g2s_step_aug;    // per step: launch index
   std::vector<int> g2s_bulk, g2s_bulk_aug;    // per group: trailing-update launch, or -1
+  // group schedule (GPEMU_POTRF=group): ONE launch per column group of width >= 2 holding
+  // its whole chain (diagonal and panel tiles of every step, handed on by counters in
+  // F.flags) beside the previous group's trailing update; width-1 groups as fused.  Per
+  // step: the launch to issue, -1 for the later steps of a group
+  std::vector<int> grp, grp_aug;
   std::vector<Launch> launches;
   std::vector<GemmProb> probs;
   std::vector<unsigned> tiles;   // concatenated tile lists
@@ -183,6 +189,10 @@ struct gpe_ctx {
   // with the standalone diagonal kernel instead of the fused one
   bool potrf_lookahead = false;
   bool potrf_g2s = false;   // GPEMU_POTRF=g2s: the two-stream group schedule (potrf_g2s)
+  // GPEMU_POTRF=group: one launch per column group (Plan::grp); list positions of the
+  // chain steps (GPEMU_GROUP_P0, GPEMU_GROUP_STRIDE)
+  bool potrf_group = false;
+  int grp_p0 = 512, grp_stride = 512;
   std::vector<hipEvent_t> ev_gbulk, ev_gchain;
   bool skinny_valu = false;   // GPEMU_SKINNY=valu: the VALU skinny kernels (A/B)
   bool kpairs_shfl = false;   // GPEMU_KPAIRS=shuffle: the lane-shuffle d-reduction K-build (A/B)
@@ -412,6 +422,17 @@ std::vector<unsigned> order_tiles(const std::vector<GemmProb>& probs) {
     out.insert(out.begin() + 256, tail.front());
     tail.erase(tail.begin());
   }
+  // A/B (GPEMU_PANEL_POS = list position): the panel tiles' own pending update does not
+  // wait on the flag; dispatched early, it no longer runs in the launch's drain
+  static const int panel_pos = [] {
+    const char* e = std::getenv("GPEMU_PANEL_POS");
+    return e ? std::atoi(e) : -1;
+  }();
+  if (panel_pos >= 0) {
+    const size_t at = std::min(out.size(), (size_t)panel_pos);
+    out.insert(out.begin() + at, tail.begin(), tail.end());
+    return out;
+  }
   out.insert(out.end(), tail.begin(), tail.end());
   return out;
 }
@@ -443,6 +464,33 @@ void add_launch(Plan& pl, int kind, std::vector<GemmProb> probs, double flops) {
   pl.launches.push_back(L);
 }
 
+size_t tiles_total_hint(const std::vector<std::vector<unsigned>>& segs) {
+  size_t n = 0;
+  for (const auto& v : segs) n += v.size();
+  return n;
+}
+
+// a launch whose tile order is given (codes p << 24 | ti << 12 | tj, p into probs)
+void add_launch_list(Plan& pl, int kind, std::vector<GemmProb> probs, double flops, const std::vector<unsigned>& order) {
+  Launch L;
+  L.kind = kind;
+  L.first = (int)pl.probs.size();
+  L.count = (int)probs.size();
+  int t = 0;
+  for (auto& p : probs) {
+    p.tile_begin = t;
+    p.ntiles = prob_tiles(p);
+    t += p.ntiles;
+    L.cdef = L.cdef || gemm_cdef(p);
+    pl.probs.push_back(p);
+  }
+  L.tiles = (int)order.size();
+  L.flops = flops;
+  L.list = (long long)pl.tiles.size();
+  pl.tiles.insert(pl.tiles.end(), order.begin(), order.end());
+  pl.launches.push_back(L);
+}
+
 GemmProb mkprob(const double* A, long long lda, const double* B, long long ldb, double* C,
                 long long ldc, int mt, int nt, int K, int flags, double alpha, double beta) {
   GemmProb p;
@@ -452,6 +500,7 @@ GemmProb mkprob(const double* A, long long lda, const double* B, long long ldb, 
   p.alpha = alpha; p.beta = beta;
   p.tile_begin = 0; p.ntiles = 0;
   p.X = nullptr; p.ldx = 0; p.logdet = nullptr; p.diag_col0 = 0; p.flag = nullptr;
+  p.pre0 = p.pre1 = p.post = nullptr; p.pre0_n = p.pre1_n = 0;
   return p;
 }
 
@@ -585,6 +634,146 @@ int build_plan(gpe_ctx* c, Fact& F) {
       }
       fidx[t] = (int)pl.launches.size();
       add_launch(pl, 4, fp, fl);
+    }
+  }
+  // the group schedule: one launch per group of width >= 2.  Its tile list (= dispatch
+  // order): the first step's diagonal tile; the previous group's updates of the group's
+  // later columns (counted per column in cnt_col); the previous group's update of the
+  // columns after the group, in order_tiles' order; spliced into it, step h's chain tiles
+  // (its diagonal tile, then its panels, counted per step in cnt_pan) at list position
+  // grp_p0 + h grp_stride (step 0's first panel at 256: workgroup 0's CU partner).
+  // Step h >= 1 waits for step h-1's panels and its column's update, so every wait points
+  // to earlier tiles; one drain per group instead of one per step.
+  if (c->potrf_group && !c->potrf_lookahead) {
+    std::vector<int>& gidx = aug ? pl.grp_aug : pl.grp;
+    gidx.assign(NB, -1);
+    int* cnt_col = F.flags + NB;
+    int* cnt_pan = F.flags + 2 * NB;
+    for (int gi = 0; gi + 1 < (int)gs.size(); ++gi) {
+      const int gb = gs[gi], ge = gs[gi + 1], W1 = ge - gb;
+      if (W1 < 2) {
+        gidx[gb] = fidx[gb];
+        continue;
+      }
+      const int g0 = gi > 0 ? gs[gi - 1] : 0, Kb = (gb - g0) * TILE;
+      std::vector<GemmProb> fp;
+      double fl = 0.0;
+      auto codes = [&](int pi, std::vector<unsigned>& out) {
+        const GemmProb& q = fp[pi];
+        for (int ti = 0; ti < q.mt; ++ti)
+          for (int tj = 0; tj < q.nt && ((q.flags & G_CLOWER) == 0 || tj <= ti); ++tj)
+            out.push_back(((unsigned)pi << 24) | ((unsigned)ti << 12) | (unsigned)tj);
+      };
+      std::vector<unsigned> early, bulkc;
+      std::vector<std::vector<unsigned>> seg(W1);
+      std::vector<int> ncol(W1, 0), npan(W1, 0);
+      if (gi > 0)
+        for (int h = 1; h < W1; ++h) {   // column gb+h by the previous group
+          const size_t b0 = fp.size();
+          bulk(fp, fl, gb + h, gb + h + 1, g0, Kb);
+          for (size_t k = b0; k < fp.size(); ++k) {
+            fp[k].post = cnt_col + gb + h;
+            const size_t e0 = early.size();
+            codes((int)k, early);
+            ncol[h] += (int)(early.size() - e0);
+          }
+        }
+      for (int h = 0; h < W1; ++h) {
+        const int t = gb + h;
+        const int p0 = (h == 0) ? g0 : gb;
+        const int K = (t - p0) * TILE;
+        const double al = K ? -1.0 : 1.0;
+        const int m = NB - t - 1;
+        auto wire = [&](GemmProb& q) {
+          if (h == 0) return;
+          q.pre0 = cnt_pan + t - 1;
+          q.pre0_n = npan[h - 1];
+          if (gi > 0) {
+            q.pre1 = cnt_col + t;
+            q.pre1_n = ncol[h];
+          }
+        };
+        GemmProb d = diagprob(t, K ? tile(A, t, p0) : nullptr, K, al);
+        wire(d);
+        fp.push_back(d);
+        codes((int)fp.size() - 1, seg[h]);
+        fl += T * (T + 1.0) * K;
+        if (m >= 1) {
+          GemmProb q = panelprob(t, K ? tile(A, t + 1, p0) : nullptr, K ? tile(A, t, p0) : nullptr, K, al);
+          wire(q);
+          q.post = cnt_pan + t;
+          fp.push_back(q);
+          codes((int)fp.size() - 1, seg[h]);
+          npan[h] += m;
+          fl += 2.0 * m * T * T * K + (double)m * T * T * T;
+        }
+        if (aug) {
+          GemmProb pa = mkprob(K ? atile(p0) : nullptr, TILE, K ? tile(A, t, p0) : nullptr, ld, atile(t), TILE,
+                               1, 1, K, G_PANEL, al, 1.0);
+          pa.X = tile(B, t, t);
+          pa.ldx = ld;
+          pa.flag = F.flags + t;
+          pa.diag_col0 = -TILE;
+          wire(pa);
+          pa.post = cnt_pan + t;
+          fp.push_back(pa);
+          codes((int)fp.size() - 1, seg[h]);
+          npan[h] += 1;
+        }
+      }
+      if (gi > 0 && ge < NB) {   // the columns after the group by the previous group
+        const size_t b0 = fp.size();
+        bulk(fp, fl, ge, NB, g0, Kb);
+        std::vector<GemmProb> sub(fp.begin() + b0, fp.end());
+        for (unsigned code : order_tiles(sub)) bulkc.push_back(code + ((unsigned)b0 << 24));
+      }
+      // assemble: diag(gb), early, bulk; step 0's panels at grp_p0 (its first at 256),
+      // step h's chain at grp_p0 + h grp_stride
+      std::vector<unsigned> base;
+      base.push_back(seg[0][0]);
+      base.insert(base.end(), early.begin(), early.end());
+      base.insert(base.end(), bulkc.begin(), bulkc.end());
+      std::vector<unsigned> rest0(seg[0].begin() + 1, seg[0].end());
+      // step h's tiles go before base position min(|base|, p0 + h stride): the positions
+      // do not decrease with h, so the steps stay in order even where they clamp
+      std::vector<unsigned> order;
+      order.reserve(base.size() + tiles_total_hint(seg));
+      int h = 0;
+      for (size_t i = 0; i <= base.size(); ++i) {
+        while (h < W1 && std::min(base.size(), (size_t)c->grp_p0 + (size_t)h * c->grp_stride) == i) {
+          const std::vector<unsigned>& sg = h == 0 ? rest0 : seg[h];
+          order.insert(order.end(), sg.begin(), sg.end());
+          ++h;
+        }
+        if (i < base.size()) order.push_back(base[i]);
+      }
+      if (!rest0.empty() && order.size() > 257) {   // the first panel tile to slot 256
+        const auto it = std::find(order.begin(), order.end(), rest0.front());
+        const unsigned code = *it;
+        if (it - order.begin() > 256) {
+          order.erase(it);
+          order.insert(order.begin() + 256, code);
+        }
+      }
+      // every tile may wait only on tiles before it in the list (the dispatch order):
+      // then the earliest unfinished tile can always run.  Checked, not assumed.
+      {
+        std::map<const int*, size_t> last_post, diag_at;
+        for (size_t i = 0; i < order.size(); ++i) {
+          const GemmProb& q = fp[order[i] >> 24];
+          if (q.post) last_post[q.post] = i;
+          if (q.flags & G_DIAG) diag_at[q.flag] = i;
+        }
+        for (size_t i = 0; i < order.size(); ++i) {
+          const GemmProb& q = fp[order[i] >> 24];
+          const bool ok = (!q.pre0 || (last_post.count(q.pre0) && last_post[q.pre0] < i)) &&
+                          (!q.pre1 || (last_post.count(q.pre1) && last_post[q.pre1] < i)) &&
+                          (!(q.flags & G_PANEL) || (diag_at.count(q.flag) && diag_at[q.flag] < i));
+          if (!ok) return fail(c, GPE_ERR_HIP, "internal error: group schedule waits on a later tile");
+        }
+      }
+      gidx[gb] = (int)pl.launches.size();
+      add_launch_list(pl, 4, fp, fl, order);
     }
   }
   // the two-stream group schedule: the same chain tiles without the trailing-update
@@ -754,7 +943,7 @@ int ensure_fact(gpe_ctx* c, Fact& F, long long n_pad) {
     F.n_pad = n_pad;
     F.NB = (int)(n_pad / TILE);
     CHK(dalloc(c, &F.logdet, (size_t)F.NB));
-    CHK(dalloc(c, &F.flags, (size_t)F.NB));
+    CHK(dalloc(c, &F.flags, 3 * (size_t)F.NB));   // diagonal flags, then the group schedule's counters
     CHK(dalloc(c, &F.tflags, (size_t)F.NB));
     if (F.aug) CHK(dalloc(c, &F.Faug, (size_t)n_pad * TILE));
     F.plan = Plan();
@@ -845,7 +1034,7 @@ int potrf_g2s(gpe_ctx* c, Fact& F, bool with_aug) {
     }
   }
   hipStream_t mainst = c->stream, chain = c->stream2;
-  HIPCHK(c, hipMemsetAsync(F.flags, 0, (size_t)NB * sizeof(int), mainst));
+  HIPCHK(c, hipMemsetAsync(F.flags, 0, 3 * (size_t)NB * sizeof(int), mainst));
   HIPCHK(c, hipEventRecord(c->ev_fork, mainst));
   HIPCHK(c, hipStreamWaitEvent(chain, c->ev_fork, 0));
   int last_two = -1;   // the last group of width >= 2 so far
@@ -879,19 +1068,32 @@ int potrf(gpe_ctx* c, Fact& F, bool with_aug = false) {
   if (!c->potrf_lookahead) {
     // fused: one launch per step; the diagonal tile kt+1 is factored by the first
     // workgroup of the trailing-update launch kt and its panel follows in-launch
-    HIPCHK(c, hipMemsetAsync(F.flags, 0, (size_t)NB * sizeof(int), c->stream));
-    const std::vector<int>& fidx = (with_aug && pl.aug) ? pl.fused_aug : pl.fused;
+    HIPCHK(c, hipMemsetAsync(F.flags, 0, 3 * (size_t)NB * sizeof(int), c->stream));
+    const bool wa = with_aug && pl.aug;
+    const std::vector<int>& fidx = c->potrf_group ? (wa ? pl.grp_aug : pl.grp) : (wa ? pl.fused_aug : pl.fused);
     if (c->chol_prio) {
       // the whole sweep on the context's high-priority stream: with two tries in flight
       // its chain workgroups are dispatched ahead of the other try's inverse tiles
       HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
-      for (int t = 0; t < NB; ++t) CHK(launch_gemm_range(c, pl.launches[fidx[t]], c->stream2));
+      for (int t = 0; t < NB; ++t)
+        if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]], c->stream2));
       HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
       HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
       return GPE_OK;
     }
-    for (int t = 0; t < NB; ++t) CHK(launch_gemm_range(c, pl.launches[fidx[t]]));
+#ifdef GEMM_TTRACE
+    if (const char* es = std::getenv("GPEMU_DEBUG_STOP_STEP")) {
+      const int stop = std::atoi(es);
+      // back to back as in the sweep, every launch traced (the host resets the count)
+      for (int t = 0; t <= stop && t < NB; ++t)
+        if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]]));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      return fail(c, GPE_ERR_STATE, "debug stop after Cholesky launch " + std::to_string(stop));
+    }
+#endif
+    for (int t = 0; t < NB; ++t)
+      if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]]));
     return GPE_OK;
   }
   if ((int)c->ev_panel.size() < NB) {
@@ -965,7 +1167,7 @@ int potrf_trtri_overlap(gpe_ctx* c, Fact& F) {
   CHK(build_plan(c, F));
   const Plan& pl = F.plan;
   const int NB = F.NB, split = pl.split;
-  HIPCHK(c, hipMemsetAsync(F.flags, 0, (size_t)NB * sizeof(int), c->stream));
+  HIPCHK(c, hipMemsetAsync(F.flags, 0, 3 * (size_t)NB * sizeof(int), c->stream));
   if (c->tail_mode == 2 && c->chol_prio) {
     // the sweep on the high-priority stream, the leading block's inverse on the context
     // stream beside its second part: the chain's workgroups are dispatched first
@@ -1265,6 +1467,29 @@ int gpe_debug_trace(uint64_t* out, int32_t n) {
 }
 #endif
 
+#ifdef GEMM_TTRACE
+// dev build only: copy the per-tile timeline of the last k_gemm launch out (8 slots per
+// workgroup: start, C + first stage / panel's inverse seen, K loop done, end, HW_ID,
+// XCC_ID, kind, K); GPEMU_DEBUG_STOP_STEP=t ends the objective after Cholesky launch t
+int gpe_debug_ttrace(uint64_t* out, int32_t n) {
+  if (n > 8 * (int)GEMM_TTRACE_MAX) n = 8 * (int)GEMM_TTRACE_MAX;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gemm_ttrace), (size_t)n * 8) == hipSuccess ? 0 : -2;
+}
+// number of workgroups traced since the last reset; reset = 1 zeroes the count and trace
+int gpe_debug_ttrace_count(int32_t reset) {
+  unsigned n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(gemm_ttrace_n), sizeof(n)) != hipSuccess) return -2;
+  if (reset) {
+    const unsigned z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(gemm_ttrace_n), &z, sizeof(z)) != hipSuccess) return -2;
+    void* tt = nullptr;
+    if (hipGetSymbolAddress(&tt, HIP_SYMBOL(gemm_ttrace)) != hipSuccess ||
+        hipMemset(tt, 0, sizeof(unsigned long long) * 8 * GEMM_TTRACE_MAX) != hipSuccess) return -2;
+  }
+  return (int)n;
+}
+#endif
+
 int gpe_abi_version(void) { return GPE_ABI_VERSION; }
 
 #ifndef GPE_SOURCE_HASH
@@ -1317,6 +1542,9 @@ gpe_ctx* gpe_create(int32_t device) {
     const char* e2 = std::getenv("GPEMU_POTRF");
     c->potrf_lookahead = e2 && std::string(e2) == "lookahead";
     c->potrf_g2s = e2 && std::string(e2) == "g2s";
+    c->potrf_group = e2 && std::string(e2) == "group";
+    if (const char* eg = std::getenv("GPEMU_GROUP_P0")) c->grp_p0 = std::max(1, std::atoi(eg));
+    if (const char* eg = std::getenv("GPEMU_GROUP_STRIDE")) c->grp_stride = std::max(0, std::atoi(eg));
     if (const char* ep = std::getenv("GPEMU_CHOL_PRIO")) c->chol_prio = std::max(0, std::min(2, std::atoi(ep)));
     if (const char* ef = std::getenv("GPEMU_POTRF_FIRST")) c->potrf_first = std::max(0, std::min(8, std::atoi(ef)));
     if (const char* e3 = std::getenv("GPEMU_POTRF_W")) {

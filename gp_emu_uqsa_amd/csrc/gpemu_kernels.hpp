@@ -656,14 +656,27 @@ struct GemmProb {
   double* logdet;
   int diag_col0;
   int* flag;          // G_DIAG releases, G_PANEL waits
+  // counted hand-offs inside one launch (the group schedule of the fused Cholesky):
+  // before reading anything the tile waits until *pre0 >= pre0_n and *pre1 >= pre1_n;
+  // when its results are stored it adds 1 to *post.  Every awaited tile sits earlier in
+  // the launch's tile list (dispatch order), so the earliest unfinished tile can always run.
+  int* pre0;
+  int* pre1;
+  int* post;
+  int pre0_n, pre1_n;
 };
 
 // dev-tool per-tile timeline (-DGEMM_TTRACE build only, tools/hip/tile_probe.hip): per
 // workgroup, [0] start, [1] C and first stage landed, [2] K loop done, [3] stores done,
 // [4] hardware id, [5] XCC id
+// Entries are numbered in start order across launches (gemm_ttrace_n, reset by the host),
+// so a whole sweep of launches fits: up to GEMM_TTRACE_MAX workgroups.
 #ifdef GEMM_TTRACE
-__device__ unsigned long long gemm_ttrace[8 * 65536];
-#define TTRACE(slot) do { if (threadIdx.x == 0 && blockIdx.x < 65536) gemm_ttrace[blockIdx.x * 8 + (slot)] = wall_clock64(); } while (0)
+constexpr unsigned GEMM_TTRACE_MAX = 262144;
+__device__ unsigned long long gemm_ttrace[8 * GEMM_TTRACE_MAX];
+__device__ unsigned gemm_ttrace_n;
+__shared__ unsigned gemm_tslot;
+#define TTRACE(slot) do { if (threadIdx.x == 0 && gemm_tslot < GEMM_TTRACE_MAX) gemm_ttrace[gemm_tslot * 8 + (slot)] = wall_clock64(); } while (0)
 #else
 #define TTRACE(slot) do {} while (0)
 #endif
@@ -1151,6 +1164,31 @@ __device__ __forceinline__ int gemm_wait_flag(const int* flag) {
 
 constexpr int GEMM_WAIT_TIMEOUT = 0x7fffffff;   // info value after a flag wait timed out
 
+// bounded wait (one lane) until *cnt >= n: 1 reached, 2 the launch aborted meanwhile,
+// 0 after ~seconds (never expected: reported as an error)
+__device__ __forceinline__ int gemm_wait_count(const int* cnt, int n, const int* abort_flag) {
+  int st = 0;
+  for (long it = 0; it < (1l << 22); ++it) {
+    if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= n) { st = 1; break; }
+    if (abort_flag && __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { st = 2; break; }
+    __builtin_amdgcn_s_sleep(8);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return st;
+}
+
+// every wave's stores of this tile done, then one lane releases them and counts the tile
+__device__ __forceinline__ void gemm_post_count(int* cnt) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // dev-tool timeline of the fused Cholesky (-DGEMM_TRACE build only): per column
 // step t, slots [t*8 + 0..3] = diagonal workgroup start / update done / factor
 // done / flag published, [t*8 + 4..7] = first panel workgroup start / update done /
@@ -1211,13 +1249,37 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
   if (P.flags & G_KEND_TI) kend = min(kend, (ti + 1) * TILE);
 
   const int tid = threadIdx.x;
+  if constexpr (FUSED) {
+    if (P.pre0 || P.pre1) {   // the group schedule's in-launch hand-offs (see GemmProb)
+      int* ready = reinterpret_cast<int*>(lds + G_LDS_LAUNCH_DOUBLES - 2);
+      if (tid == 0) {
+        int st = 1;
+        if (P.pre0) st = gemm_wait_count(P.pre0, P.pre0_n, abort_flag);
+        if (st == 1 && P.pre1) st = gemm_wait_count(P.pre1, P.pre1_n, abort_flag);
+        *ready = st;
+      }
+      __syncthreads();
+      const int st = *ready;
+      __syncthreads();
+      if (st != 1) {
+        if (st == 0 && tid == 0 && abort_flag) atomicCAS(abort_flag, 0, GEMM_WAIT_TIMEOUT);
+        return;
+      }
+    }
+  }
   const int lane = tid & 63, wave = FUSED ? (tid >> 6) : gemm_wave();   // as gemm_kloop's SW
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  TTRACE(0);
 #ifdef GEMM_TTRACE
-  if (threadIdx.x == 0 && blockIdx.x < 65536) {
-    gemm_ttrace[blockIdx.x * 8 + 4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-    gemm_ttrace[blockIdx.x * 8 + 5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+  if (tid == 0) gemm_tslot = atomicAdd(&gemm_ttrace_n, 1u);
+  __syncthreads();
+  TTRACE(0);
+  if (threadIdx.x == 0 && gemm_tslot < GEMM_TTRACE_MAX) {
+    const unsigned e = gemm_tslot * 8;
+    gemm_ttrace[e + 4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    gemm_ttrace[e + 5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    // [6] kind (0 plain tile, 1 diagonal, 2 panel) + 4 x blockIdx, [7] K of its own product
+    gemm_ttrace[e + 6] = ((P.flags & G_DIAG) ? 1 : ((P.flags & G_PANEL) ? 2 : 0)) + 4ull * blockIdx.x;
+    gemm_ttrace[e + 7] = (unsigned long long)(kend - kbeg);
   }
 #endif
   if (P.flags & G_DIAG) GTRACE(P, 0);
@@ -1305,6 +1367,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
         if (tid == 0) gemm_publish_flag(P.flag, bad ? 2 : 1);
       }
       GTRACE(P, 3);
+      TTRACE(3);
       return;
     }
     if (P.flags & G_PANEL) {
@@ -1323,6 +1386,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
         if (st == 0 && tid == 0 && abort_flag) atomicCAS(abort_flag, 0, GEMM_WAIT_TIMEOUT);
         return;
       }
+      TTRACE(1);   // (panel tiles: [1] = the diagonal inverse seen)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1330,10 +1394,19 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
       gemm_kloop<false, false, true, false, false>(Cb, P.X, P.ldc, P.ldx, 0, TILE / GK, lds, acc);
       gemm_store<false>(Cb, P.ldc, 1.0, acc);
       if (ti == 0) GTRACE(P, 7);
+      if (P.post) gemm_post_count(P.post);
+#ifdef GEMM_TTRACE
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      TTRACE(3);
+#endif
       return;
     }
   }
   gemm_store<!FUSED>(Cb, P.ldc, P.alpha, acc);
+  if constexpr (FUSED) {
+    if (P.post) gemm_post_count(P.post);
+  }
 #ifdef GEMM_TTRACE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();

@@ -199,6 +199,10 @@ _SCHEDULES = [
     {"GPEMU_CHOL_PRIO": "0"},
     {"GPEMU_CHOL_PRIO": "2"},
     {"GPEMU_POTRF": "g2s"},
+    {"GPEMU_POTRF": "group"},
+    {"GPEMU_POTRF": "group", "GPEMU_GROUP_STRIDE": "0", "GPEMU_GROUP_P0": "1"},
+    {"GPEMU_POTRF": "group", "GPEMU_GROUP_STRIDE": "5000"},
+    {"GPEMU_POTRF": "group", "GPEMU_POTRF_W": "8:40,3:20", "GPEMU_GROUP_STRIDE": "900"},
     {"GPEMU_POTRF_FIRST": "1"},
     {"GPEMU_TAIL_OVERLAP": "1"},
     {"GPEMU_TAIL_OVERLAP": "2", "GPEMU_TAIL_SPLIT": "48"},

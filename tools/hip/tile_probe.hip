@@ -57,13 +57,17 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   float ms = 0.f;
   for (int rep = 0; rep < 4; ++rep) {   // warm clocks; the last launch is the one traced
+    if (rep == 3) {   // entries are numbered in start order from the reset count
+      const unsigned z = 0;
+      CK(hipMemcpyToSymbol(HIP_SYMBOL(gemm_ttrace_n), &z, sizeof(z)));
+    }
     CK(hipEventRecord(e0));
     hipLaunchKernelGGL(kern, dim3(tiles), dim3(256), lds, 0, dp, 1, (const unsigned*)nullptr, (int*)nullptr);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(&ms, e0, e1));
   }
-  std::vector<unsigned long long> t((size_t)8 * 65536);
+  std::vector<unsigned long long> t((size_t)8 * GEMM_TTRACE_MAX);
   CK(hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(gemm_ttrace), t.size() * 8));
   unsigned long long t0 = ~0ull, t3 = 0;
   double d01 = 0, d12 = 0, d23 = 0;

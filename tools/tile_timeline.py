@@ -1,0 +1,90 @@
+"""Per-tile timeline of the fused Cholesky sweep (dev tool; the -DGEMM_TTRACE build):
+  bash tools/tile_timeline.sh      (builds gp_emu_uqsa_amd/libgpemu_ttrace.so here)
+  GPEMU_LIB=gp_emu_uqsa_amd/libgpemu_ttrace.so GPEMU_CHOL_PRIO=0 python tools/tile_timeline.py [stop]
+The objective stops after Cholesky launch `stop` (GPEMU_DEBUG_STOP_STEP, default the last);
+every workgroup of the sweep is traced in start order (start / end on the 100 MHz wall
+clock, kind, K).  Per phase: the 512 workgroup slots' occupancy, the launches' spans and
+the gaps between them, the drains (time a launch spends below 90% occupancy at its end)
+and the tile durations.  -> gpurun_out/tile_timeline.json"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from gp_emu_uqsa_amd import native, synthetic  # noqa: E402
+
+n = 16384
+NB = n // 128
+stop = int(sys.argv[1]) if len(sys.argv) > 1 else NB - 1
+tag = sys.argv[2] if len(sys.argv) > 2 else ""
+ctx = native.Context(0)
+X, f, H = synthetic.problem(n, 10, seed=0)
+ctx.set_data(X, f, H)
+hp = np.concatenate([np.ones(10), [1e-3, 1.0]])
+ctx.objective(0, 0, hp)
+ctx.objective(0, 0, hp)
+lib = native.load_library()
+lib.gpe_debug_ttrace.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+lib.gpe_debug_ttrace_count.argtypes = [ctypes.c_int32]
+assert lib.gpe_debug_ttrace_count(1) >= 0
+os.environ["GPEMU_DEBUG_STOP_STEP"] = str(stop)
+try:
+    ctx.objective(0, 0, hp)
+except Exception:   # the debug stop
+    pass
+os.environ.pop("GPEMU_DEBUG_STOP_STEP", None)
+cnt = lib.gpe_debug_ttrace_count(0)
+assert 0 < cnt <= 262144, cnt
+buf = np.zeros(8 * cnt, dtype=np.uint64)
+assert lib.gpe_debug_ttrace(buf.ctypes.data, buf.size) == 0
+w = buf.reshape(cnt, 8)
+np.save(os.path.join(ROOT, "gpurun_out", f"tile_timeline{tag}.npy"), w)   # raw, for offline analysis
+t0 = w[:, 0].min()
+st = (w[:, 0] - t0) / 100.0
+en = (w[:, 3].astype(np.float64) - t0) / 100.0
+kind = (w[:, 6] & 3).astype(int)
+bidx = (w[:, 6] >> 2).astype(int)
+order = np.argsort(st, kind="stable")
+# launch boundaries: each launch's workgroup 0 is its diagonal tile
+starts0 = np.sort(st[(bidx == 0) & (kind == 1)])
+# (one launch per step, or per column group under GPEMU_POTRF=group)
+launch = np.searchsorted(starts0, st, side="right") - 1
+span_end = np.array([en[launch == L].max() for L in range(stop + 1)])
+span_beg = np.array([st[launch == L].min() for L in range(stop + 1)])
+total = span_end[-1]
+# occupancy sampled every 0.5 us over the sweep
+grid = np.arange(0.0, total, 0.5)
+act = np.zeros_like(grid)
+ev = np.concatenate([np.stack([st, np.ones_like(st)], 1), np.stack([en, -np.ones_like(en)], 1)])
+ev = ev[np.argsort(ev[:, 0], kind="stable")]
+cum = np.cumsum(ev[:, 1])
+idx = np.searchsorted(ev[:, 0], grid, side="right") - 1
+act = np.where(idx >= 0, cum[np.maximum(idx, 0)], 0)
+out = {"stop": stop, "tiles": int(cnt), "sweep_ms": float(total / 1e3), "phases": {}}
+for lo, hi, name in ((0, 48, "steps 0-47"), (48, 88, "steps 48-87"), (88, NB, "steps 88-127")):
+    hi = min(hi, stop + 1)
+    if lo >= hi:
+        continue
+    a, b = span_beg[lo], span_end[hi - 1]
+    m = (grid >= a) & (grid < b)
+    spans = span_end[lo:hi] - span_beg[lo:hi]
+    gaps = span_beg[lo + 1:hi] - span_end[lo:hi - 1] if hi - lo > 1 else np.array([0.0])
+    drains = []
+    for L in range(lo, hi):
+        mm = (grid >= span_beg[L]) & (grid < span_end[L])
+        full = np.nonzero(act[mm] >= 0.9 * 512)[0]
+        drains.append((span_end[L] - grid[mm][full[-1]]) if len(full) else span_end[L] - span_beg[L])
+    ph = {"ms": float((b - a) / 1e3), "occupancy": float(act[m].mean() / 512),
+          "span_mean_us": float(spans.mean()), "gap_mean_us": float(gaps.mean()), "drain_mean_us": float(np.mean(drains))}
+    for k, kn in ((0, "bulk"), (1, "diag"), (2, "panel")):
+        sel = (kind == k) & (launch >= lo) & (launch < hi)
+        if sel.any():
+            ph[kn + "_us"] = float(np.mean(en[sel] - st[sel]))
+            ph[kn + "_slot_ms"] = float(np.sum(en[sel] - st[sel]) / 1e3)
+    out["phases"][name] = ph
+print(json.dumps(out, indent=1))
+json.dump(out, open(os.path.join(ROOT, "gpurun_out", f"tile_timeline{tag}.json"), "w"), indent=1)
