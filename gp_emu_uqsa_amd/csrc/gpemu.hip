@@ -191,8 +191,8 @@ struct gpe_ctx {
   bool potrf_g2s = false;   // GPEMU_POTRF=g2s: the two-stream group schedule (potrf_g2s)
   // GPEMU_POTRF=group: one launch per column group (Plan::grp); list positions of the
   // chain steps (GPEMU_GROUP_P0, GPEMU_GROUP_STRIDE)
-  bool potrf_group = false;
-  int grp_p0 = 512, grp_stride = 512;
+  bool potrf_group = true;
+  int grp_p0 = 512, grp_stride = 896;
   std::vector<hipEvent_t> ev_gbulk, ev_gchain;
   bool skinny_valu = false;   // GPEMU_SKINNY=valu: the VALU skinny kernels (A/B)
   bool kpairs_shfl = false;   // GPEMU_KPAIRS=shuffle: the lane-shuffle d-reduction K-build (A/B)
@@ -734,26 +734,38 @@ int build_plan(gpe_ctx* c, Fact& F) {
       base.insert(base.end(), early.begin(), early.end());
       base.insert(base.end(), bulkc.begin(), bulkc.end());
       std::vector<unsigned> rest0(seg[0].begin() + 1, seg[0].end());
-      // step h's tiles go before base position min(|base|, p0 + h stride): the positions
-      // do not decrease with h, so the steps stay in order even where they clamp
+      // step h's tiles go before base position min(|base|, p0 + h stride), for h >= 1 not
+      // before the column updates they wait on: the positions do not decrease with h, so
+      // the steps stay in order even where they clamp
       std::vector<unsigned> order;
       order.reserve(base.size() + tiles_total_hint(seg));
+      auto pos = [&](int h) {
+        size_t at = (size_t)c->grp_p0 + (size_t)h * c->grp_stride;
+        if (h >= 1) at = std::max(at, 1 + early.size());
+        return std::min(base.size(), at);
+      };
       int h = 0;
       for (size_t i = 0; i <= base.size(); ++i) {
-        while (h < W1 && std::min(base.size(), (size_t)c->grp_p0 + (size_t)h * c->grp_stride) == i) {
+        while (h < W1 && pos(h) == i) {
           const std::vector<unsigned>& sg = h == 0 ? rest0 : seg[h];
           order.insert(order.end(), sg.begin(), sg.end());
           ++h;
         }
         if (i < base.size()) order.push_back(base[i]);
       }
+      // The first 512 workgroups of a launch on an idle GPU fill two slots per CU in
+      // order, workgroup 256 + k beside workgroup k (tools/hip/placement_probe.hip): step
+      // 0's first panel tile goes to 256, beside the diagonal tile 0, so the factorisation
+      // has its CU's SIMDs to itself.  (Pinning the later steps' diagonal tiles the same
+      // way, to slots 1 .. W-1, measured no faster: DESIGN.md section 10.)
+      auto move_to = [&](unsigned code, size_t at) {
+        const auto it = std::find(order.begin(), order.end(), code);
+        order.erase(it);
+        order.insert(order.begin() + std::min(at, order.size()), code);
+      };
       if (!rest0.empty() && order.size() > 257) {   // the first panel tile to slot 256
         const auto it = std::find(order.begin(), order.end(), rest0.front());
-        const unsigned code = *it;
-        if (it - order.begin() > 256) {
-          order.erase(it);
-          order.insert(order.begin() + 256, code);
-        }
+        if (it - order.begin() > 256) move_to(rest0.front(), 256);
       }
       // every tile may wait only on tiles before it in the list (the dispatch order):
       // then the earliest unfinished tile can always run.  Checked, not assumed.
@@ -1542,7 +1554,7 @@ gpe_ctx* gpe_create(int32_t device) {
     const char* e2 = std::getenv("GPEMU_POTRF");
     c->potrf_lookahead = e2 && std::string(e2) == "lookahead";
     c->potrf_g2s = e2 && std::string(e2) == "g2s";
-    c->potrf_group = e2 && std::string(e2) == "group";
+    if (e2) c->potrf_group = std::string(e2) == "group";   // GPEMU_POTRF=fused: one launch per step
     if (const char* eg = std::getenv("GPEMU_GROUP_P0")) c->grp_p0 = std::max(1, std::atoi(eg));
     if (const char* eg = std::getenv("GPEMU_GROUP_STRIDE")) c->grp_stride = std::max(0, std::atoi(eg));
     if (const char* ep = std::getenv("GPEMU_CHOL_PRIO")) c->chol_prio = std::max(0, std::min(2, std::atoi(ep)));

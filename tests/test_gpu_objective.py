@@ -199,10 +199,11 @@ _SCHEDULES = [
     {"GPEMU_CHOL_PRIO": "0"},
     {"GPEMU_CHOL_PRIO": "2"},
     {"GPEMU_POTRF": "g2s"},
-    {"GPEMU_POTRF": "group"},
-    {"GPEMU_POTRF": "group", "GPEMU_GROUP_STRIDE": "0", "GPEMU_GROUP_P0": "1"},
-    {"GPEMU_POTRF": "group", "GPEMU_GROUP_STRIDE": "5000"},
-    {"GPEMU_POTRF": "group", "GPEMU_POTRF_W": "8:40,3:20", "GPEMU_GROUP_STRIDE": "900"},
+    {"GPEMU_POTRF": "fused"},
+    {"GPEMU_POTRF": "fused", "GPEMU_POTRF_FIRST": "1"},
+    {"GPEMU_GROUP_STRIDE": "0", "GPEMU_GROUP_P0": "1"},
+    {"GPEMU_GROUP_STRIDE": "5000"},
+    {"GPEMU_POTRF_W": "8:40,3:20", "GPEMU_GROUP_STRIDE": "300"},
     {"GPEMU_POTRF_FIRST": "1"},
     {"GPEMU_TAIL_OVERLAP": "1"},
     {"GPEMU_TAIL_OVERLAP": "2", "GPEMU_TAIL_SPLIT": "48"},
@@ -233,9 +234,10 @@ def schedule_problem():
 @pytest.mark.parametrize("env", _SCHEDULES, ids=lambda e: ",".join(f"{k[6:]}={v}" for k, v in e.items()))
 def test_schedule_switches_match_default(monkeypatch, schedule_problem, env):
     """Every A/B schedule switch (the Cholesky's stream priority,
-    the two-stream group schedule, the first group's width, the overlapped tail on
-    CU-masked halves or a plain stream) computes the default schedule's value, gradient
-    and sigma^2: the same tiles in another order or on other streams."""
+    one launch per step instead of per column group, the group launch's chain positions
+    and widths, the two-stream group schedule, the first group's width, the overlapped
+    tail on CU-masked halves or a plain stream) computes the default schedule's value,
+    gradient and sigma^2: the same tiles in another order, launch or stream."""
     X, f, H, hp, v0, llh0, g0, s20 = schedule_problem
     for k, val in env.items():
         monkeypatch.setenv(k, val)

@@ -48,43 +48,41 @@ st = (w[:, 0] - t0) / 100.0
 en = (w[:, 3].astype(np.float64) - t0) / 100.0
 kind = (w[:, 6] & 3).astype(int)
 bidx = (w[:, 6] >> 2).astype(int)
-order = np.argsort(st, kind="stable")
-# launch boundaries: each launch's workgroup 0 is its diagonal tile
-starts0 = np.sort(st[(bidx == 0) & (kind == 1)])
-# (one launch per step, or per column group under GPEMU_POTRF=group)
+# launches: each starts with its workgroup 0, a diagonal tile (10 us of slack for the
+# dispatch skew between XCDs); steps: the diagonal tiles in start order
+starts0 = np.sort(st[(bidx == 0) & (kind == 1)]) - 10.0
 launch = np.searchsorted(starts0, st, side="right") - 1
-span_end = np.array([en[launch == L].max() for L in range(stop + 1)])
-span_beg = np.array([st[launch == L].min() for L in range(stop + 1)])
-total = span_end[-1]
-# occupancy sampled every 0.5 us over the sweep
+NL = len(starts0)
+beg = np.array([st[launch == L].min() for L in range(NL)])
+end = np.array([np.nanmax(en[launch == L]) for L in range(NL)])
+dstart = np.sort(st[kind == 1])
+total = float(np.nanmax(end))
 grid = np.arange(0.0, total, 0.5)
-act = np.zeros_like(grid)
-ev = np.concatenate([np.stack([st, np.ones_like(st)], 1), np.stack([en, -np.ones_like(en)], 1)])
+ok = np.isfinite(en)
+ev = np.concatenate([np.stack([st[ok], np.ones(ok.sum())], 1), np.stack([en[ok], -np.ones(ok.sum())], 1)])
 ev = ev[np.argsort(ev[:, 0], kind="stable")]
 cum = np.cumsum(ev[:, 1])
 idx = np.searchsorted(ev[:, 0], grid, side="right") - 1
 act = np.where(idx >= 0, cum[np.maximum(idx, 0)], 0)
-out = {"stop": stop, "tiles": int(cnt), "sweep_ms": float(total / 1e3), "phases": {}}
-for lo, hi, name in ((0, 48, "steps 0-47"), (48, 88, "steps 48-87"), (88, NB, "steps 88-127")):
-    hi = min(hi, stop + 1)
-    if lo >= hi:
-        continue
-    a, b = span_beg[lo], span_end[hi - 1]
+drain = np.zeros(NL)
+for L in range(NL):
+    mm = (grid >= beg[L]) & (grid < end[L])
+    full = np.nonzero(act[mm] >= 0.9 * 512)[0]
+    drain[L] = (end[L] - grid[mm][full[-1]]) if len(full) else end[L] - beg[L]
+out = {"stop": stop, "tiles": int(cnt), "launches": int(NL), "sweep_ms": total / 1e3,
+       "occupancy": float(act.mean() / 512), "phases": {}}
+bounds = [0.0] + [float(dstart[k]) for k in (48, 88) if k < len(dstart)] + [total]
+names = ["steps 0-47", "steps 48-87", "steps 88-127"]
+for i in range(len(bounds) - 1):
+    a, b = bounds[i], bounds[i + 1]
     m = (grid >= a) & (grid < b)
-    spans = span_end[lo:hi] - span_beg[lo:hi]
-    gaps = span_beg[lo + 1:hi] - span_end[lo:hi - 1] if hi - lo > 1 else np.array([0.0])
-    drains = []
-    for L in range(lo, hi):
-        mm = (grid >= span_beg[L]) & (grid < span_end[L])
-        full = np.nonzero(act[mm] >= 0.9 * 512)[0]
-        drains.append((span_end[L] - grid[mm][full[-1]]) if len(full) else span_end[L] - span_beg[L])
-    ph = {"ms": float((b - a) / 1e3), "occupancy": float(act[m].mean() / 512),
-          "span_mean_us": float(spans.mean()), "gap_mean_us": float(gaps.mean()), "drain_mean_us": float(np.mean(drains))}
+    Ls = [L for L in range(NL) if a <= beg[L] < b]
+    ph = {"ms": (b - a) / 1e3, "occupancy": float(act[m].mean() / 512), "launches": len(Ls),
+          "drain_ms": float(drain[Ls].sum() / 1e3) if Ls else 0.0}
     for k, kn in ((0, "bulk"), (1, "diag"), (2, "panel")):
-        sel = (kind == k) & (launch >= lo) & (launch < hi)
+        sel = (kind == k) & (st >= a) & (st < b) & ok
         if sel.any():
             ph[kn + "_us"] = float(np.mean(en[sel] - st[sel]))
-            ph[kn + "_slot_ms"] = float(np.sum(en[sel] - st[sel]) / 1e3)
-    out["phases"][name] = ph
+    out["phases"][names[i]] = ph
 print(json.dumps(out, indent=1))
 json.dump(out, open(os.path.join(ROOT, "gpurun_out", f"tile_timeline{tag}.json"), "w"), indent=1)
