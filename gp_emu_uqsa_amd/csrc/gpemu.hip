@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
 #include <cmath>
 #include <cstdio>
@@ -191,7 +192,12 @@ struct gpe_ctx {
   bool potrf_g2s = false;   // GPEMU_POTRF=g2s: the two-stream group schedule (potrf_g2s)
   // GPEMU_POTRF=group: one launch per column group (Plan::grp); list positions of the
   // chain steps (GPEMU_GROUP_P0, GPEMU_GROUP_STRIDE)
-  bool potrf_group = true;
+  bool potrf_group = true;    // the group launches are built (Plan::grp)
+  // 0 auto: group launches while this is the only objective evaluation in flight on the
+  // device, one launch per step when others run beside it (their tiles fill the per-step
+  // drains, and the group launches' waiting chain tiles would hold slots they could use);
+  // 1 always group (GPEMU_POTRF=group), 2 always per step (GPEMU_POTRF=fused)
+  int potrf_mode = 0;
   int grp_p0 = 512, grp_stride = 896;
   std::vector<hipEvent_t> ev_gbulk, ev_gchain;
   bool skinny_valu = false;   // GPEMU_SKINNY=valu: the VALU skinny kernels (A/B)
@@ -490,6 +496,15 @@ void add_launch_list(Plan& pl, int kind, std::vector<GemmProb> probs, double flo
   pl.tiles.insert(pl.tiles.end(), order.begin(), order.end());
   pl.launches.push_back(L);
 }
+
+// objective evaluations in flight per device (gpe_objective), for the auto Cholesky schedule
+std::atomic<int> g_inflight[64];
+
+struct InflightGuard {
+  int dev;
+  explicit InflightGuard(int d) : dev(d & 63) { g_inflight[dev].fetch_add(1); }
+  ~InflightGuard() { g_inflight[dev].fetch_sub(1); }
+};
 
 GemmProb mkprob(const double* A, long long lda, const double* B, long long ldb, double* C,
                 long long ldc, int mt, int nt, int K, int flags, double alpha, double beta) {
@@ -1082,7 +1097,9 @@ int potrf(gpe_ctx* c, Fact& F, bool with_aug = false) {
     // workgroup of the trailing-update launch kt and its panel follows in-launch
     HIPCHK(c, hipMemsetAsync(F.flags, 0, 3 * (size_t)NB * sizeof(int), c->stream));
     const bool wa = with_aug && pl.aug;
-    const std::vector<int>& fidx = c->potrf_group ? (wa ? pl.grp_aug : pl.grp) : (wa ? pl.fused_aug : pl.fused);
+    const bool grp = c->potrf_group &&
+                     (c->potrf_mode == 1 || (c->potrf_mode == 0 && g_inflight[c->device & 63].load() <= 1));
+    const std::vector<int>& fidx = grp ? (wa ? pl.grp_aug : pl.grp) : (wa ? pl.fused_aug : pl.fused);
     if (c->chol_prio) {
       // the whole sweep on the context's high-priority stream: with two tries in flight
       // its chain workgroups are dispatched ahead of the other try's inverse tiles
@@ -1554,7 +1571,11 @@ gpe_ctx* gpe_create(int32_t device) {
     const char* e2 = std::getenv("GPEMU_POTRF");
     c->potrf_lookahead = e2 && std::string(e2) == "lookahead";
     c->potrf_g2s = e2 && std::string(e2) == "g2s";
-    if (e2) c->potrf_group = std::string(e2) == "group";   // GPEMU_POTRF=fused: one launch per step
+    if (e2) {
+      const std::string m(e2);
+      c->potrf_group = m == "group" || m == "auto";
+      c->potrf_mode = m == "group" ? 1 : (m == "auto" ? 0 : 2);
+    }
     if (const char* eg = std::getenv("GPEMU_GROUP_P0")) c->grp_p0 = std::max(1, std::atoi(eg));
     if (const char* eg = std::getenv("GPEMU_GROUP_STRIDE")) c->grp_stride = std::max(0, std::atoi(eg));
     if (const char* ep = std::getenv("GPEMU_CHOL_PRIO")) c->chol_prio = std::max(0, std::min(2, std::atoi(ep)));
@@ -1738,6 +1759,7 @@ int gpe_gemm_stats(gpe_ctx* c, double* ms_out, double* launches_out, double* flo
 int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp, int32_t n_hp,
                   double nu_fixed, int32_t want_grad, double* llh_out, double* grad_out,
                   double* sigma2_out) {
+  const InflightGuard inflight(c->device);
   CHK(check_ready(c));
   if (!hp || !llh_out) return fail(c, GPE_ERR_ARG, "null output");
   if (variant != GPE_GP4ML && variant != GPE_MUCM) return fail(c, GPE_ERR_ARG, "bad variant");

@@ -200,6 +200,7 @@ _SCHEDULES = [
     {"GPEMU_CHOL_PRIO": "2"},
     {"GPEMU_POTRF": "g2s"},
     {"GPEMU_POTRF": "fused"},
+    {"GPEMU_POTRF": "group"},
     {"GPEMU_POTRF": "fused", "GPEMU_POTRF_FIRST": "1"},
     {"GPEMU_GROUP_STRIDE": "0", "GPEMU_GROUP_P0": "1"},
     {"GPEMU_GROUP_STRIDE": "5000"},

@@ -19,7 +19,7 @@ from gp_emu_uqsa_amd import native, synthetic  # noqa: E402
 
 n = 16384
 NB = n // 128
-stop = int(sys.argv[1]) if len(sys.argv) > 1 else NB - 1
+stop = int(sys.argv[1]) if len(sys.argv) > 1 else NB - 1   # < 0: the whole evaluation
 tag = sys.argv[2] if len(sys.argv) > 2 else ""
 ctx = native.Context(0)
 X, f, H = synthetic.problem(n, 10, seed=0)
@@ -31,12 +31,15 @@ lib = native.load_library()
 lib.gpe_debug_ttrace.argtypes = [ctypes.c_void_p, ctypes.c_int32]
 lib.gpe_debug_ttrace_count.argtypes = [ctypes.c_int32]
 assert lib.gpe_debug_ttrace_count(1) >= 0
-os.environ["GPEMU_DEBUG_STOP_STEP"] = str(stop)
-try:
+if stop >= 0:
+    os.environ["GPEMU_DEBUG_STOP_STEP"] = str(stop)
+    try:
+        ctx.objective(0, 0, hp)
+    except Exception:   # the debug stop
+        pass
+    os.environ.pop("GPEMU_DEBUG_STOP_STEP", None)
+else:   # stop < 0: one whole evaluation; per launch after the Cholesky (TRTRI, LAUUM)
     ctx.objective(0, 0, hp)
-except Exception:   # the debug stop
-    pass
-os.environ.pop("GPEMU_DEBUG_STOP_STEP", None)
 cnt = lib.gpe_debug_ttrace_count(0)
 assert 0 < cnt <= 262144, cnt
 buf = np.zeros(8 * cnt, dtype=np.uint64)
@@ -84,5 +87,23 @@ for i in range(len(bounds) - 1):
         if sel.any():
             ph[kn + "_us"] = float(np.mean(en[sel] - st[sel]))
     out["phases"][names[i]] = ph
+if stop < 0:   # the launches after the sweep: every launch starts with its workgroup 0
+    s0 = np.sort(st[bidx == 0])
+    after = s0[s0 > dstart[-1] + 1.0]
+    rows = []
+    for i, a in enumerate(after):
+        b = after[i + 1] if i + 1 < len(after) else np.inf
+        sel = (st >= a - 10.0) & (st < b - 10.0) & ok
+        if not sel.any():
+            continue
+        lb, le = st[sel].min(), en[sel].max()
+        mm = (grid >= lb) & (grid < le)
+        full = np.nonzero(act[mm] >= 0.9 * 512)[0]
+        rows.append({"tiles": int(sel.sum()), "span_us": float(le - lb),
+                     "occupancy": float(act[mm].mean() / 512) if mm.any() else 0.0,
+                     "drain_us": float(le - grid[mm][full[-1]]) if len(full) else float(le - lb),
+                     "tile_us_mean": float(np.mean(en[sel] - st[sel])), "tile_us_max": float(np.max(en[sel] - st[sel])),
+                     "K_max": int(w[sel, 7].max())})
+    out["after_sweep"] = rows
 print(json.dumps(out, indent=1))
 json.dump(out, open(os.path.join(ROOT, "gpurun_out", f"tile_timeline{tag}.json"), "w"), indent=1)
