@@ -6,8 +6,8 @@ apart), each over one evaluation at (n, d) (tools/prof_objective.py).  Launches 
 matched across passes by their order.  Per MI355X_MICROARCH.md: clock = GRBM_GUI_ACTIVE
 / 8 / wall time, MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (clock cycles x 1024 SIMDs),
 FETCH_SIZE doubled on gfx950 (KiB).
-Phases: the 128 fused Cholesky launches in column groups (steps 1-47 / 48-87 / 88-127),
-the TRTRI launches, the LAUUM.
+Phases: the Cholesky launches (one per step or one per column group) by steps 0/1-47 /
+48-87 / 88-127, the TRTRI launches, the LAUUM.
 usage: python tools/pmc_phases.py [n] [d]"""
 import csv
 import glob
@@ -48,10 +48,17 @@ for i, counters in enumerate(passes):
             for key, v in b.items():
                 if key not in ("ns", "kind"):
                     a[key] = v
-assert len(launches) == 143, len(launches)   # 128 Cholesky + 14 TRTRI + 1 LAUUM at n = 16384
-groups = {"chol 1-47": launches[1:48], "chol 48-87": launches[48:88], "chol 88-127": launches[88:128],
-          "trtri": launches[128:142], "lauum": launches[142:143]}
-out = {"n": n, "d": d, "phases": {}}
+# 14 TRTRI + 1 LAUUM after the Cholesky's launches: 128 per step (GPEMU_POTRF=fused), or 72
+# per column group (the default for a lone evaluation: 12 groups of 4, 20 of 2, 40 of 1)
+nch = len(launches) - 15
+if nch == 128:
+    groups = {"chol 1-47": launches[1:48], "chol 48-87": launches[48:88], "chol 88-127": launches[88:128]}
+elif nch == 72:
+    groups = {"chol 0-47": launches[0:12], "chol 48-87": launches[12:32], "chol 88-127": launches[32:72]}
+else:
+    groups = {"chol": launches[:nch]}
+groups.update({"trtri": launches[nch:nch + 14], "lauum": launches[nch + 14:nch + 15]})
+out = {"n": n, "d": d, "schedule": os.environ.get("GPEMU_POTRF", "auto"), "phases": {}}
 for name, ls in groups.items():
     ns = sum(e["ns"] for e in ls)
     gui = sum(e.get("GRBM_GUI_ACTIVE", 0.0) for e in ls)
