@@ -123,10 +123,11 @@ struct gpe_ctx {
   double* dskp = nullptr;    // skinny partials
   size_t skp_cap = 0;
   double* dgpart = nullptr;  // gram partials
-  double* dgram = nullptr;   // GPE_MAX_COLS^2
-  double* dT2 = nullptr;     // GPE_MAX_COLS^2
+  double* dgram = nullptr;   // P^2 (P = q + 1 basis columns)
+  double* dT2 = nullptr;     // P^2
   double* dcpart = nullptr;  // contraction partials
   size_t cpart_cap = 0;
+  size_t invd_cap = 0, csum_cap = 0, gram_cap = 0;   // dinvdelta (d), dcsum (d + 3), dgram / dT2 (P^2)
   double* dcsum = nullptr;   // d+3
   GemmProb* dprobs = nullptr;
   unsigned* dtiles = nullptr;    // tile lists: training plan [0, cap/2), aux plan [cap/2, cap)
@@ -270,6 +271,27 @@ int dalloc(gpe_ctx* c, T** p, size_t count) {
     *p = nullptr;
     return fail(c, GPE_ERR_ALLOC, std::string("hipMalloc failed: ") + hipGetErrorString(e) +
                                       " (" + std::to_string(count * sizeof(T)) + " bytes)");
+  }
+  return GPE_OK;
+}
+
+// the per-dimension and per-basis-column device buffers, grown to the shape in use: the
+// reference takes any d and any basis (_emulatorkernels.py:39-50), and so does the library
+// (d > 32 and P > 33 run the LDS-staged wide kernels)
+int ensure_shape_bufs(gpe_ctx* c, int d, int P) {
+  if ((size_t)d > c->invd_cap) {
+    CHK(dalloc(c, &c->dinvdelta, (size_t)d));
+    c->invd_cap = (size_t)d;
+  }
+  if ((size_t)d + 3 > c->csum_cap) {
+    CHK(dalloc(c, &c->dcsum, (size_t)d + 3));
+    c->csum_cap = (size_t)d + 3;
+  }
+  const size_t pp = (size_t)P * P;
+  if (pp > c->gram_cap) {
+    CHK(dalloc(c, &c->dgram, pp));
+    CHK(dalloc(c, &c->dT2, pp));
+    c->gram_cap = pp;
   }
   return GPE_OK;
 }
@@ -980,7 +1002,7 @@ int ensure_fact(gpe_ctx* c, Fact& F, long long n_pad) {
 
 // scaled points for the training set
 int scale_training(gpe_ctx* c, const double* delta) {
-  CHK(ensure_pinned(c, GPE_MAX_DIMS + 64));
+  CHK(ensure_pinned(c, (size_t)c->d + 64));
   for (int k = 0; k < c->d; ++k) {
     // zero or NaN length scale: the reference's covariance is NaN there and its Cholesky
     // raises LinAlgError (-> `return None`, _emulatoroptimise.py:374-376, :489-491)
@@ -1411,7 +1433,7 @@ int factor_and_invert(gpe_ctx* c, int kernel, const double* delta, double nu, do
   // without the inverse (value only, gpe_factor) the sweep carries [f H]^T in the
   // augmented row and leaves L^-1 [f H] there; with it, L^-1 [f H] is one skinny product
   // with L^-1 and the sweep stays lean
-  c->zaug_valid = !invert && c->tr.plan.aug;
+  c->zaug_valid = !invert && c->tr.plan.aug && P <= TILE;   // the row holds at most 128 columns
   if (c->zaug_valid) {
     const long long tot = c->n_pad * TILE;
     hipLaunchKernelGGL(k_aug_init, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, c->dF,
@@ -1606,10 +1628,7 @@ gpe_ctx* gpe_create(int32_t device) {
     return nullptr;
   }
   bool ok = dalloc(c, &c->dinfo, 4) == GPE_OK && dalloc(c, &c->dprobs, MAX_PROBS) == GPE_OK &&
-            dalloc(c, &c->dgram, GPE_MAX_COLS * GPE_MAX_COLS) == GPE_OK &&
-            dalloc(c, &c->dT2, GPE_MAX_COLS * GPE_MAX_COLS) == GPE_OK &&
-            dalloc(c, &c->dinvdelta, GPE_MAX_DIMS) == GPE_OK &&
-            dalloc(c, &c->dcsum, 64) == GPE_OK;
+            ensure_shape_bufs(c, GPE_MAX_DIMS, GPE_MAX_COLS) == GPE_OK;
   for (int i = 0; i < 16 && ok; ++i) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
   if (ok) {
     const int gl = G_LDS_DOUBLES * (int)sizeof(double);
@@ -1690,11 +1709,10 @@ int gpe_set_data(gpe_ctx* c, int64_t n, int32_t d, int32_t q, const double* X, c
                  const double* H, const double* r) {
   if (!c) return GPE_ERR_ARG;
   if (n <= 0 || d <= 0 || q <= 0 || !X || !f || !H) return fail(c, GPE_ERR_ARG, "bad data arguments");
-  if (d > GPE_MAX_DIMS) return fail(c, GPE_ERR_UNSUPPORTED, "more than 128 input dimensions");
-  if (q + 1 > GPE_MAX_COLS) return fail(c, GPE_ERR_UNSUPPORTED, "more than 127 basis functions");
   if (n > (1LL << 20)) return fail(c, GPE_ERR_UNSUPPORTED, "n too large");
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  CHK(ensure_shape_bufs(c, d, q + 1));
   const long long n_pad = ((n + TILE - 1) / TILE) * TILE;
   const bool resize = (n_pad != c->n_pad) || (d != c->d) || (q != c->q);
   c->n = n; c->d = d; c->q = q; c->n_pad = n_pad; c->NB = (int)(n_pad / TILE);
@@ -2519,8 +2537,9 @@ int gpe_kernel_var(gpe_ctx* c, int32_t kernel, const double* delta, int32_t d, d
                    int32_t predict, int64_t m, const double* X, const double* r, double r_scale,
                    double* A_out) {
   if (!c) return GPE_ERR_ARG;
-  if (!delta || !X || !A_out || m <= 0 || d <= 0 || d > GPE_MAX_DIMS) return fail(c, GPE_ERR_ARG, "bad kernel_var args");
+  if (!delta || !X || !A_out || m <= 0 || d <= 0) return fail(c, GPE_ERR_ARG, "bad kernel_var args");
   HIPCHK(c, hipSetDevice(c->device));
+  CHK(ensure_shape_bufs(c, d, 1));
   const long long mp = ((m + TILE - 1) / TILE) * TILE;
   const int mt = (int)(mp / TILE);
   double *dx = nullptr, *dxw = nullptr, *dout = nullptr, *dr = nullptr;
@@ -2571,8 +2590,9 @@ int gpe_kernel_var(gpe_ctx* c, int32_t kernel, const double* delta, int32_t d, d
 int gpe_kernel_grad(gpe_ctx* c, const double* delta, int32_t d, int64_t m, const double* X,
                     const double* col, double col_scale, double pre, double* G_out) {
   if (!c) return GPE_ERR_ARG;
-  if (!delta || !X || !G_out || m <= 0 || d <= 0 || d > GPE_MAX_DIMS) return fail(c, GPE_ERR_ARG, "bad kernel_grad args");
+  if (!delta || !X || !G_out || m <= 0 || d <= 0) return fail(c, GPE_ERR_ARG, "bad kernel_grad args");
   HIPCHK(c, hipSetDevice(c->device));
+  CHK(ensure_shape_bufs(c, d, 1));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   const long long mp = ((m + TILE - 1) / TILE) * TILE;
   const int mt = (int)(mp / TILE);
@@ -2683,9 +2703,10 @@ int gpe_lhc_maximin(gpe_ctx* c, int32_t N, int64_t n, int32_t dim, const double*
 int gpe_kernel_covar(gpe_ctx* c, int32_t kernel, const double* delta, int32_t d, double nu,
                      int64_t n, const double* XT, int64_t m, const double* XV, double* C_out) {
   if (!c) return GPE_ERR_ARG;
-  if (!delta || !XT || !XV || !C_out || n <= 0 || m <= 0 || d <= 0 || d > GPE_MAX_DIMS)
+  if (!delta || !XT || !XV || !C_out || n <= 0 || m <= 0 || d <= 0)
     return fail(c, GPE_ERR_ARG, "bad kernel_covar args");
   HIPCHK(c, hipSetDevice(c->device));
+  CHK(ensure_shape_bufs(c, d, 1));
   // compute C^T (m x n, column-major == n x m row-major)
   const long long mp = ((m + TILE - 1) / TILE) * TILE, np = ((n + TILE - 1) / TILE) * TILE;
   double *dxt = nullptr, *dxv = nullptr, *dxtw = nullptr, *dxvw = nullptr, *dout = nullptr;

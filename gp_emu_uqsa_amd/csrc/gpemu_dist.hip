@@ -1076,7 +1076,9 @@ const char* gpe_dist_last_error(gpe_dist* h) { return h ? h->err.c_str() : "null
 int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double* X, const double* f,
                       const double* H, const double* r) {
   if (!h) return GPE_ERR_ARG;
-  if (n <= 0 || d <= 0 || d > GPE_MAX_DIMS || q < 0 || q + 1 > GPE_MAX_COLS || !X || !f || (q > 0 && !H))
+  // [f H]^T rides in ONE tile row under the matrix (tile row NB): at most 128 columns
+  if (q + 1 > TILE) return dfail(h, GPE_ERR_UNSUPPORTED, "the row-block path takes at most 127 basis functions");
+  if (n <= 0 || d <= 0 || q < 0 || !X || !f || (q > 0 && !H))
     return dfail(h, GPE_ERR_ARG, "bad shapes");
   DCHK_HIP(h, hipSetDevice(h->device));
   DCHK_HIP(h, hipStreamSynchronize(h->stream));
@@ -1119,7 +1121,7 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
     std::memcpy(h->hpin, r, (size_t)n * sizeof(double));
     DCHK_HIP(h, hipMemcpy(h->dr, h->hpin, (size_t)np * sizeof(double), hipMemcpyHostToDevice));
   }
-  DCHK(dalloc(h, &h->dinvdelta, GPE_MAX_DIMS, &h->shared_bytes));
+  DCHK(dalloc(h, &h->dinvdelta, (size_t)d, &h->shared_bytes));
   // local ranks and their sweep buffers
   build_groups(h);
   h->panel_sz = (size_t)(h->NB + 1) * TILE * TILE * h->wmax;

@@ -50,10 +50,12 @@ enum gpe_kernel { GPE_KERNEL_STD = 0, GPE_KERNEL_ALT_NUG = 1 };
 /* objective: _emulatoroptimise.py:412 (gp4ml) and :305 (mucm) */
 enum gpe_variant { GPE_GP4ML = 0, GPE_MUCM = 1 };
 
-/* Shape limits: input dimensions d and columns q + 1 of [f H] (the reference's
- * linear mean has q = d + 1).  The kernels for d <= 32 and q + 1 <= 32 keep
- * coordinates and basis rows in registers; beyond that they stage them through LDS
- * in chunks of 32. */
+/* Input dimensions d and columns q + 1 of [f H] (the reference's linear mean has
+ * q = d + 1) take any value, as in the reference (_emulatorkernels.py:39-50): the
+ * kernels for d <= 32 and q + 1 <= 33 keep coordinates and basis rows in registers,
+ * beyond that they stage them through LDS in chunks of 32.  The two constants below
+ * are only the sizes a context's small per-dimension / per-column buffers start at
+ * (they grow with the data); they are no longer limits (ABI version 8 and later). */
 #define GPE_MAX_DIMS 128
 #define GPE_MAX_COLS 128
 

@@ -42,14 +42,51 @@ def test_nan_hyperparameter_is_not_pd(ctx):
     assert np.isfinite(llh)
 
 
-def test_argument_limits(ctx):
-    """GPE_MAX_DIMS = GPE_MAX_COLS = 128 (include/gpemu.h); beyond: a loud error."""
-    X, f, H = orc.synthetic_problem(100, 3, seed=1)
+def _wide_problem(n, d, seed):
+    rs = np.random.RandomState(seed)
+    X = rs.uniform(size=(n, d))
+    f = np.sin(X @ rs.normal(size=d) / np.sqrt(d)) + 0.01 * rs.normal(size=n)
+    return X, f, orc.linear_basis(X)
+
+
+def test_any_d_and_basis_width(ctx):
+    """No input-dimension or basis-width limit, as in the reference
+    (_emulatorkernels.py:39-50 takes any d): d = 150 inputs with the linear mean's
+    151 basis columns, beyond the 128 the context's small buffers start at
+    (GPE_MAX_DIMS / GPE_MAX_COLS, include/gpemu.h).  Value, gradient and sigma^2
+    against the oracle (the value path without the augmented row, which holds 128
+    columns), then the kernel matrix at d = 129, and the row-block path (2 loopback
+    ranks) at d = 150 with 21 basis columns (it carries [f H]^T in one tile row: more
+    than 128 columns there is a loud error)."""
+    n, d = 400, 150
+    X, f, H = _wide_problem(n, d, seed=8)
+    hp = np.concatenate([np.linspace(2.5, 4.0, d), [1e-2, 0.9]])
     ctx.set_data(X, f, H)
-    with pytest.raises(RuntimeError):      # more than 128 input dimensions
-        ctx.kernel_var(native.KERNEL_STD, np.ones(129), 1e-3, np.zeros((10, 129)))
-    with pytest.raises(RuntimeError):      # more than 127 basis functions
-        ctx.set_data(X, f, np.ones((100, 128)))
+    llh, g, s2 = ctx.objective(native.GP4ML, native.KERNEL_STD, hp)
+    ref = orc.objective_fast(X, f, H, hp, orc.GP4ML, orc.STD, True)
+    assert abs(llh - ref[0]) <= 1e-10 * abs(ref[0]), (llh, ref[0])
+    scale = np.max(np.abs(ref[1])) + 1.0
+    assert np.max(np.abs(g - ref[1])) <= 1e-7 * scale, np.max(np.abs(g - ref[1]))
+    v = ctx.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=False)[0]
+    assert abs(v - ref[0]) <= 1e-10 * abs(ref[0])
+    X2 = np.random.RandomState(9).uniform(size=(50, 129))
+    A = ctx.kernel_var(native.KERNEL_STD, np.full(129, 3.0), 1e-3, X2)
+    Aref, _ = orc.kernel_var_ref(X2, np.full(129, 3.0), 1e-3, orc.STD, True)
+    assert np.max(np.abs(A - Aref)) <= 1e-13
+    # the row-block path carries [f H]^T in one tile row: any d, at most 128 columns
+    H2 = H[:, :21]
+    ref2 = orc.objective_fast(X, f, H2, hp, orc.GP4ML, orc.STD, True)
+    dc = native.DistContext(0, 2)
+    try:
+        with pytest.raises(RuntimeError):
+            dc.set_data(X, f, H)
+        dc.set_data(X, f, H2)
+        llh_d, g_d, _ = dc.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=True)
+    finally:
+        dc.close()
+    assert abs(llh_d - ref2[0]) <= 1e-10 * abs(ref2[0]), (llh_d, ref2[0])
+    scale2 = np.max(np.abs(ref2[1])) + 1.0
+    assert np.max(np.abs(g_d - ref2[1])) <= 1e-7 * scale2
 
 
 def test_noise_sample_single_point(ctx):
