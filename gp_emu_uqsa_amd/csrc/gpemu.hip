@@ -208,6 +208,10 @@ struct gpe_ctx {
   std::vector<std::pair<int, int>> potrf_groups = {{4, 80}, {2, 40}};
   int chol_prio = 1;   // fused Cholesky (1), and the TRTRI levels (2), on the high-priority stream
   int potrf_first = 0;   // width of the first column group (0: as potrf_groups)
+  // panel tiles of the fused Cholesky by block substitution with L and X's diagonal
+  // blocks, released before the diagonal workgroup assembles the rest of X (default);
+  // GPEMU_PANEL=xmul: multiply by the whole X = L^-1, released after it (A/B)
+  bool panel_trsm = true;
 
   // overlapped Cholesky tail (potrf_trtri_overlap): the width-1 tail steps on one half of
   // the CUs, the triangular inverse of the leading block on the other half (CU-masked
@@ -537,6 +541,7 @@ GemmProb mkprob(const double* A, long long lda, const double* B, long long ldb, 
   p.alpha = alpha; p.beta = beta;
   p.tile_begin = 0; p.ntiles = 0;
   p.X = nullptr; p.ldx = 0; p.logdet = nullptr; p.diag_col0 = 0; p.flag = nullptr;
+  p.Ld = nullptr; p.ldd = 0;
   p.pre0 = p.pre1 = p.post = nullptr; p.pre0_n = p.pre1_n = 0;
   return p;
 }
@@ -583,6 +588,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
     p.logdet = F.logdet + t;
     p.diag_col0 = t * TILE;
     p.flag = F.flags + t;
+    if (c->panel_trsm) { p.Ld = tile(A, t, t); p.ldd = ld; }
     return p;
   };
   auto panelprob = [&](int t, const double* Lp, const double* Lt, int K, double alpha) {
@@ -591,6 +597,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
     p.ldx = ld;
     p.flag = F.flags + t;
     p.diag_col0 = t * TILE;   // step index for the GEMM_TRACE dev build
+    if (c->panel_trsm) { p.Ld = tile(A, t, t); p.ldd = ld; }
     return p;
   };
   // bulk problems: tiles (i, j), i >= j, j in [a, b), updated by columns [g0, g0 + K/128);
@@ -661,6 +668,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
         pa.X = tile(B, t, t);
         pa.ldx = ld;
         pa.flag = F.flags + t;
+        if (c->panel_trsm) { pa.Ld = tile(A, t, t); pa.ldd = ld; }
         pa.diag_col0 = -TILE;   // (no GEMM_TRACE slot)
         fp.push_back(pa);
       }
@@ -750,6 +758,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
           pa.X = tile(B, t, t);
           pa.ldx = ld;
           pa.flag = F.flags + t;
+        if (c->panel_trsm) { pa.Ld = tile(A, t, t); pa.ldd = ld; }
           pa.diag_col0 = -TILE;
           wire(pa);
           pa.post = cnt_pan + t;
@@ -858,6 +867,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
           pa.X = tile(B, t, t);
           pa.ldx = ld;
           pa.flag = F.flags + t;
+        if (c->panel_trsm) { pa.Ld = tile(A, t, t); pa.ldd = ld; }
           pa.diag_col0 = -TILE;
           fp.push_back(pa);
         }
@@ -1602,6 +1612,7 @@ gpe_ctx* gpe_create(int32_t device) {
     if (const char* eg = std::getenv("GPEMU_GROUP_STRIDE")) c->grp_stride = std::max(0, std::atoi(eg));
     if (const char* ep = std::getenv("GPEMU_CHOL_PRIO")) c->chol_prio = std::max(0, std::min(2, std::atoi(ep)));
     if (const char* ef = std::getenv("GPEMU_POTRF_FIRST")) c->potrf_first = std::max(0, std::min(8, std::atoi(ef)));
+    if (const char* ep = std::getenv("GPEMU_PANEL")) c->panel_trsm = std::string(ep) != "xmul";
     if (const char* e3 = std::getenv("GPEMU_POTRF_W")) {
       c->potrf_groups.clear();
       std::string spec(e3);

@@ -29,9 +29,16 @@ constexpr int DB_EXTRA_DOUBLES = 128 + 8;        // X diagonal, reduction slots,
 // dev-tool phase timing (tools/hip/db_bench.hip): -DDB_TIMING
 #ifdef DB_TIMING
 __device__ unsigned long long db_tsc[8];
-#define DB_T(slot) do { if (threadIdx.x == 0) db_tsc[slot] += wall_clock64(); } while (0)
-#define DB_TN(slot) do { if (threadIdx.x == 0) db_tsc[slot] -= wall_clock64(); } while (0)
+// per-thread register accumulators (a global read-modify-write per mark would put
+// an HBM round trip inside every interval); slot 7 is timed by wave 1
+#define DB_T(slot) do { dbt[slot] += wall_clock64(); } while (0)
+#define DB_TN(slot) do { dbt[slot] -= wall_clock64(); } while (0)
+#define DB_TDECL unsigned long long dbt[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define DB_TFLUSH do { if (threadIdx.x == 0 || threadIdx.x == 64) \
+    for (int s_ = 0; s_ < 8; ++s_) if ((s_ == 7) == (threadIdx.x == 64)) atomicAdd(&db_tsc[s_], dbt[s_]); } while (0)
 #else
+#define DB_TDECL do {} while (0)
+#define DB_TFLUSH do {} while (0)
 #define DB_T(slot) do {} while (0)
 #define DB_TN(slot) do {} while (0)
 #endif
@@ -187,22 +194,75 @@ __device__ __forceinline__ void db_xlevel(double* lb) {
   __syncthreads();
 }
 
+// One wave stores 16 x 16 block (column-major at lb[off]) to G (its top-left element):
+// lane = 8 columns x 8 row pairs per 16-byte store.  MODE 0: whole block; 1: lower
+// part with the diagonal only (L's diagonal blocks, whose upper part holds X^T);
+// 2: lower part and zeros above (X's diagonal blocks).
+template <int MODE>
+__device__ __forceinline__ void db_put_block(const double* lb, int off, double* G, long long ld) {
+  const int lane = threadIdx.x & 63;
+  const int r = (lane & 7) * 2;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = (lane >> 3) + 8 * h;
+    double2 v = *reinterpret_cast<const double2*>(lb + off + r + c * 16);
+    double* gp = G + r + (long long)c * ld;
+    if (MODE == 1) {
+      if (r >= c) *reinterpret_cast<double2*>(gp) = v;
+      else if (r + 1 == c) gp[1] = v.y;
+    } else {
+      if (MODE == 2) {
+        if (r < c) v.x = 0.0;
+        if (r + 1 < c) v.y = 0.0;
+      }
+      *reinterpret_cast<double2*>(gp) = v;
+    }
+  }
+}
+
+__device__ __forceinline__ int db_blk(int bi, int bk) { return (bi * (bi + 1) / 2 + bk) * 256; }
+
 // Factor + invert the tile held block-packed in lb[0 .. 36*256).  Writes L (lower)
 // to Lg, X = L^-1 (full tile, zero upper) to Xg, returns 0 or the 1-based column
 // of the first bad pivot; *logdet_out (thread 0) = sum log L_jj.
 // LDS: lb[0, DB_LDS_DOUBLES) plus DB_EXTRA_DOUBLES after it.
+// The global stores ride beside the arithmetic: X's zero upper blocks while wave 0
+// factors the first leaf, each column block of L once its panel step is done (waves
+// 1-3, behind their share of the trailing update), X's blocks as each level of the
+// assembly finishes them -- so only the last level's 16 blocks follow the arithmetic.
+// on_factored(): called by every thread once L and X's diagonal blocks are stored (only
+// with a good factor), before the rest of X is assembled -- the fused Cholesky's panel
+// tiles need no more than those (their block substitution, k_gemm G_PANEL).
+template <class OnFactored>
 __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long long ldl, double* Xg,
-                                                long long ldx, double* logdet_out) {
+                                                long long ldx, double* logdet_out, OnFactored on_factored) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   double* xs = lb + 36 * 256;             // current leaf inverse, column-major 16 x 16
   double* xdiag = lb + DB_LDS_DOUBLES;    // 128 diagonal entries of X
   double* red = xdiag + 128;              // 4
   int* flag = reinterpret_cast<int*>(red + 4);
+  auto lg_at = [&](int bi, int bk) { return Lg + bi * 16 + (long long)(bk * 16) * ldl; };
+  auto xg_at = [&](int bi, int bk) { return Xg + bi * 16 + (long long)(bk * 16) * ldx; };
   if (tid == 0) *flag = 0;
+  DB_TDECL;
   __syncthreads();
   DB_TN(0);
   DB_TN(1);
-  if (wave == 0) db_leaf(lb, xs, xdiag, 0, flag);
+  if (wave == 0) {
+    db_leaf(lb, xs, xdiag, 0, flag);
+  } else {
+    // X's 28 strictly-upper blocks are zero
+    for (int b = wave - 1; b < 28; b += 3) {
+      int bk = 1;
+      while (bk * (bk + 1) / 2 <= b) ++bk;            // b = bk(bk-1)/2 + bi, bi < bk
+      const int bi = b - bk * (bk - 1) / 2;
+      const int r = (lane & 7) * 2;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        *reinterpret_cast<double2*>(xg_at(bi, bk) + r + (long long)((lane >> 3) + 8 * h) * ldx) =
+            make_double2(0.0, 0.0);
+    }
+  }
   __syncthreads();
   DB_T(1);
   for (int jb = 0; jb < 8; ++jb) {
@@ -210,7 +270,7 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
     DB_TN(2);
     // ---- panel: L(ib,jb) = A(ib,jb) X_jb^T, one 16x16 block per wave
     for (int ib = jb + 1 + wave; ib < 8; ib += 4) {
-      const int bo = (ib * (ib + 1) / 2 + jb) * 256;
+      const int bo = db_blk(ib, jb);
       d4 acc = d4{0.0, 0.0, 0.0, 0.0};
       double av[4], bv[4];
 #pragma unroll
@@ -228,39 +288,38 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
     DB_T(2);
     if (jb == 7) break;
     // ---- wave 0: update diagonal block jb+1 and factor it (look-ahead);
-    //      waves 1-3: the rest of the trailing update A(ib,kb) -= L(ib,jb) L(kb,jb)^T
+    //      waves 1-3: the rest of the trailing update A(ib,kb) -= L(ib,jb) L(kb,jb)^T,
+    //      then column block jb of L out
     DB_TN(1);
     if (wave == 0) {
-      const int p1 = ((jb + 1) * (jb + 2) / 2 + jb) * 256;
+      const int p1 = db_blk(jb + 1, jb);
       DB_TN(6);
-      db_syrk_block(lb, p1, p1, ((jb + 1) * (jb + 2) / 2 + jb + 1) * 256);
+      db_syrk_block(lb, p1, p1, db_blk(jb + 1, jb + 1));
       DB_T(6);
       DB_TN(5);
       db_leaf(lb, xs, xdiag, jb + 1, flag);
       DB_T(5);
     } else {
+      DB_TN(7);
       const int m = 7 - jb, cnt = m * (m + 1) / 2;
       for (int b = wave; b < cnt; b += 3) {          // b = 0 is the diagonal block (wave 0)
         int rr = 0;
         while ((rr + 1) * (rr + 2) / 2 <= b) ++rr;
         const int ib = jb + 1 + rr, kb = jb + 1 + (b - rr * (rr + 1) / 2);
-        db_syrk_block(lb, (ib * (ib + 1) / 2 + jb) * 256, (kb * (kb + 1) / 2 + jb) * 256,
-                      (ib * (ib + 1) / 2 + kb) * 256);
+        db_syrk_block(lb, db_blk(ib, jb), db_blk(kb, jb), db_blk(ib, kb));
       }
+      for (int ib = jb + wave - 1; ib < 8; ib += 3) {
+        if (ib == jb) db_put_block<1>(lb, db_blk(jb, jb), lg_at(jb, jb), ldl);
+        else db_put_block<0>(lb, db_blk(ib, jb), lg_at(ib, jb), ldl);
+      }
+      DB_T(7);
     }
     __syncthreads();
     DB_T(1);
   }
   DB_TN(4);
-  // ---- L out (lower part), log-determinant
-  for (int e = tid; e < 64 * 128; e += 256) {
-    const int i = (e & 63) * 2, k = e >> 6;
-    if (i + 1 < k) continue;
-    double* lp = Lg + i + (long long)k * ldl;
-    const double l1 = lb[db_off(i + 1, k)];
-    if (i >= k) *reinterpret_cast<double2*>(lp) = make_double2(lb[db_off(i, k)], l1);
-    else lp[1] = l1;
-  }
+  // ---- last diagonal block of L out, log-determinant
+  if (wave == 1) db_put_block<1>(lb, db_blk(7, 7), lg_at(7, 7), ldl);
   double lg = (tid < 128) ? log(lb[db_off(tid, tid)]) : 0.0;
   for (int off = 32; off > 0; off >>= 1) lg += __shfl_down(lg, off, 64);
   if ((tid & 63) == 0) red[tid >> 6] = lg;
@@ -269,7 +328,7 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
   // ---- diagonal blocks -> X leaves (lower part): X(i,c) stored at (c,i), diag in xdiag
   {
     const int jb = tid >> 5, t = tid & 31;          // 8 blocks x 32 threads
-    const int base = (jb * (jb + 1) / 2 + jb) * 256;
+    const int base = db_blk(jb, jb);
     for (int e = t; e < 256; e += 32) {
       const int i = e & 15, c = e >> 4;
       if (i > c) lb[base + i + c * 16] = lb[base + c + i * 16];
@@ -279,21 +338,28 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
   __syncthreads();
   DB_T(4);
   DB_TN(3);
+  for (int b = wave; b < 8; b += 4) db_put_block<2>(lb, db_blk(b, b), xg_at(b, b), ldx);
+  on_factored();
   db_xlevel<16>(lb);
+  db_put_block<0>(lb, db_blk(2 * wave + 1, 2 * wave), xg_at(2 * wave + 1, 2 * wave), ldx);
   db_xlevel<32>(lb);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {                       // rows {2,3} x cols {0,1}, rows {6,7} x cols {4,5}
+    const int q = wave * 2 + h, o = (q >> 2) * 4;
+    const int bi = o + 2 + ((q >> 1) & 1), bk = o + (q & 1);
+    db_put_block<0>(lb, db_blk(bi, bk), xg_at(bi, bk), ldx);
+  }
   db_xlevel<64>(lb);
   DB_T(3);
   DB_TN(4);
-  // ---- X out: full tile, zero above the diagonal
-  for (int e = tid; e < 64 * 128; e += 256) {
-    const int i = (e & 63) * 2, k = e >> 6;
-    double x0 = 0.0, x1 = 0.0;
-    if (i >= k) x0 = lb[db_off(i, k)];
-    if (i + 1 >= k) x1 = lb[db_off(i + 1, k)];
-    *reinterpret_cast<double2*>(Xg + i + (long long)k * ldx) = make_double2(x0, x1);
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {                       // rows 4-7 x cols 0-3
+    const int bi = 4 + wave, bk = h;
+    db_put_block<0>(lb, db_blk(bi, bk), xg_at(bi, bk), ldx);
   }
   DB_T(4);
   DB_T(0);
+  DB_TFLUSH;
   return 0;
 }
 

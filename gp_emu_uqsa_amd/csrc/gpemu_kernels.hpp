@@ -651,8 +651,13 @@ struct GemmProb {
   int mt, nt, K, flags;
   double alpha, beta;
   int tile_begin, ntiles;
-  double* X;          // G_DIAG only
+  double* X;          // G_DIAG: X = L^-1 out; G_PANEL: X's diagonal 16 x 16 blocks in
   long long ldx;
+  // G_PANEL: the factored diagonal tile L (its strictly lower 16 x 16 blocks), for the
+  // block substitution P = C L^-T; G_DIAG: non-null = release the panel tiles as soon
+  // as L and X's diagonal blocks are out (null: after all of X, for X-multiply panels)
+  const double* Ld;
+  long long ldd;
   double* logdet;
   int diag_col0;
   int* flag;          // G_DIAG releases, G_PANEL waits
@@ -1200,6 +1205,78 @@ __device__ unsigned long long gemm_trace[8 * 4096];
 #define GTRACE(P, slot) do {} while (0)
 #endif
 
+// Panel tile of the fused Cholesky by block substitution: P = C L^-T for a 128 x 128
+// tile C (in place, ldc) against the factored diagonal tile L (ldd) and its diagonal
+// blocks' inverses X_b (X's diagonal 16 x 16 blocks, ldx).  As transposes, P^T(jb) =
+// X_jb (C^T(jb) - sum_{kb<jb} L(jb,kb) P^T(kb)) for the eight 16-row blocks jb.
+// LDS: -L(jb,kb) (kb < jb) and X_jb, block-packed (db_blk) -- 72 KB, the staging space.
+// Wave w owns the tile's rows 32w .. 32w+31 (two 16-column blocks cb of P^T), so the
+// waves never exchange data; an MFMA result (row (lane>>4)+4r, column lane&15) is
+// already the B operand of the next product (k = 4s + (lane>>4), n = lane&15 at s = r).
+__device__ __forceinline__ void panel_subst(double* Cb, long long ldc, const double* Ld, long long ldd,
+                                            const double* Xd, long long ldx, double* lb) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // stage: 36 blocks x 128 16-byte pieces
+  for (int e = tid; e < 36 * 128; e += 256) {
+    const int b = e >> 7, w = e & 127;
+    int bi = 0;
+    while ((bi + 1) * (bi + 2) / 2 <= b) ++bi;
+    const int bk = b - bi * (bi + 1) / 2;
+    const int r = (w & 7) * 2, c = w >> 3;
+    double2 v;
+    if (bi == bk) {
+      v = *reinterpret_cast<const double2*>(Xd + (bi * 16 + r) + (long long)(bk * 16 + c) * ldx);
+    } else {
+      v = *reinterpret_cast<const double2*>(Ld + (bi * 16 + r) + (long long)(bk * 16 + c) * ldd);
+      v.x = -v.x;
+      v.y = -v.y;
+    }
+    *reinterpret_cast<double2*>(lb + b * 256 + r + c * 16) = v;
+  }
+  // C^T blocks of this wave's rows (D layout)
+  d4 pt[8][2];
+  const int row0 = wave * 32 + (lane & 15);
+#pragma unroll
+  for (int jb = 0; jb < 8; ++jb)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        pt[jb][cb][r] = Cb[(row0 + cb * 16) + (long long)(jb * 16 + (lane >> 4) + 4 * r) * ldc];
+  __syncthreads();
+  const int ao = (lane & 15) + (lane >> 4) * 16;   // A operand (m = lane&15, k = 4s + lane>>4) at ao + 64 s
+#pragma unroll
+  for (int jb = 0; jb < 8; ++jb) {
+    d4 t0[2], t1[2];
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) { t0[cb] = pt[jb][cb]; t1[cb] = d4{0.0, 0.0, 0.0, 0.0}; }
+#pragma unroll
+    for (int kb = 0; kb < jb; ++kb) {
+      const double* a = lb + db_blk(jb, kb) + ao;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const double av = a[64 * s];
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          if (kb & 1) t1[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, pt[kb][cb][s], t1[cb], 0, 0, 0);
+          else t0[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, pt[kb][cb][s], t0[cb], 0, 0, 0);
+        }
+      }
+    }
+    const double* x = lb + db_blk(jb, jb) + ao;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const d4 t = t0[cb] + t1[cb];
+      d4 o = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) o = __builtin_amdgcn_mfma_f64_16x16x4f64(x[64 * s], t[s], o, 0, 0, 0);
+      pt[jb][cb] = o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Cb[(row0 + cb * 16) + (long long)(jb * 16 + (lane >> 4) + 4 * r) * ldc] = o[r];
+    }
+  }
+}
+
 // FUSED (only <false, false, true>): the fused Cholesky's launches, whose problems may be
 // G_DIAG / G_PANEL; the other instances hold no factor / panel code, so they stay well
 // inside the register budget and use the 16-byte C preload and epilogue.
@@ -1358,10 +1435,19 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
             if (m >= n) lds[db_off(m, n)] = P.alpha * acc[i][j][r];
           }
       __syncthreads();
-      const int bad = db_factor_invert(lds, Cb, P.ldc, P.X, P.ldx, P.logdet);
-      GTRACE(P, 2);
+      // substitution panels (P.Ld set) are released once L and X's diagonal blocks are
+      // out; X-multiply panels after the whole of X
+      const bool early = P.flag && P.Ld;
+      const int bad = db_factor_invert(lds, Cb, P.ldc, P.X, P.ldx, P.logdet, [&] {
+        if (early) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's L / X-block stores done
+          __syncthreads();
+          if (tid == 0) { gemm_publish_flag(P.flag, 1); GTRACE(P, 2); }
+        }
+      });
+      if (!early) GTRACE(P, 2);
       if (bad && tid == 0 && abort_flag) atomicCAS(abort_flag, 0, P.diag_col0 + bad);
-      if (P.flag) {
+      if (P.flag && (bad || !early)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's L / X stores done
         __syncthreads();
         if (tid == 0) gemm_publish_flag(P.flag, bad ? 2 : 1);
@@ -1387,12 +1473,16 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
         return;
       }
       TTRACE(1);   // (panel tiles: [1] = the diagonal inverse seen)
+      if (P.Ld) {
+        panel_subst(Cb, P.ldc, P.Ld, P.ldd, P.X, P.ldx, lds);
+      } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
-      gemm_kloop<false, false, true, false, false>(Cb, P.X, P.ldc, P.ldx, 0, TILE / GK, lds, acc);
-      gemm_store<false>(Cb, P.ldc, 1.0, acc);
+          for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+        gemm_kloop<false, false, true, false, false>(Cb, P.X, P.ldc, P.ldx, 0, TILE / GK, lds, acc);
+        gemm_store<false>(Cb, P.ldc, 1.0, acc);
+      }
       if (ti == 0) GTRACE(P, 7);
       if (P.post) gemm_post_count(P.post);
 #ifdef GEMM_TTRACE
