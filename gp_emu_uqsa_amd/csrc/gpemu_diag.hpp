@@ -302,6 +302,9 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
     } else {
       DB_TN(7);
       const int m = 7 - jb, cnt = m * (m + 1) / 2;
+#ifdef DB_NO_UPDATE
+      if (cnt < 0)   // dev probe: the leaf without the concurrent update (wrong results)
+#endif
       for (int b = wave; b < cnt; b += 3) {          // b = 0 is the diagonal block (wave 0)
         int rr = 0;
         while ((rr + 1) * (rr + 2) / 2 <= b) ++rr;

@@ -1209,33 +1209,14 @@ __device__ unsigned long long gemm_trace[8 * 4096];
 // tile C (in place, ldc) against the factored diagonal tile L (ldd) and its diagonal
 // blocks' inverses X_b (X's diagonal 16 x 16 blocks, ldx).  As transposes, P^T(jb) =
 // X_jb (C^T(jb) - sum_{kb<jb} L(jb,kb) P^T(kb)) for the eight 16-row blocks jb.
-// LDS: -L(jb,kb) (kb < jb) and X_jb, block-packed (db_blk) -- 72 KB, the staging space.
 // Wave w owns the tile's rows 32w .. 32w+31 (two 16-column blocks cb of P^T), so the
 // waves never exchange data; an MFMA result (row (lane>>4)+4r, column lane&15) is
 // already the B operand of the next product (k = 4s + (lane>>4), n = lane&15 at s = r).
-__device__ __forceinline__ void panel_subst(double* Cb, long long ldc, const double* Ld, long long ldd,
-                                            const double* Xd, long long ldx, double* lb) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // stage: 36 blocks x 128 16-byte pieces
-  for (int e = tid; e < 36 * 128; e += 256) {
-    const int b = e >> 7, w = e & 127;
-    int bi = 0;
-    while ((bi + 1) * (bi + 2) / 2 <= b) ++bi;
-    const int bk = b - bi * (bi + 1) / 2;
-    const int r = (w & 7) * 2, c = w >> 3;
-    double2 v;
-    if (bi == bk) {
-      v = *reinterpret_cast<const double2*>(Xd + (bi * 16 + r) + (long long)(bk * 16 + c) * ldx);
-    } else {
-      v = *reinterpret_cast<const double2*>(Ld + (bi * 16 + r) + (long long)(bk * 16 + c) * ldd);
-      v.x = -v.x;
-      v.y = -v.y;
-    }
-    *reinterpret_cast<double2*>(lb + b * 256 + r + c * 16) = v;
-  }
-  // C^T blocks of this wave's rows (D layout)
-  d4 pt[8][2];
-  const int row0 = wave * 32 + (lane & 15);
+// panel_subst_c: this wave's C^T blocks into pt -- issued before the flag wait (C is
+// the tile's own update, stored just before by all four waves: the caller has them
+// land first), so they arrive while the factor finishes.
+__device__ __forceinline__ void panel_subst_c(const double* Cb, long long ldc, d4 (&pt)[8][2]) {
+  const int lane = threadIdx.x & 63, row0 = (threadIdx.x >> 6) * 32 + (lane & 15);
 #pragma unroll
   for (int jb = 0; jb < 8; ++jb)
 #pragma unroll
@@ -1243,13 +1224,45 @@ __device__ __forceinline__ void panel_subst(double* Cb, long long ldc, const dou
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         pt[jb][cb][r] = Cb[(row0 + cb * 16) + (long long)(jb * 16 + (lane >> 4) + 4 * r) * ldc];
+}
+
+typedef double dv2 __attribute__((ext_vector_type(2)));
+
+__host__ __device__ constexpr int tri_row(int b) {   // bi of packed lower block b = bi(bi+1)/2 + bk
+  int bi = 0;
+  while ((bi + 1) * (bi + 2) / 2 <= b) ++bi;
+  return bi;
+}
+
+// LDS: L(jb,kb) (kb < jb) and X_jb, block-packed (db_blk) -- 72 KB, the staging space;
+// every thread's 18 16-byte pieces are loaded together (one round trip), then stored.
+__device__ __forceinline__ void panel_subst(double* Cb, long long ldc, const double* Ld, long long ldd,
+                                            const double* Xd, long long ldx, double* lb, d4 (&pt)[8][2]) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  {
+    const int hi = tid >> 7, w = tid & 127, r = (w & 7) * 2, c = w >> 3;
+    dv2 v[18];
+#pragma unroll
+    for (int i = 0; i < 18; ++i) {   // block b = 2i + hi (both candidates fold at compile time)
+      const int bi0 = tri_row(2 * i), bk0 = 2 * i - bi0 * (bi0 + 1) / 2;
+      const int bi1 = tri_row(2 * i + 1), bk1 = 2 * i + 1 - bi1 * (bi1 + 1) / 2;
+      const long long off0 = (bi0 * 16 + r) + (long long)(bk0 * 16 + c) * (bi0 == bk0 ? ldx : ldd);
+      const long long off1 = (bi1 * 16 + r) + (long long)(bk1 * 16 + c) * (bi1 == bk1 ? ldx : ldd);
+      const double* b0 = bi0 == bk0 ? Xd : Ld;
+      const double* b1 = bi1 == bk1 ? Xd : Ld;
+      v[i] = *reinterpret_cast<const dv2*>(hi ? b1 + off1 : b0 + off0);
+    }
+#pragma unroll
+    for (int i = 0; i < 18; ++i) *reinterpret_cast<dv2*>(lb + (2 * i + hi) * 256 + r + c * 16) = v[i];
+  }
   __syncthreads();
+  const int row0 = (tid >> 6) * 32 + (lane & 15);
   const int ao = (lane & 15) + (lane >> 4) * 16;   // A operand (m = lane&15, k = 4s + lane>>4) at ao + 64 s
 #pragma unroll
   for (int jb = 0; jb < 8; ++jb) {
     d4 t0[2], t1[2];
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) { t0[cb] = pt[jb][cb]; t1[cb] = d4{0.0, 0.0, 0.0, 0.0}; }
+    for (int cb = 0; cb < 2; ++cb) { t0[cb] = d4{0.0, 0.0, 0.0, 0.0}; t1[cb] = t0[cb]; }
 #pragma unroll
     for (int kb = 0; kb < jb; ++kb) {
       const double* a = lb + db_blk(jb, kb) + ao;
@@ -1266,7 +1279,7 @@ __device__ __forceinline__ void panel_subst(double* Cb, long long ldc, const dou
     const double* x = lb + db_blk(jb, jb) + ao;
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
-      const d4 t = t0[cb] + t1[cb];
+      const d4 t = pt[jb][cb] - (t0[cb] + t1[cb]);
       d4 o = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int s = 0; s < 4; ++s) o = __builtin_amdgcn_mfma_f64_16x16x4f64(x[64 * s], t[s], o, 0, 0, 0);
@@ -1462,6 +1475,13 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
       if (ti == 0) GTRACE(P, 5);
       gemm_store<false>(Cb, P.ldc, P.alpha, acc);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      d4 pt[8][2];
+      if (P.Ld) {
+        // the C^T rows span every wave's stores: all of them landed, and no stale L1 line
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        panel_subst_c(Cb, P.ldc, pt);
+      }
       int* ready = reinterpret_cast<int*>(lds + G_LDS_LAUNCH_DOUBLES - 1);   // staging is idle here
       if (tid == 0) *ready = gemm_wait_flag(P.flag);
       __syncthreads();
@@ -1474,7 +1494,17 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
       }
       TTRACE(1);   // (panel tiles: [1] = the diagonal inverse seen)
       if (P.Ld) {
-        panel_subst(Cb, P.ldc, P.Ld, P.ldd, P.X, P.ldx, lds);
+#ifdef PANEL_TWICE   // dev probe (wrong results): the substitution cold, then again warm
+        {
+          d4 pt2[8][2];
+#pragma unroll
+          for (int a = 0; a < 8; ++a) pt2[a][0] = pt[a][0], pt2[a][1] = pt[a][1];
+          panel_subst(Cb, P.ldc, P.Ld, P.ldd, P.X, P.ldx, lds, pt2);
+          __syncthreads();
+          if (ti == 0) GTRACE(P, 5);
+        }
+#endif
+        panel_subst(Cb, P.ldc, P.Ld, P.ldd, P.X, P.ldx, lds, pt);
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
