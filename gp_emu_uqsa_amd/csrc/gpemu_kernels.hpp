@@ -1236,8 +1236,10 @@ __host__ __device__ constexpr int tri_row(int b) {   // bi of packed lower block
 
 // LDS: L(jb,kb) (kb < jb) and X_jb, block-packed (db_blk) -- 72 KB, the staging space;
 // every thread's 18 16-byte pieces are loaded together (one round trip), then stored.
+template <class Prob>
 __device__ __forceinline__ void panel_subst(double* Cb, long long ldc, const double* Ld, long long ldd,
-                                            const double* Xd, long long ldx, double* lb, d4 (&pt)[8][2]) {
+                                            const double* Xd, long long ldx, double* lb, d4 (&pt)[8][2],
+                                            const Prob& P, int ti) {
   const int tid = threadIdx.x, lane = tid & 63;
   {
     const int hi = tid >> 7, w = tid & 127, r = (w & 7) * 2, c = w >> 3;
@@ -1256,6 +1258,9 @@ __device__ __forceinline__ void panel_subst(double* Cb, long long ldc, const dou
     for (int i = 0; i < 18; ++i) *reinterpret_cast<dv2*>(lb + (2 * i + hi) * 256 + r + c * 16) = v[i];
   }
   __syncthreads();
+#ifdef PANEL_PHASES   // dev probe: GEMM_TRACE slot 5 = staging done
+  if (ti == 0) GTRACE(P, 5);
+#endif
   const int row0 = (tid >> 6) * 32 + (lane & 15);
   const int ao = (lane & 15) + (lane >> 4) * 16;   // A operand (m = lane&15, k = 4s + lane>>4) at ao + 64 s
 #pragma unroll
@@ -1494,17 +1499,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
       }
       TTRACE(1);   // (panel tiles: [1] = the diagonal inverse seen)
       if (P.Ld) {
-#ifdef PANEL_TWICE   // dev probe (wrong results): the substitution cold, then again warm
-        {
-          d4 pt2[8][2];
-#pragma unroll
-          for (int a = 0; a < 8; ++a) pt2[a][0] = pt[a][0], pt2[a][1] = pt[a][1];
-          panel_subst(Cb, P.ldc, P.Ld, P.ldd, P.X, P.ldx, lds, pt2);
-          __syncthreads();
-          if (ti == 0) GTRACE(P, 5);
-        }
-#endif
-        panel_subst(Cb, P.ldc, P.Ld, P.ldd, P.X, P.ldx, lds, pt);
+        panel_subst(Cb, P.ldc, P.Ld, P.ldd, P.X, P.ldx, lds, pt, P, ti);
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)

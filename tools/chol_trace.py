@@ -31,10 +31,10 @@ for k in range(NB):
     nxt = t[k + 1][0] - max(d3, p3 if p3 > 0 else d3) if k + 1 < NB else 0
     rows.append((k, d1 - d0, d2 - d1, d3 - d2, (p1 - p0) if p0 else 0, (p2 - p1) if p0 else 0,
                  (p3 - p2) if p0 else 0, (p2 - d3) if p0 else 0, nxt, (t[k + 1][0] - d0) if k + 1 < NB else 0))
-if os.environ.get("PANEL_TWICE"):   # libgpemu_trace built with -DPANEL_TWICE: slot 5 = first pass done
+if os.environ.get("PANEL_PHASES"):   # libgpemu_trace built with -DPANEL_PHASES: slot 5 = staged
     first = [t[k][5] - t[k][6] for k in range(NB - 1)]
     second = [t[k][7] - t[k][5] for k in range(NB - 1)]
-    print("panel substitution, first pass %.1f us, second pass %.1f us (mean over steps)"
+    print("panel substitution: staging %.1f us, products + stores %.1f us (mean over steps)"
           % (np.mean(first[1:]), np.mean(second[1:])))
 print(" k   d.upd  d.fac  d.pub  p.upd  p.wait  p.mul  seen-pub  gap   step")
 for r in rows[:3] + rows[60:63] + rows[100:103] + rows[-6:]:
