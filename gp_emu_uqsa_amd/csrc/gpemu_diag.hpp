@@ -43,6 +43,14 @@ __device__ unsigned long long db_tsc[8];
 #define DB_TN(slot) do {} while (0)
 #endif
 
+// global-address-space stores: a FLAT store also counts in lgkmcnt, so the LDS waits
+// after it would wait for the store to land
+typedef double db_v2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void db_gst2(double* p, double x, double y) {
+  *(__attribute__((address_space(1))) db_v2*)(p) = db_v2{x, y};
+}
+__device__ __forceinline__ void db_gst1(double* p, double x) { *(__attribute__((address_space(1))) double*)(p) = x; }
+
 __device__ __forceinline__ int db_off(int i, int k) {   // i >= k
   const int bi = i >> 4, bk = k >> 4;
   return (bi * (bi + 1) / 2 + bk) * 256 + (i & 15) + (k & 15) * 16;
@@ -208,14 +216,14 @@ __device__ __forceinline__ void db_put_block(const double* lb, int off, double* 
     double2 v = *reinterpret_cast<const double2*>(lb + off + r + c * 16);
     double* gp = G + r + (long long)c * ld;
     if (MODE == 1) {
-      if (r >= c) *reinterpret_cast<double2*>(gp) = v;
-      else if (r + 1 == c) gp[1] = v.y;
+      if (r >= c) db_gst2(gp, v.x, v.y);
+      else if (r + 1 == c) db_gst1(gp + 1, v.y);
     } else {
       if (MODE == 2) {
         if (r < c) v.x = 0.0;
         if (r + 1 < c) v.y = 0.0;
       }
-      *reinterpret_cast<double2*>(gp) = v;
+      db_gst2(gp, v.x, v.y);
     }
   }
 }
@@ -259,8 +267,7 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
       const int r = (lane & 7) * 2;
 #pragma unroll
       for (int h = 0; h < 2; ++h)
-        *reinterpret_cast<double2*>(xg_at(bi, bk) + r + (long long)((lane >> 3) + 8 * h) * ldx) =
-            make_double2(0.0, 0.0);
+        db_gst2(xg_at(bi, bk) + r + (long long)((lane >> 3) + 8 * h) * ldx, 0.0, 0.0);
     }
   }
   __syncthreads();
@@ -327,7 +334,7 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
   for (int off = 32; off > 0; off >>= 1) lg += __shfl_down(lg, off, 64);
   if ((tid & 63) == 0) red[tid >> 6] = lg;
   __syncthreads();
-  if (tid == 0) *logdet_out = (red[0] + red[1]) + (red[2] + red[3]);
+  if (tid == 0) db_gst1(logdet_out, (red[0] + red[1]) + (red[2] + red[3]));
   // ---- diagonal blocks -> X leaves (lower part): X(i,c) stored at (c,i), diag in xdiag
   {
     const int jb = tid >> 5, t = tid & 31;          // 8 blocks x 32 threads

@@ -1223,7 +1223,7 @@ __device__ __forceinline__ void panel_subst_c(const double* Cb, long long ldc, d
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        pt[jb][cb][r] = Cb[(row0 + cb * 16) + (long long)(jb * 16 + (lane >> 4) + 4 * r) * ldc];
+        pt[jb][cb][r] = gld1(Cb + (row0 + cb * 16) + (long long)(jb * 16 + (lane >> 4) + 4 * r) * ldc);
 }
 
 typedef double dv2 __attribute__((ext_vector_type(2)));
@@ -1252,7 +1252,7 @@ __device__ __forceinline__ void panel_subst(double* Cb, long long ldc, const dou
       const long long off1 = (bi1 * 16 + r) + (long long)(bk1 * 16 + c) * (bi1 == bk1 ? ldx : ldd);
       const double* b0 = bi0 == bk0 ? Xd : Ld;
       const double* b1 = bi1 == bk1 ? Xd : Ld;
-      v[i] = *reinterpret_cast<const dv2*>(hi ? b1 + off1 : b0 + off0);
+      v[i] = *(__attribute__((address_space(1))) const dv2*)(hi ? b1 + off1 : b0 + off0);
     }
 #pragma unroll
     for (int i = 0; i < 18; ++i) *reinterpret_cast<dv2*>(lb + (2 * i + hi) * 256 + r + c * 16) = v[i];
@@ -1265,32 +1265,41 @@ __device__ __forceinline__ void panel_subst(double* Cb, long long ldc, const dou
   const int ao = (lane & 15) + (lane >> 4) * 16;   // A operand (m = lane&15, k = 4s + lane>>4) at ao + 64 s
 #pragma unroll
   for (int jb = 0; jb < 8; ++jb) {
+    // the step's A operands first, in one batch (row block jb of L, then X_jb): a read
+    // beside each product would put an LDS round trip in front of every MFMA
+    double av[8][4], xv[4];
+    const double* arow = lb + db_blk(jb, 0) + ao;   // blocks (jb, 0 .. jb) are contiguous
+#pragma unroll
+    for (int kb = 0; kb < jb; ++kb)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) av[kb][s] = arow[kb * 256 + 64 * s];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) xv[s] = arow[jb * 256 + 64 * s];
     d4 t0[2], t1[2];
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) { t0[cb] = d4{0.0, 0.0, 0.0, 0.0}; t1[cb] = t0[cb]; }
 #pragma unroll
     for (int kb = 0; kb < jb; ++kb) {
-      const double* a = lb + db_blk(jb, kb) + ao;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const double av = a[64 * s];
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
-          if (kb & 1) t1[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, pt[kb][cb][s], t1[cb], 0, 0, 0);
-          else t0[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, pt[kb][cb][s], t0[cb], 0, 0, 0);
+          if (kb & 1) t1[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kb][s], pt[kb][cb][s], t1[cb], 0, 0, 0);
+          else t0[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kb][s], pt[kb][cb][s], t0[cb], 0, 0, 0);
         }
       }
     }
-    const double* x = lb + db_blk(jb, jb) + ao;
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
       const d4 t = pt[jb][cb] - (t0[cb] + t1[cb]);
       d4 o = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) o = __builtin_amdgcn_mfma_f64_16x16x4f64(x[64 * s], t[s], o, 0, 0, 0);
+      for (int s = 0; s < 4; ++s) o = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[s], t[s], o, 0, 0, 0);
       pt[jb][cb] = o;
+      // global stores: a FLAT store also counts in lgkmcnt, and the next step's LDS
+      // wait would wait for it to land
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Cb[(row0 + cb * 16) + (long long)(jb * 16 + (lane >> 4) + 4 * r) * ldc] = o[r];
+      for (int r = 0; r < 4; ++r) gst1(Cb + (row0 + cb * 16) + (long long)(jb * 16 + (lane >> 4) + 4 * r) * ldc, o[r]);
     }
   }
 }
