@@ -41,34 +41,20 @@ struct Launch {       // one grouped GEMM launch of the cached schedule
   double flops;       // algorithmic flops
   long long list = -1;  // offset of its tile list in the device list array (-1: implicit order)
   bool cdef = false;    // k_gemm's CDEF instance (gemm_cdef of some problem)
+  int* ticket = nullptr;  // fused Cholesky launches: list positions claimed by ticket (k_gemm)
 };
 
 struct Plan {
   long long n_pad = 0;
   const double* a_ptr = nullptr;   // buffers the descriptors point into
   const double* b_ptr = nullptr;
-  // potrf with depth-1 look-ahead: per step kt the panel launch, the update of
-  // column block kt+1 (critical path) and the rest of the trailing update
-  std::vector<int> panel, colupd, rest;
-  // fused schedule (default): one launch per column block (see build_plan); fused_aug:
-  // the same launches also carrying the augmented row (when the workspace has one)
+  // fused schedule: one launch per column block (see build_plan); fused_aug: the same
+  // launches also carrying the augmented row (when the workspace has one)
   std::vector<int> fused, fused_aug;
   std::vector<int> trtri;   // launches in order
-  // the same triangular inverse split for the overlapped tail (potrf_overlap): the pairs
-  // inside the leading block [0, split) (their L is final once the Cholesky reaches the
-  // tail), then the rest; split = 0: not built
-  int split = 0;
-  std::vector<int> trtri_lead, trtri_rest;
   int lauum = -1;
   bool aug = false;         // fused_aug is built
-  // two-stream group schedule (potrf_g2s, GPEMU_POTRF=g2s): for groups of width >= 2 a
-  // chain launch per step (diagonal, panels, the next column's update) and ONE trailing-
-  // update launch per group on the other stream; width-1 groups run their fused launches
-  bool g2s = false;
-  std::vector<int> g2s_gs;                    // group starts, then NB
-  std::vector<int> g2s_step, g2s_step_aug;    // per step: launch index
-  std::vector<int> g2s_bulk, g2s_bulk_aug;    // per group: trailing-update launch, or -1
-  // group schedule (GPEMU_POTRF=group): ONE launch per column group of width >= 2 holding
+  // group schedule (the default for a lone evaluation): ONE launch per column group of width >= 2 holding
   // its whole chain (diagonal and panel tiles of every step, handed on by counters in
   // F.flags) beside the previous group's trailing update; width-1 groups as fused.  Per
   // step: the launch to issue, -1 for the later steps of a group
@@ -78,6 +64,10 @@ struct Plan {
   std::vector<unsigned> tiles;   // concatenated tile lists
 };
 
+// F.flags: NB ints each of the diagonal-inverse flags, the group schedule's column and
+// panel counters, and the list tickets of the Cholesky launches (one per column step)
+constexpr int FACT_FLAG_INTS = 4;
+
 // A factorisation workspace: two n_pad x n_pad buffers and their GEMM schedule.
 struct Fact {
   long long n_pad = 0;
@@ -86,8 +76,8 @@ struct Fact {
   double* B = nullptr;   // Dinv tiles -> L^-1 (strictly-upper tiles: scratch)
   size_t cap = 0;
   double* logdet = nullptr;  // NB per-block log-determinant parts
-  int* flags = nullptr;      // NB diagonal-inverse ready flags (fused Cholesky)
-  int* tflags = nullptr;     // row counter of the forward substitution (k_trsv_lower)
+  int* flags = nullptr;      // FACT_FLAG_INTS x NB: flags, counters, tickets (fused Cholesky)
+  int* tflags = nullptr;     // row counter and row ticket of the forward substitution (k_trsv_lower)
   // augmented tile row ([f H]^T under the matrix, TILE x n_pad, ld TILE): carried by the
   // fused Cholesky's panels and trailing updates, it ends as (L^-1 [f H])^T (training
   // workspace only)
@@ -185,12 +175,6 @@ struct gpe_ctx {
   std::vector<double> f_delta;
   double f_nu = 0.0;
 
-  // A/B switch: GPEMU_DIAG=rows selects the register-blocked diagonal kernel
-  bool diag_rows = false;
-  // A/B switch: GPEMU_POTRF=lookahead selects the two-stream look-ahead schedule
-  // with the standalone diagonal kernel instead of the fused one
-  bool potrf_lookahead = false;
-  bool potrf_g2s = false;   // GPEMU_POTRF=g2s: the two-stream group schedule (potrf_g2s)
   // GPEMU_POTRF=group: one launch per column group (Plan::grp); list positions of the
   // chain steps (GPEMU_GROUP_P0, GPEMU_GROUP_STRIDE)
   bool potrf_group = true;    // the group launches are built (Plan::grp)
@@ -200,37 +184,15 @@ struct gpe_ctx {
   // 1 always group (GPEMU_POTRF=group), 2 always per step (GPEMU_POTRF=fused)
   int potrf_mode = 0;
   int grp_p0 = 512, grp_stride = 896;
-  std::vector<hipEvent_t> ev_gbulk, ev_gchain;
-  bool skinny_valu = false;   // GPEMU_SKINNY=valu: the VALU skinny kernels (A/B)
-  bool kpairs_shfl = false;   // GPEMU_KPAIRS=shuffle: the lane-shuffle d-reduction K-build (A/B)
   // column-group widths of the fused Cholesky: {width, min remaining columns}, first
   // match wins, else 1 (GPEMU_POTRF_W="4:64,2:32" style)
   std::vector<std::pair<int, int>> potrf_groups = {{4, 80}, {2, 40}};
-  int chol_prio = 1;   // fused Cholesky (1), and the TRTRI levels (2), on the high-priority stream
-  int potrf_first = 0;   // width of the first column group (0: as potrf_groups)
-  // panel tiles of the fused Cholesky by block substitution with L and X's diagonal
-  // blocks, released before the diagonal workgroup assembles the rest of X (default);
-  // GPEMU_PANEL=xmul: multiply by the whole X = L^-1, released after it (A/B)
-  bool panel_trsm = true;
-
-  // overlapped Cholesky tail (potrf_trtri_overlap): the width-1 tail steps on one half of
-  // the CUs, the triangular inverse of the leading block on the other half (CU-masked
-  // streams, created on first use).  A/B switch GPEMU_TAIL_OVERLAP=1; off by default: it
-  // measured slower
-  bool tail_overlap = false;
-  // GPEMU_TAIL_OVERLAP=2: the leading block's inverse on a plain second stream (no CU
-  // mask) from Cholesky step tail_split on (GPEMU_TAIL_SPLIT, default 64), the Cholesky
-  // staying on the context stream: the bulk-bound middle of the sweep absorbs it
-  int tail_mode = 0, tail_split = 64;
-  hipStream_t st_plain = nullptr;
-  bool tail_streams_ok = false, tail_streams_tried = false;
-  hipStream_t st_tail = nullptr, st_fill = nullptr;
-  hipEvent_t ev_split = nullptr, ev_tail = nullptr, ev_fill = nullptr;
-  // look-ahead stream and events
-  hipStream_t stream2 = nullptr;
+  // the fused Cholesky on the context's high-priority stream (default 1; 0: on the
+  // context stream, GPEMU_CHOL_PRIO=0)
+  int chol_prio = 1;
+  hipStream_t stream2 = nullptr;   // the high-priority stream
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_host = nullptr;   // host-visible results of the value part are in hpin
-  std::vector<hipEvent_t> ev_panel, ev_rest;
 
   // profiling
   bool prof = false;
@@ -282,17 +244,22 @@ int dalloc(gpe_ctx* c, T** p, size_t count) {
 // the per-dimension and per-basis-column device buffers, grown to the shape in use: the
 // reference takes any d and any basis (_emulatorkernels.py:39-50), and so does the library
 // (d > 32 and P > 33 run the LDS-staged wide kernels)
+// (each cap is zeroed before its reallocation: a failed dalloc leaves the buffer NULL, and
+// the next call must not find the old, larger cap and skip it)
 int ensure_shape_bufs(gpe_ctx* c, int d, int P) {
   if ((size_t)d > c->invd_cap) {
+    c->invd_cap = 0;
     CHK(dalloc(c, &c->dinvdelta, (size_t)d));
     c->invd_cap = (size_t)d;
   }
   if ((size_t)d + 3 > c->csum_cap) {
+    c->csum_cap = 0;
     CHK(dalloc(c, &c->dcsum, (size_t)d + 3));
     c->csum_cap = (size_t)d + 3;
   }
   const size_t pp = (size_t)P * P;
   if (pp > c->gram_cap) {
+    c->gram_cap = 0;
     CHK(dalloc(c, &c->dgram, pp));
     CHK(dalloc(c, &c->dT2, pp));
     c->gram_cap = pp;
@@ -312,12 +279,11 @@ int ensure_pinned(gpe_ctx* c, size_t doubles) {
 
 int ensure_small(gpe_ctx* c, size_t doubles) {
   if (doubles <= c->small_cap) return GPE_OK;
+  c->small_cap = 0;
   CHK(dalloc(c, &c->dsmall, doubles));
   c->small_cap = doubles;
   return GPE_OK;
 }
-
-inline int pmax_bucket(int P) { return P <= 8 ? 8 : (P <= 16 ? 16 : 32); }
 
 // ------------------------------------------------------------------ launches
 int launch_pairs(gpe_ctx* c, const PairArgs& a, int nblocks) {
@@ -366,19 +332,19 @@ int launch_gemm_range(gpe_ctx* c, const Launch& L, hipStream_t st = nullptr) {
   const dim3 g(L.tiles), b(256);
   if (L.cdef) {
     switch (L.kind) {
-      case 0: hipLaunchKernelGGL((k_gemm<false, false, false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
-      case 1: hipLaunchKernelGGL((k_gemm<true, false, false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
-      case 2: hipLaunchKernelGGL((k_gemm<true, true, false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
-      case 3: hipLaunchKernelGGL((k_gemm<false, true, false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
-      default: hipLaunchKernelGGL((k_gemm<false, false, true, true>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
+      case 0: hipLaunchKernelGGL((k_gemm<false, false, false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo, L.ticket); break;
+      case 1: hipLaunchKernelGGL((k_gemm<true, false, false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo, L.ticket); break;
+      case 2: hipLaunchKernelGGL((k_gemm<true, true, false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo, L.ticket); break;
+      case 3: hipLaunchKernelGGL((k_gemm<false, true, false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo, L.ticket); break;
+      default: hipLaunchKernelGGL((k_gemm<false, false, true, true>), g, b, lds, st, pr, L.count, tl, c->dinfo, L.ticket); break;
     }
   } else {
     switch (L.kind) {
-      case 0: hipLaunchKernelGGL((k_gemm<false, false>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
-      case 1: hipLaunchKernelGGL((k_gemm<true, false>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
-      case 2: hipLaunchKernelGGL((k_gemm<true, true>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
-      case 3: hipLaunchKernelGGL((k_gemm<false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
-      default: hipLaunchKernelGGL((k_gemm<false, false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo); break;
+      case 0: hipLaunchKernelGGL((k_gemm<false, false>), g, b, lds, st, pr, L.count, tl, c->dinfo, L.ticket); break;
+      case 1: hipLaunchKernelGGL((k_gemm<true, false>), g, b, lds, st, pr, L.count, tl, c->dinfo, L.ticket); break;
+      case 2: hipLaunchKernelGGL((k_gemm<true, true>), g, b, lds, st, pr, L.count, tl, c->dinfo, L.ticket); break;
+      case 3: hipLaunchKernelGGL((k_gemm<false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo, L.ticket); break;
+      default: hipLaunchKernelGGL((k_gemm<false, false, true>), g, b, lds, st, pr, L.count, tl, c->dinfo, L.ticket); break;
     }
   }
   HIPCHK(c, hipGetLastError());
@@ -562,13 +528,10 @@ int build_plan(gpe_ctx* c, Fact& F) {
   auto tile = [&](double* M, int i, int j) { return M + (long long)i * TILE + (long long)j * TILE * ld; };
   // tile (0, j) of the augmented row (ld TILE); the fused schedule is built without it
   // and, when the workspace has one, a second time with it (aug in the lambdas below)
-  pl.aug = F.aug && F.Faug && !c->potrf_lookahead;
+  pl.aug = F.aug && F.Faug;
   bool aug = false;
   auto atile = [&](int j) { return F.Faug + (long long)j * TILE * TILE; };
   // --- Cholesky (right-looking, 128-column steps)
-  pl.panel.assign(NB, -1);
-  pl.colupd.assign(NB, -1);
-  pl.rest.assign(NB, -1);
   pl.fused.assign(NB, -1);
   pl.fused_aug.assign(NB, -1);
   // Fused schedule, one launch per column block t.  Columns are grouped (widths from
@@ -588,7 +551,8 @@ int build_plan(gpe_ctx* c, Fact& F) {
     p.logdet = F.logdet + t;
     p.diag_col0 = t * TILE;
     p.flag = F.flags + t;
-    if (c->panel_trsm) { p.Ld = tile(A, t, t); p.ldd = ld; }
+    p.Ld = tile(A, t, t);
+    p.ldd = ld;
     return p;
   };
   auto panelprob = [&](int t, const double* Lp, const double* Lt, int K, double alpha) {
@@ -597,7 +561,20 @@ int build_plan(gpe_ctx* c, Fact& F) {
     p.ldx = ld;
     p.flag = F.flags + t;
     p.diag_col0 = t * TILE;   // step index for the GEMM_TRACE dev build
-    if (c->panel_trsm) { p.Ld = tile(A, t, t); p.ldd = ld; }
+    p.Ld = tile(A, t, t);
+    p.ldd = ld;
+    return p;
+  };
+  // the augmented row's panel tile (aug, t): pending columns [p0, t), then x L_tt^-T
+  auto augpanel = [&](int t, int p0, int K, double alpha) {
+    GemmProb p = mkprob(K ? atile(p0) : nullptr, TILE, K ? tile(A, t, p0) : nullptr, ld, atile(t), TILE, 1, 1, K,
+                        G_PANEL, alpha, 1.0);
+    p.X = tile(B, t, t);
+    p.ldx = ld;
+    p.flag = F.flags + t;
+    p.Ld = tile(A, t, t);
+    p.ldd = ld;
+    p.diag_col0 = -TILE;   // (no GEMM_TRACE slot)
     return p;
   };
   // bulk problems: tiles (i, j), i >= j, j in [a, b), updated by columns [g0, g0 + K/128);
@@ -620,16 +597,13 @@ int build_plan(gpe_ctx* c, Fact& F) {
     int w = 1;
     for (const auto& r : c->potrf_groups)
       if (NB - g > r.second) { w = r.first; break; }
-    // the first group has no trailing update to carry (nothing precedes it): a narrower
-    // first group starts the first update sooner (GPEMU_POTRF_FIRST)
-    if (g == 0 && c->potrf_first > 0) w = c->potrf_first;
     g += std::max(1, std::min(w, NB - g));
   }
   gs.push_back(NB);
   for (int va = 0; va < (pl.aug ? 2 : 1); ++va) {
   aug = va == 1;
   std::vector<int>& fidx = aug ? pl.fused_aug : pl.fused;
-  for (int gi = 0; gi + 1 < (int)gs.size() && !c->potrf_lookahead; ++gi) {
+  for (int gi = 0; gi + 1 < (int)gs.size(); ++gi) {
     const int gb = gs[gi], ge = gs[gi + 1], W1 = ge - gb;
     // previous group's bulk: columns [gb+1, NB) split into W1 parts
     std::vector<std::pair<int, int>> rng(W1, {0, 0});   // share of [ge, NB) per part
@@ -662,16 +636,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
         fp.push_back(panelprob(t, K ? tile(A, t + 1, p0) : nullptr, K ? tile(A, t, p0) : nullptr, K, al));
         fl += 2.0 * m * T * T * K + (double)m * T * T * T;
       }
-      if (aug) {   // the augmented row's panel tile (aug, t): pending columns, then x X_t^T
-        GemmProb pa = mkprob(K ? atile(p0) : nullptr, TILE, K ? tile(A, t, p0) : nullptr, ld, atile(t), TILE,
-                             1, 1, K, G_PANEL, al, 1.0);
-        pa.X = tile(B, t, t);
-        pa.ldx = ld;
-        pa.flag = F.flags + t;
-        if (c->panel_trsm) { pa.Ld = tile(A, t, t); pa.ldd = ld; }
-        pa.diag_col0 = -TILE;   // (no GEMM_TRACE slot)
-        fp.push_back(pa);
-      }
+      if (aug) fp.push_back(augpanel(t, p0, K, al));
       if (gi > 0) {
         const int g0 = gs[gi - 1], Kb = (gb - g0) * TILE;
         if (h + 1 < W1) bulk(fp, fl, t + 1, t + 2, g0, Kb);   // the column factored next
@@ -679,6 +644,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
       }
       fidx[t] = (int)pl.launches.size();
       add_launch(pl, 4, fp, fl);
+      pl.launches.back().ticket = F.flags + 3 * NB + t;
     }
   }
   // the group schedule: one launch per group of width >= 2.  Its tile list (= dispatch
@@ -689,7 +655,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
   // grp_p0 + h grp_stride (step 0's first panel at 256: workgroup 0's CU partner).
   // Step h >= 1 waits for step h-1's panels and its column's update, so every wait points
   // to earlier tiles; one drain per group instead of one per step.
-  if (c->potrf_group && !c->potrf_lookahead) {
+  if (c->potrf_group) {
     std::vector<int>& gidx = aug ? pl.grp_aug : pl.grp;
     gidx.assign(NB, -1);
     int* cnt_col = F.flags + NB;
@@ -753,13 +719,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
           fl += 2.0 * m * T * T * K + (double)m * T * T * T;
         }
         if (aug) {
-          GemmProb pa = mkprob(K ? atile(p0) : nullptr, TILE, K ? tile(A, t, p0) : nullptr, ld, atile(t), TILE,
-                               1, 1, K, G_PANEL, al, 1.0);
-          pa.X = tile(B, t, t);
-          pa.ldx = ld;
-          pa.flag = F.flags + t;
-        if (c->panel_trsm) { pa.Ld = tile(A, t, t); pa.ldd = ld; }
-          pa.diag_col0 = -TILE;
+          GemmProb pa = augpanel(t, p0, K, al);
           wire(pa);
           pa.post = cnt_pan + t;
           fp.push_back(pa);
@@ -832,86 +792,11 @@ int build_plan(gpe_ctx* c, Fact& F) {
       }
       gidx[gb] = (int)pl.launches.size();
       add_launch_list(pl, 4, fp, fl, order);
-    }
-  }
-  // the two-stream group schedule: the same chain tiles without the trailing-update
-  // shares, which form one plain launch per group (columns [ge, NB) by the previous group)
-  if (c->potrf_g2s && !c->potrf_lookahead) {
-    pl.g2s = true;
-    pl.g2s_gs = gs;
-    std::vector<int>& sidx = aug ? pl.g2s_step_aug : pl.g2s_step;
-    std::vector<int>& bidx = aug ? pl.g2s_bulk_aug : pl.g2s_bulk;
-    sidx.assign(NB, -1);
-    bidx.assign(gs.size(), -1);
-    for (int gi = 0; gi + 1 < (int)gs.size(); ++gi) {
-      const int gb = gs[gi], ge = gs[gi + 1], W1 = ge - gb;
-      if (W1 < 2) {   // width 1: the fused launch as it is (its own trailing update)
-        sidx[gb] = fidx[gb];
-        continue;
-      }
-      for (int h = 0; h < W1; ++h) {
-        const int t = gb + h;
-        const int p0 = (h == 0) ? (gi > 0 ? gs[gi - 1] : 0) : gb;
-        const int K = (t - p0) * TILE;
-        const double al = K ? -1.0 : 1.0;
-        const int m = NB - t - 1;
-        std::vector<GemmProb> fp = {diagprob(t, K ? tile(A, t, p0) : nullptr, K, al)};
-        double fl = T * (T + 1.0) * K;
-        if (m >= 1) {
-          fp.push_back(panelprob(t, K ? tile(A, t + 1, p0) : nullptr, K ? tile(A, t, p0) : nullptr, K, al));
-          fl += 2.0 * m * T * T * K + (double)m * T * T * T;
-        }
-        if (aug) {
-          GemmProb pa = mkprob(K ? atile(p0) : nullptr, TILE, K ? tile(A, t, p0) : nullptr, ld, atile(t), TILE,
-                               1, 1, K, G_PANEL, al, 1.0);
-          pa.X = tile(B, t, t);
-          pa.ldx = ld;
-          pa.flag = F.flags + t;
-        if (c->panel_trsm) { pa.Ld = tile(A, t, t); pa.ldd = ld; }
-          pa.diag_col0 = -TILE;
-          fp.push_back(pa);
-        }
-        if (gi > 0 && h + 1 < W1) bulk(fp, fl, t + 1, t + 2, gs[gi - 1], (gb - gs[gi - 1]) * TILE);
-        sidx[t] = (int)pl.launches.size();
-        add_launch(pl, 4, fp, fl);
-      }
-      if (gi > 0 && ge < NB) {
-        std::vector<GemmProb> fp;
-        double fl = 0.0;
-        bulk(fp, fl, ge, NB, gs[gi - 1], (gb - gs[gi - 1]) * TILE);
-        bidx[gi] = (int)pl.launches.size();
-        add_launch(pl, 0, fp, fl);
-      }
+      pl.launches.back().ticket = F.flags + 3 * NB + gb;
     }
   }
   }
-  for (int kt = 0; kt + 1 < NB; ++kt) {
-    if (!c->potrf_lookahead) break;
-    const int m = NB - kt - 1;
-    // L(kt+1:, kt) = A(kt+1:, kt) * Dinv_kt^T     (opB(k,n) = Dinv(n,k): N-contiguous)
-    pl.panel[kt] = (int)pl.launches.size();
-    add_launch(pl, 0,
-               {mkprob(tile(A, kt + 1, kt), ld, tile(B, kt, kt), ld, tile(A, kt + 1, kt), ld, m, 1,
-                       TILE, 0, 1.0, 0.0)},
-               (double)m * T * T * T);
-    // column block kt+1: A(kt+1:, kt+1) -= L(kt+1:, kt) L(kt+1, kt)^T
-    pl.colupd[kt] = (int)pl.launches.size();
-    add_launch(pl, 0,
-               {mkprob(tile(A, kt + 1, kt), ld, tile(A, kt + 1, kt), ld, tile(A, kt + 1, kt + 1), ld,
-                       m, 1, TILE, 0, -1.0, 1.0)},
-               (double)m * T * T * T * 2.0 - T * T * T);
-    // the rest: A(kt+2:, kt+2:) -= L(kt+2:, kt) L(kt+2:, kt)^T   (lower tiles)
-    if (m >= 2) {
-      pl.rest[kt] = (int)pl.launches.size();
-      add_launch(pl, 0,
-                 {mkprob(tile(A, kt + 2, kt), ld, tile(A, kt + 2, kt), ld, tile(A, kt + 2, kt + 2), ld,
-                         m - 1, m - 1, TILE, G_CLOWER, -1.0, 1.0)},
-                 (double)(m - 1) * T * ((double)(m - 1) * T + 1.0) * T);
-    }
-  }
-  // --- triangular inverse X = L^-1 in B (diagonal tiles already hold Dinv); sel: 0 all
-  // pairs, 1 the pairs inside [0, split), 2 the others
-  auto build_trtri = [&](int sel, int split, std::vector<int>& out) {
+  // --- triangular inverse X = L^-1 in B (diagonal tiles already hold Dinv)
   for (int s = 2; s / 2 < NB; s *= 2) {
     std::vector<GemmProb> pa, pb;
     double fa = 0.0, fb = 0.0;
@@ -919,8 +804,6 @@ int build_plan(gpe_ctx* c, Fact& F) {
       const int h = t0 + s / 2;
       if (h >= NB) continue;
       const int t1 = std::min(t0 + s, NB);
-      if (sel == 1 && t1 > split) continue;
-      if (sel == 2 && t1 <= split) continue;
       const int a = h - t0, b = t1 - h;
       // T^T (a x b tiles, stored in the upper block rows t0:h, cols h:t1 of B)
       //   = X11^T L21^T ;  opA(m,k) = X11(k,m): K-contiguous, upper -> kbeg = ti*128
@@ -933,27 +816,10 @@ int build_plan(gpe_ctx* c, Fact& F) {
       fb += (double)b * T * b * T * a * T;
     }
     if (pa.empty()) continue;
-    out.push_back((int)pl.launches.size());
+    pl.trtri.push_back((int)pl.launches.size());
     add_launch(pl, 1, pa, fa);
-    out.push_back((int)pl.launches.size());
+    pl.trtri.push_back((int)pl.launches.size());
     add_launch(pl, 0, pb, fb);
-  }
-  };
-  build_trtri(0, 0, pl.trtri);
-  // the overlapped tail: the width-1 steps of the fused Cholesky (the chain-bound end)
-  if (!c->potrf_lookahead && F.aug && NB >= 64) {
-    int split = 0;
-    if (c->tail_mode == 2) {
-      split = std::min(c->tail_split, NB - 1);
-    } else {
-      for (size_t gi = 0; gi + 1 < gs.size(); ++gi)
-        if (gs[gi + 1] - gs[gi] == 1) { split = gs[gi]; break; }
-    }
-    if (split >= 16 && split < NB) {
-      pl.split = split;
-      build_trtri(1, split, pl.trtri_lead);
-      build_trtri(2, split, pl.trtri_rest);
-    }
   }
   // --- A^-1 = X^T X (lower tiles), written over L in A
   pl.lauum = (int)pl.launches.size();
@@ -972,6 +838,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
   const size_t need = 2 * half;
   if (need > c->tiles_cap) {
     // growing invalidates the other plan's uploaded lists: force its rebuild
+    c->tiles_cap = 0;
     CHK(dalloc(c, &c->dtiles, need));
     c->tiles_cap = need;
     Fact& other = (&F == &c->tr) ? c->aux : c->tr;
@@ -1002,8 +869,8 @@ int ensure_fact(gpe_ctx* c, Fact& F, long long n_pad) {
     F.n_pad = n_pad;
     F.NB = (int)(n_pad / TILE);
     CHK(dalloc(c, &F.logdet, (size_t)F.NB));
-    CHK(dalloc(c, &F.flags, 3 * (size_t)F.NB));   // diagonal flags, then the group schedule's counters
-    CHK(dalloc(c, &F.tflags, (size_t)F.NB));
+    CHK(dalloc(c, &F.flags, FACT_FLAG_INTS * (size_t)F.NB));
+    CHK(dalloc(c, &F.tflags, 2));   // k_trsv_lower: row counter, list ticket
     if (F.aug) CHK(dalloc(c, &F.Faug, (size_t)n_pad * TILE));
     F.plan = Plan();
   }
@@ -1049,227 +916,54 @@ int kbuild(gpe_ctx* c, int kernel, double nu, double s2, double rscale) {
   kernel_consts(kernel, nu, true, &coff, &cdiag);
   a.s2 = s2; a.coff = coff; a.cdiag = cdiag;
   a.rscale = rscale; a.r = (c->has_r && rscale != 0.0) ? c->dr : nullptr;
-  if (c->kpairs_shfl && a.d <= 32) {   // A/B: the d-reduction as a lane-shuffle tree
-    const dim3 g(c->NB * (c->NB + 1) / 2), b(256);
-    if (a.d <= 8) hipLaunchKernelGGL(k_pairs_shfl<8>, g, b, 0, c->stream, a);
-    else if (a.d <= 16) hipLaunchKernelGGL(k_pairs_shfl<16>, g, b, 0, c->stream, a);
-    else hipLaunchKernelGGL(k_pairs_shfl<32>, g, b, 0, c->stream, a);
-    HIPCHK(c, hipGetLastError());
-    return GPE_OK;
-  }
   return launch_pairs(c, a, c->NB * (c->NB + 1) / 2);
 }
 
-// Right-looking blocked Cholesky with depth-1 look-ahead on two streams.
-//   aux  : wait rest(k-2) | diag(k) | panel(k) | rec ev_panel[k] | wait rest(k-1) | colupd(k)
-//   main : wait ev_panel[k] | rest(k) | rec ev_rest[k]
-// diag/panel/colupd of the next step run while the big trailing update runs.
+// Right-looking blocked Cholesky, fused: one launch per column step (or per column group,
+// Plan::grp); the diagonal tile of each step is factored by the first workgroup of its
+// launch and the step's panel tiles follow in-launch (build_plan).
 // Every launcher of a workspace's schedule first makes sure it is built: growing the
 // tile-list array for one workspace's plan resets the other's (build_plan), e.g. the
 // aux plan of gpe_noise_sample between gpe_factor and a later on-demand TRTRI / LAUUM.
-// Two-stream group schedule.  Groups of width >= 2: the chain launches of group g (their
-// diagonal factorisations, panels and the next column's update) on the high-priority
-// stream2 and, beside them on the context stream, ONE launch updating the columns beyond
-// g by group g - 1: its tiles no longer drain at every step's launch boundary.  B(g) waits
-// for the chain of g - 1 (its panels); the chain of g + 1 waits for B(g) (its columns'
-// update by g - 1).  Width-1 groups (the chain-bound tail) run their fused launches on the
-// context stream after the join.  Writes are disjoint: B(g) touches columns >= end(g), the
-// chain of g only the columns of g.
-int potrf_g2s(gpe_ctx* c, Fact& F, bool with_aug) {
-  const Plan& pl = F.plan;
-  const int NB = F.NB;
-  const std::vector<int>& gs = pl.g2s_gs;
-  const std::vector<int>& sidx = with_aug ? pl.g2s_step_aug : pl.g2s_step;
-  const std::vector<int>& bidx = with_aug ? pl.g2s_bulk_aug : pl.g2s_bulk;
-  const int ng = (int)gs.size() - 1;
-  if ((int)c->ev_gbulk.size() < ng) {
-    for (auto& e : c->ev_gbulk) (void)hipEventDestroy(e);
-    for (auto& e : c->ev_gchain) (void)hipEventDestroy(e);
-    c->ev_gbulk.assign(ng, nullptr);
-    c->ev_gchain.assign(ng, nullptr);
-    for (int i = 0; i < ng; ++i) {
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_gbulk[i], hipEventDisableTiming));
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_gchain[i], hipEventDisableTiming));
-    }
-  }
-  hipStream_t mainst = c->stream, chain = c->stream2;
-  HIPCHK(c, hipMemsetAsync(F.flags, 0, 3 * (size_t)NB * sizeof(int), mainst));
-  HIPCHK(c, hipEventRecord(c->ev_fork, mainst));
-  HIPCHK(c, hipStreamWaitEvent(chain, c->ev_fork, 0));
-  int last_two = -1;   // the last group of width >= 2 so far
-  for (int gi = 0; gi < ng; ++gi) {
-    const int gb = gs[gi], ge = gs[gi + 1];
-    if (ge - gb >= 2) {
-      if (bidx[gi] >= 0) {
-        HIPCHK(c, hipStreamWaitEvent(mainst, c->ev_gchain[gi - 1], 0));
-        CHK(launch_gemm_range(c, pl.launches[bidx[gi]], mainst));
-        HIPCHK(c, hipEventRecord(c->ev_gbulk[gi], mainst));
-      }
-      if (gi > 0 && bidx[gi - 1] >= 0) HIPCHK(c, hipStreamWaitEvent(chain, c->ev_gbulk[gi - 1], 0));
-      for (int t = gb; t < ge; ++t) CHK(launch_gemm_range(c, pl.launches[sidx[t]], chain));
-      HIPCHK(c, hipEventRecord(c->ev_gchain[gi], chain));
-      last_two = gi;
-    } else {
-      if (last_two == gi - 1 && last_two >= 0)   // join: the tail runs on the context stream
-        HIPCHK(c, hipStreamWaitEvent(mainst, c->ev_gchain[last_two], 0));
-      CHK(launch_gemm_range(c, pl.launches[sidx[gb]], mainst));
-    }
-  }
-  if (last_two == ng - 1) HIPCHK(c, hipStreamWaitEvent(mainst, c->ev_gchain[last_two], 0));
-  return GPE_OK;
-}
-
 int potrf(gpe_ctx* c, Fact& F, bool with_aug = false) {
   CHK(build_plan(c, F));
   const Plan& pl = F.plan;
   const int NB = F.NB;
-  if (pl.g2s) return potrf_g2s(c, F, with_aug && pl.aug);
-  if (!c->potrf_lookahead) {
-    // fused: one launch per step; the diagonal tile kt+1 is factored by the first
-    // workgroup of the trailing-update launch kt and its panel follows in-launch
-    HIPCHK(c, hipMemsetAsync(F.flags, 0, 3 * (size_t)NB * sizeof(int), c->stream));
-    const bool wa = with_aug && pl.aug;
-    const bool grp = c->potrf_group &&
-                     (c->potrf_mode == 1 || (c->potrf_mode == 0 && g_inflight[c->device & 63].load() <= 1));
-    const std::vector<int>& fidx = grp ? (wa ? pl.grp_aug : pl.grp) : (wa ? pl.fused_aug : pl.fused);
-    if (c->chol_prio) {
-      // the whole sweep on the context's high-priority stream: with two tries in flight
-      // its chain workgroups are dispatched ahead of the other try's inverse tiles
-      HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
-      HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
-      for (int t = 0; t < NB; ++t)
-        if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]], c->stream2));
-      HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
-      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
-      return GPE_OK;
-    }
-#ifdef GEMM_TTRACE
-    if (const char* es = std::getenv("GPEMU_DEBUG_STOP_STEP")) {
-      const int stop = std::atoi(es);
-      // back to back as in the sweep, every launch traced (the host resets the count)
-      for (int t = 0; t <= stop && t < NB; ++t)
-        if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]]));
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      return fail(c, GPE_ERR_STATE, "debug stop after Cholesky launch " + std::to_string(stop));
-    }
-#endif
-    for (int t = 0; t < NB; ++t)
-      if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]]));
-    return GPE_OK;
-  }
-  if ((int)c->ev_panel.size() < NB) {
-    for (auto& e : c->ev_panel) (void)hipEventDestroy(e);
-    for (auto& e : c->ev_rest) (void)hipEventDestroy(e);
-    c->ev_panel.assign(NB, nullptr);
-    c->ev_rest.assign(NB, nullptr);
-    for (int i = 0; i < NB; ++i) {
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_panel[i], hipEventDisableTiming));
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_rest[i], hipEventDisableTiming));
-    }
-  }
-  hipStream_t aux = c->stream2, mainst = c->stream;
-  HIPCHK(c, hipEventRecord(c->ev_fork, mainst));
-  HIPCHK(c, hipStreamWaitEvent(aux, c->ev_fork, 0));
-  for (int kt = 0; kt < NB; ++kt) {
-    if (kt >= 2 && pl.rest[kt - 2] >= 0) HIPCHK(c, hipStreamWaitEvent(aux, c->ev_rest[kt - 2], 0));
-    if (c->diag_rows)
-      hipLaunchKernelGGL(k_potrf_diag_rows, dim3(1), dim3(DIAG_ROWS_THREADS), 0, aux, F.A,
-                         (long long)F.n_pad, kt, F.B, (long long)F.n_pad, F.logdet, c->dinfo);
-    else
-      hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(DIAG_THREADS), 0, aux, F.A, (long long)F.n_pad,
-                         kt, F.B, (long long)F.n_pad, F.logdet, c->dinfo);
-    HIPCHK(c, hipGetLastError());
-    if (kt + 1 < NB) {
-      CHK(launch_gemm_range(c, pl.launches[pl.panel[kt]], aux));
-      HIPCHK(c, hipEventRecord(c->ev_panel[kt], aux));
-      if (kt >= 1 && pl.rest[kt - 1] >= 0) HIPCHK(c, hipStreamWaitEvent(aux, c->ev_rest[kt - 1], 0));
-      CHK(launch_gemm_range(c, pl.launches[pl.colupd[kt]], aux));
-      if (pl.rest[kt] >= 0) {
-        HIPCHK(c, hipStreamWaitEvent(mainst, c->ev_panel[kt], 0));
-        CHK(launch_gemm_range(c, pl.launches[pl.rest[kt]], mainst));
-        HIPCHK(c, hipEventRecord(c->ev_rest[kt], mainst));
-      }
-    }
-  }
-  HIPCHK(c, hipEventRecord(c->ev_join, aux));
-  HIPCHK(c, hipStreamWaitEvent(mainst, c->ev_join, 0));
-  return GPE_OK;
-}
-
-// A^-1 = X^T X over L (the plan's LAUUM launch)
-void ev_rec(gpe_ctx* c, int i);
-
-// CU-masked streams for potrf_overlap: bits [0, 128) and [128, 256) of the mask are
-// disjoint halves, 16 CUs of every XCD each (tools/hip/cumask_probe.hip on gfx950)
-bool ensure_tail_streams(gpe_ctx* c) {
-  if (c->tail_streams_tried) return c->tail_streams_ok;
-  c->tail_streams_tried = true;
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, c->device) != hipSuccess || prop.multiProcessorCount < 64) return false;
-  const int ncu = prop.multiProcessorCount, words = (ncu + 31) / 32;
-  std::vector<unsigned> lo(words, 0u), hi(words, 0u);
-  for (int b = 0; b < ncu; ++b) (b < ncu / 2 ? lo : hi)[b >> 5] |= 1u << (b & 31);
-  c->tail_streams_ok = hipStreamCreateWithFlags(&c->st_plain, hipStreamNonBlocking) == hipSuccess &&
-                       hipExtStreamCreateWithCUMask(&c->st_tail, words, lo.data()) == hipSuccess &&
-                       hipExtStreamCreateWithCUMask(&c->st_fill, words, hi.data()) == hipSuccess &&
-                       hipEventCreateWithFlags(&c->ev_split, hipEventDisableTiming) == hipSuccess &&
-                       hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming) == hipSuccess &&
-                       hipEventCreateWithFlags(&c->ev_fill, hipEventDisableTiming) == hipSuccess;
-  return c->tail_streams_ok;
-}
-
-// Cholesky + triangular inverse with the chain-bound tail overlapped: steps [0, split)
-// on the context stream (every CU); then, on two disjoint halves of the CUs at once, the
-// width-1 tail steps [split, NB) and the inverse of the leading block [0, split) (its L
-// is final: DESIGN.md section 6.3); then the rest of the inverse on the context stream.
-// A plain stream beside the tail slowed its chain (the factorisation shares a CU with a
-// long inverse tile); the masks keep the chain's CUs free of them.
-int potrf_trtri_overlap(gpe_ctx* c, Fact& F) {
-  CHK(build_plan(c, F));
-  const Plan& pl = F.plan;
-  const int NB = F.NB, split = pl.split;
-  HIPCHK(c, hipMemsetAsync(F.flags, 0, 3 * (size_t)NB * sizeof(int), c->stream));
-  if (c->tail_mode == 2 && c->chol_prio) {
-    // the sweep on the high-priority stream, the leading block's inverse on the context
-    // stream beside its second part: the chain's workgroups are dispatched first
+  // flags, the group schedule's counters and the launches' list tickets start at zero
+  HIPCHK(c, hipMemsetAsync(F.flags, 0, FACT_FLAG_INTS * (size_t)NB * sizeof(int), c->stream));
+  const bool wa = with_aug && pl.aug;
+  const bool grp = c->potrf_group &&
+                   (c->potrf_mode == 1 || (c->potrf_mode == 0 && g_inflight[c->device & 63].load() <= 1));
+  const std::vector<int>& fidx = grp ? (wa ? pl.grp_aug : pl.grp) : (wa ? pl.fused_aug : pl.fused);
+  if (c->chol_prio) {
+    // the whole sweep on the context's high-priority stream: with two tries in flight
+    // its chain workgroups are dispatched ahead of the other try's inverse tiles
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
-    for (int t = 0; t < split; ++t) CHK(launch_gemm_range(c, pl.launches[pl.fused[t]], c->stream2));
-    HIPCHK(c, hipEventRecord(c->ev_split, c->stream2));
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_split, 0));
-    for (int li : pl.trtri_lead) CHK(launch_gemm_range(c, pl.launches[li]));
-    for (int t = split; t < NB; ++t) CHK(launch_gemm_range(c, pl.launches[pl.fused[t]], c->stream2));
+    for (int t = 0; t < NB; ++t)
+      if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]], c->stream2));
     HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
-    ev_rec(c, 2);
-    for (int li : pl.trtri_rest) CHK(launch_gemm_range(c, pl.launches[li]));
     return GPE_OK;
   }
-  for (int t = 0; t < split; ++t) CHK(launch_gemm_range(c, pl.launches[pl.fused[t]]));
-  HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
-  if (c->tail_mode == 2) {   // plain second stream beside the rest of the sweep
-    HIPCHK(c, hipStreamWaitEvent(c->st_plain, c->ev_split, 0));
-    for (int li : pl.trtri_lead) CHK(launch_gemm_range(c, pl.launches[li], c->st_plain));
-    HIPCHK(c, hipEventRecord(c->ev_fill, c->st_plain));
-    for (int t = split; t < NB; ++t) CHK(launch_gemm_range(c, pl.launches[pl.fused[t]]));
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_fill, 0));
-    ev_rec(c, 2);
-    for (int li : pl.trtri_rest) CHK(launch_gemm_range(c, pl.launches[li]));
-    return GPE_OK;
+#ifdef GEMM_TTRACE
+  if (const char* es = std::getenv("GPEMU_DEBUG_STOP_STEP")) {
+    const int stop = std::atoi(es);
+    // back to back as in the sweep, every launch traced (the host resets the count)
+    for (int t = 0; t <= stop && t < NB; ++t)
+      if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]]));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return fail(c, GPE_ERR_STATE, "debug stop after Cholesky launch " + std::to_string(stop));
   }
-  HIPCHK(c, hipStreamWaitEvent(c->st_tail, c->ev_split, 0));
-  HIPCHK(c, hipStreamWaitEvent(c->st_fill, c->ev_split, 0));
-  for (int t = split; t < NB; ++t) CHK(launch_gemm_range(c, pl.launches[pl.fused[t]], c->st_tail));
-  for (int li : pl.trtri_lead) CHK(launch_gemm_range(c, pl.launches[li], c->st_fill));
-  HIPCHK(c, hipEventRecord(c->ev_tail, c->st_tail));
-  HIPCHK(c, hipEventRecord(c->ev_fill, c->st_fill));
-  HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_tail, 0));
-  HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_fill, 0));
-  ev_rec(c, 2);
-  for (int li : pl.trtri_rest) CHK(launch_gemm_range(c, pl.launches[li]));
+#endif
+  for (int t = 0; t < NB; ++t)
+    if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]]));
   return GPE_OK;
 }
 
+void ev_rec(gpe_ctx* c, int i);
+
+// A^-1 = X^T X over L (the plan's LAUUM launch)
 int lauum(gpe_ctx* c, Fact& F) {
   CHK(build_plan(c, F));
   return launch_gemm_range(c, F.plan.launches[F.plan.lauum]);
@@ -1277,14 +971,6 @@ int lauum(gpe_ctx* c, Fact& F) {
 
 int trtri(gpe_ctx* c, Fact& F) {
   CHK(build_plan(c, F));
-  if (c->chol_prio >= 2) {   // the level launches on the high-priority stream too
-    HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
-    HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
-    for (int li : F.plan.trtri) CHK(launch_gemm_range(c, F.plan.launches[li], c->stream2));
-    HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
-    return GPE_OK;
-  }
   for (int li : F.plan.trtri) CHK(launch_gemm_range(c, F.plan.launches[li]));
   return GPE_OK;
 }
@@ -1302,6 +988,7 @@ int skinny(gpe_ctx* c, bool transposed, const double* M, long long ldm, int ntr,
   const long long rows = (long long)nit * TILE;
   const size_t need = (size_t)nch * rows * P;
   if (need > c->skp_cap) {
+    c->skp_cap = 0;
     CHK(dalloc(c, &c->dskp, need));
     c->skp_cap = need;
   }
@@ -1309,27 +996,14 @@ int skinny(gpe_ctx* c, bool transposed, const double* M, long long ldm, int ntr,
   a.M = M; a.ldm = ldm; a.R = R; a.ldr = ldr; a.part = c->dskp; a.ldp = rows;
   a.pstride = rows * P; a.P = P; a.ntr = ntr; a.lower = lower ? 1 : 0; a.nit = nit;
   a.abort_flag = c->dinfo;
-  const int pm = pmax_bucket(P);
   dim3 grid(nit * nch);
-  if (c->skinny_valu) {
-    if (!transposed) {
-      if (pm == 8) hipLaunchKernelGGL(k_trmm_skinny_n<8>, grid, dim3(256), 0, c->stream, a);
-      else if (pm == 16) hipLaunchKernelGGL(k_trmm_skinny_n<16>, grid, dim3(256), 0, c->stream, a);
-      else hipLaunchKernelGGL(k_trmm_skinny_n<32>, grid, dim3(256), 0, c->stream, a);
-    } else {
-      if (pm == 8) hipLaunchKernelGGL(k_trmm_skinny_t<8>, grid, dim3(256), 0, c->stream, a);
-      else if (pm == 16) hipLaunchKernelGGL(k_trmm_skinny_t<16>, grid, dim3(256), 0, c->stream, a);
-      else hipLaunchKernelGGL(k_trmm_skinny_t<32>, grid, dim3(256), 0, c->stream, a);
-    }
+  const bool p16 = P <= 16;
+  if (!transposed) {
+    if (p16) hipLaunchKernelGGL((k_skinny_mfma<16, false>), grid, dim3(256), 0, c->stream, a);
+    else hipLaunchKernelGGL((k_skinny_mfma<32, false>), grid, dim3(256), 0, c->stream, a);
   } else {
-    const bool p16 = P <= 16;
-    if (!transposed) {
-      if (p16) hipLaunchKernelGGL((k_skinny_mfma<16, false>), grid, dim3(256), 0, c->stream, a);
-      else hipLaunchKernelGGL((k_skinny_mfma<32, false>), grid, dim3(256), 0, c->stream, a);
-    } else {
-      if (p16) hipLaunchKernelGGL((k_skinny_mfma<16, true>), grid, dim3(256), 0, c->stream, a);
-      else hipLaunchKernelGGL((k_skinny_mfma<32, true>), grid, dim3(256), 0, c->stream, a);
-    }
+    if (p16) hipLaunchKernelGGL((k_skinny_mfma<16, true>), grid, dim3(256), 0, c->stream, a);
+    else hipLaunchKernelGGL((k_skinny_mfma<32, true>), grid, dim3(256), 0, c->stream, a);
   }
   HIPCHK(c, hipGetLastError());
   const int mode = lower ? (transposed ? 1 : 0) : 2;
@@ -1429,11 +1103,10 @@ int trsv_lower(gpe_ctx* c, Fact& F, const double* R, long long ldr, int P, doubl
 int factor_and_invert(gpe_ctx* c, int kernel, const double* delta, double nu, double s2,
                       double rscale, bool invert = true) {
   c->linv_valid = false;
-  if (c->tail_streams_ok) {   // a failed earlier call may have left work on the tail streams
-    HIPCHK(c, hipStreamSynchronize(c->st_tail));
-    HIPCHK(c, hipStreamSynchronize(c->st_fill));
-    HIPCHK(c, hipStreamSynchronize(c->st_plain));
-  }
+  // a call that failed inside the sweep may have left Cholesky launches on the
+  // high-priority stream (the join is recorded only after the last one): drain them
+  // before this call's memsets and K-build touch the same buffers
+  HIPCHK(c, hipStreamSynchronize(c->stream2));
   HIPCHK(c, hipMemsetAsync(c->dinfo, 0, sizeof(int), c->stream));
   CHK(build_plan(c, c->tr));
   ev_rec(c, 0);
@@ -1452,16 +1125,11 @@ int factor_and_invert(gpe_ctx* c, int kernel, const double* delta, double nu, do
   }
   ev_rec(c, 1);
   CHK(build_plan(c, c->tr));
-  if (invert && c->tail_overlap && c->tr.plan.split > 0 && ensure_tail_streams(c)) {
-    CHK(potrf_trtri_overlap(c, c->tr));   // records phase event 2 at the join
+  CHK(potrf(c, c->tr, c->zaug_valid));
+  ev_rec(c, 2);
+  if (invert) {
+    CHK(trtri(c, c->tr));
     c->linv_valid = true;
-  } else {
-    CHK(potrf(c, c->tr, c->zaug_valid));
-    ev_rec(c, 2);
-    if (invert) {
-      CHK(trtri(c, c->tr));
-      c->linv_valid = true;
-    }
   }
   CHK(z_from_factor(c));
   ev_rec(c, 3);
@@ -1499,9 +1167,10 @@ int ensure_linv(gpe_ctx* c) {
 int trsv_lower(gpe_ctx* c, Fact& F, const double* R, long long ldr, int P, double* Y, long long ldy) {
   for (int c0 = 0; c0 < P; c0 += TS_PM) {
     const int pc = std::min(TS_PM, P - c0);
-    HIPCHK(c, hipMemsetAsync(F.tflags, 0, sizeof(int), c->stream));   // the row counter
+    HIPCHK(c, hipMemsetAsync(F.tflags, 0, 2 * sizeof(int), c->stream));   // the row counter and ticket
     hipLaunchKernelGGL(k_trsv_lower, dim3(F.NB), dim3(512), 0, c->stream, F.A, (long long)F.n_pad, F.B,
-                       R + (long long)c0 * ldr, ldr, Y + (long long)c0 * ldy, ldy, pc, F.tflags, c->dinfo);
+                       R + (long long)c0 * ldr, ldr, Y + (long long)c0 * ldy, ldy, pc, F.tflags, F.tflags + 1,
+                       c->dinfo);
     HIPCHK(c, hipGetLastError());
   }
   return GPE_OK;
@@ -1590,19 +1259,7 @@ gpe_ctx* gpe_create(int32_t device) {
     c->tr.aug = !(ea && std::string(ea) == "0");
   }
   {
-    const char* e = std::getenv("GPEMU_DIAG");
-    c->diag_rows = e && std::string(e) == "rows";
-    const char* es = std::getenv("GPEMU_SKINNY");
-    c->skinny_valu = es && std::string(es) == "valu";
-    const char* et = std::getenv("GPEMU_TAIL_OVERLAP");
-    c->tail_mode = et ? std::atoi(et) : 0;
-    c->tail_overlap = c->tail_mode == 1 || c->tail_mode == 2;
-    if (const char* es = std::getenv("GPEMU_TAIL_SPLIT")) c->tail_split = std::atoi(es);
-    const char* ek = std::getenv("GPEMU_KPAIRS");
-    c->kpairs_shfl = ek && std::string(ek) == "shuffle";
     const char* e2 = std::getenv("GPEMU_POTRF");
-    c->potrf_lookahead = e2 && std::string(e2) == "lookahead";
-    c->potrf_g2s = e2 && std::string(e2) == "g2s";
     if (e2) {
       const std::string m(e2);
       c->potrf_group = m == "group" || m == "auto";
@@ -1610,9 +1267,7 @@ gpe_ctx* gpe_create(int32_t device) {
     }
     if (const char* eg = std::getenv("GPEMU_GROUP_P0")) c->grp_p0 = std::max(1, std::atoi(eg));
     if (const char* eg = std::getenv("GPEMU_GROUP_STRIDE")) c->grp_stride = std::max(0, std::atoi(eg));
-    if (const char* ep = std::getenv("GPEMU_CHOL_PRIO")) c->chol_prio = std::max(0, std::min(2, std::atoi(ep)));
-    if (const char* ef = std::getenv("GPEMU_POTRF_FIRST")) c->potrf_first = std::max(0, std::min(8, std::atoi(ef)));
-    if (const char* ep = std::getenv("GPEMU_PANEL")) c->panel_trsm = std::string(ep) != "xmul";
+    if (const char* ep = std::getenv("GPEMU_CHOL_PRIO")) c->chol_prio = std::atoi(ep) != 0;
     if (const char* e3 = std::getenv("GPEMU_POTRF_W")) {
       c->potrf_groups.clear();
       std::string spec(e3);
@@ -1689,10 +1344,6 @@ void gpe_destroy(gpe_ctx* c) {
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
   for (auto& e : c->gev) (void)hipEventDestroy(e);
-  for (auto& e : c->ev_panel) (void)hipEventDestroy(e);
-  for (auto& e : c->ev_rest) (void)hipEventDestroy(e);
-  for (auto& e : c->ev_gbulk) (void)hipEventDestroy(e);
-  for (auto& e : c->ev_gchain) (void)hipEventDestroy(e);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->ev_host) (void)hipEventDestroy(c->ev_host);
@@ -1700,13 +1351,6 @@ void gpe_destroy(gpe_ctx* c) {
     (void)hipStreamSynchronize(c->stream2);
     (void)hipStreamDestroy(c->stream2);
   }
-  for (hipStream_t st : {c->st_tail, c->st_fill, c->st_plain})
-    if (st) {
-      (void)hipStreamSynchronize(st);
-      (void)hipStreamDestroy(st);
-    }
-  for (hipEvent_t e : {c->ev_split, c->ev_tail, c->ev_fill})
-    if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1788,8 +1432,8 @@ int gpe_gemm_stats(gpe_ctx* c, double* ms_out, double* launches_out, double* flo
 int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp, int32_t n_hp,
                   double nu_fixed, int32_t want_grad, double* llh_out, double* grad_out,
                   double* sigma2_out) {
-  const InflightGuard inflight(c->device);
   CHK(check_ready(c));
+  const InflightGuard inflight(c->device);
   if (!hp || !llh_out) return fail(c, GPE_ERR_ARG, "null output");
   if (variant != GPE_GP4ML && variant != GPE_MUCM) return fail(c, GPE_ERR_ARG, "bad variant");
   if (kernel != GPE_KERNEL_STD && kernel != GPE_KERNEL_ALT_NUG) return fail(c, GPE_ERR_ARG, "bad kernel");
@@ -1951,6 +1595,7 @@ int gpe_factor(gpe_ctx* c, int32_t kernel, const double* delta, double nu, doubl
 // grow a device buffer to at least `need` doubles
 static int grow(gpe_ctx* c, double** p, size_t* cap, size_t need) {
   if (need <= *cap) return GPE_OK;
+  *cap = 0;
   CHK(dalloc(c, p, need));
   *cap = need;
   return GPE_OK;
@@ -2188,11 +1833,13 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
     // workspace: K* (np x mp) and V (np x mp) [+ full var mp x mp]
     const size_t need = (size_t)np * mp;
     if (need > c->w_cap) {
+      c->w_cap = 0;
       CHK(dalloc(c, &c->dW1, need));
       CHK(dalloc(c, &c->dW2, need));
       c->w_cap = need;
     }
     if ((size_t)mp * d > c->xs_cap) {
+      c->xs_cap = 0;
       CHK(dalloc(c, &c->dXs, (size_t)mp * d));
       CHK(dalloc(c, &c->dXsw, (size_t)mp * d));
       c->xs_cap = (size_t)mp * d;
@@ -2228,19 +1875,15 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
       const int nch = (c->NB + SK_CH - 1) / SK_CH;
       const size_t needp = (size_t)nch * mp * pc;
       if (needp > c->skp_cap) {
+        c->skp_cap = 0;
         CHK(dalloc(c, &c->dskp, needp));
         c->skp_cap = needp;
       }
       SkinnyArgs a;
       a.M = c->dW1; a.ldm = np; a.R = c->dWa + (long long)c0 * np; a.ldr = np; a.part = c->dskp; a.ldp = mp;
       a.pstride = mp * pc; a.P = pc; a.ntr = c->NB; a.lower = 0; a.nit = mt; a.abort_flag = nullptr;
-      const int pm = pmax_bucket(pc);
       dim3 grid(mt * nch);
-      if (c->skinny_valu) {
-        if (pm == 8) hipLaunchKernelGGL(k_trmm_skinny_t<8>, grid, dim3(256), 0, c->stream, a);
-        else if (pm == 16) hipLaunchKernelGGL(k_trmm_skinny_t<16>, grid, dim3(256), 0, c->stream, a);
-        else hipLaunchKernelGGL(k_trmm_skinny_t<32>, grid, dim3(256), 0, c->stream, a);
-      } else if (pc <= 16) {
+      if (pc <= 16) {
         hipLaunchKernelGGL((k_skinny_mfma<16, true>), grid, dim3(256), 0, c->stream, a);
       } else {
         hipLaunchKernelGGL((k_skinny_mfma<32, true>), grid, dim3(256), 0, c->stream, a);
@@ -2326,6 +1969,7 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
       // C = s2 * (A** - V^T V + Tt Tt^T), all tiles (full symmetric)
       const size_t needc = (size_t)mp * mp;
       if (needc + (size_t)mp * kq > c->w3_cap) {
+        c->w3_cap = 0;
         CHK(dalloc(c, &c->dW3, needc + (size_t)mp * kq));
         c->w3_cap = needc + (size_t)mp * kq;
       }
@@ -2380,6 +2024,7 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const size_t needc = (size_t)CHUNK * CHUNK;
     if (!keep_dev && needc > c->w3_cap) {
+      c->w3_cap = 0;
       CHK(dalloc(c, &c->dW3, needc));
       c->w3_cap = needc;
     }

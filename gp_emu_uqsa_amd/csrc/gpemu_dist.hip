@@ -674,17 +674,17 @@ int launch(gpe_dist* h, const DLaunch& L, const GemmProb* base = nullptr) {
   const dim3 b(256);
   if (L.cdef) {
     switch (L.kind) {
-      case 1: hipLaunchKernelGGL((k_gemm<false, true, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo); break;
-      case 2: hipLaunchKernelGGL((k_gemm<true, true, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo); break;
+      case 1: hipLaunchKernelGGL((k_gemm<false, true, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
+      case 2: hipLaunchKernelGGL((k_gemm<true, true, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
       default:   // kind 0 launches may carry G_DIAG / G_PANEL problems
-        hipLaunchKernelGGL((k_gemm<false, false, true, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo); break;
+        hipLaunchKernelGGL((k_gemm<false, false, true, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
     }
   } else {
     switch (L.kind) {
-      case 1: hipLaunchKernelGGL((k_gemm<false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo); break;
-      case 2: hipLaunchKernelGGL((k_gemm<true, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo); break;
+      case 1: hipLaunchKernelGGL((k_gemm<false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
+      case 2: hipLaunchKernelGGL((k_gemm<true, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
       default:   // kind 0 launches may carry G_DIAG / G_PANEL problems
-        hipLaunchKernelGGL((k_gemm<false, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo); break;
+        hipLaunchKernelGGL((k_gemm<false, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
     }
   }
   DCHK_HIP(h, hipGetLastError());

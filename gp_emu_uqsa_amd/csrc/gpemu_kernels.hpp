@@ -10,10 +10,10 @@
 //
 // Kernels (reference call they replace):
 //  k_pairs          K.var / K.covar pair kernel (pdist+exp+squareform, a1,a2,a11)
-//  k_potrf_diag     128x128 diagonal-block Cholesky + its inverse (dpotrf leaf)
 //  k_gemm<AK,BK>    grouped fp64 MFMA GEMM (v_mfma_f64_16x16x4_f64), used for the
-//                   trailing SYRK, panel TRSM, recursive TRTRI and LAUUM
-//  k_trmm_skinny*   L^-1 x [f H] and L^-T x [u w] (the n x q solves of a7)
+//                   trailing SYRK, panel TRSM, recursive TRTRI and LAUUM; its fused
+//                   instance also factors the 128x128 diagonal tiles (gpemu_diag.hpp)
+//  k_skinny_mfma    L^-1 x [f H] and L^-T x [u w] (the n x q solves of a7)
 //  k_contract       fused <M, dA/dtheta> for all d+2 hyperparameters (a4,a5,a7)
 //  small kernels    Gram, reductions, apply q x q transform, column norms
 #pragma once
@@ -112,55 +112,6 @@ static __global__ void __launch_bounds__(256) k_pairs(PairArgs a) {
   }
 }
 
-// A/B variant of the training K-build (GPEMU_KPAIRS=shuffle):
-// north_star's "wavefront shuffle reductions over d" taken literally.  Each pair's squared
-// distance is split over 8 lanes (dimensions l, l + 8, ...), summed by a 3-step xor
-// shuffle tree, and lane 0 of the group evaluates exp and stores.  Same values up to the
-// order of the sum over d (<= 1 ulp of s).  k_pairs instead keeps a whole pair in one
-// lane: the d FMAs are serial in registers and every lane evaluates its own exp, which
-// is where the time goes (one fp64 exp per pair); this variant is kept only to measure.
-template <int DMAX>
-static __global__ void __launch_bounds__(256) k_pairs_shfl(PairArgs a) {
-  __shared__ double xs_col[TILE * DMAX];
-  __shared__ double xs_row[TILE * DMAX];
-  int ti, tj;
-  if (a.mode & 1) tri_decode(blockIdx.x, ti, tj);
-  else { ti = blockIdx.x % a.mt; tj = blockIdx.x / a.mt; }
-  const int tid = threadIdx.x, d = a.d;
-  for (int e = tid; e < TILE * DMAX; e += 256) {
-    const int c = e / DMAX, k = e - c * DMAX;
-    xs_col[e] = k < d ? a.xc[(long long)(tj * TILE + c) * d + k] : 0.0;
-    xs_row[e] = k < d ? a.xr[(long long)(ti * TILE + c) * d + k] : 0.0;
-  }
-  __syncthreads();
-  const int lane = tid & 63, g = lane >> 3, l = lane & 7, wave = tid >> 6;
-  const double pre = a.s2 * a.coff;
-  const bool train = (a.mode & 2) != 0;
-  for (int e = wave * 8 + g; e < TILE * TILE; e += 32) {
-    const int r = e & (TILE - 1), c = e >> 7;
-    double s = 0.0;
-#pragma unroll
-    for (int k = l; k < DMAX; k += 8) {
-      const double df = xs_row[r * DMAX + k] - xs_col[c * DMAX + k];
-      s = fma(df, df, s);
-    }
-    s += __shfl_xor(s, 1, 8);
-    s += __shfl_xor(s, 2, 8);
-    s += __shfl_xor(s, 4, 8);
-    if (l == 0) {
-      const int gi = ti * TILE + r, gj = tj * TILE + c;
-      double v = pre * exp(-s);
-      const bool pad = gi >= a.nr_valid || gj >= a.nc_valid;
-      const bool diag = gi == gj;
-      double vdiag = a.s2 * a.cdiag;
-      if (train && a.r && diag && !pad) vdiag += a.rscale * a.r[gi];
-      if (train) v = pad ? (diag ? 1.0 : 0.0) : (diag ? vdiag : v);
-      else v = pad ? 0.0 : v;
-      a.out[gi + (long long)gj * a.ld] = v;
-    }
-  }
-}
-
 // k_pairs for any d (the reference's kernel takes any number of inputs,
 // _emulatorkernels.py:39-50): coordinates staged through LDS 32 dimensions at a
 // time, each thread keeping the running squared distances of its 64 columns.  The
@@ -226,407 +177,6 @@ static __global__ void __launch_bounds__(256) k_pairs_wide(PairArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// diagonal-block Cholesky + inverse of one 128x128 tile, recursive and MFMA-based.
-// In : A tile (kt,kt) lower part.  Out: L_kk (lower, in place), Dinv_kk = L_kk^-1
-// into tile (kt,kt) of the inverse buffer (upper part zeroed), sum log(L_jj) into
-// logdet[kt], info = 1-based global column of the first bad pivot (LAPACK dpotrf
-// convention) on failure.  Pivot test `!(p > 0)` rejects 0, negatives and NaN.
-//
-// The tile lives in LDS (S, column-major, pitch SP): L in the lower triangle and
-// X = L^-1 stored transposed in the strictly-upper triangle (X(i,c) at S[c+i*SP]),
-// X's diagonal in xd.  node<O,SZ> factors and inverts the SZ x SZ diagonal block
-// at offset O:  node(R1); L21 = A21 X11^T; A22 -= L21 L21^T; node(R2);
-// X21 = -X22 (L21 X11) -- the off-diagonal products on v_mfma_f64_16x16x4_f64
-// straight from LDS (16x16 blocks, 4 waves).  16x16 leaves are factored and
-// inverted by one wave with cross-lane shuffles (16 dependent column steps each).
-// ---------------------------------------------------------------------------
-constexpr int SP = TILE + 1;
-constexpr int DIAG_THREADS = 256;
-
-__device__ __forceinline__ double dg_x(const double* S, const double* xd, int i, int c) {
-  return i > c ? S[c + i * SP] : (i == c ? xd[i] : 0.0);
-}
-
-// wave-uniform broadcast of lane `src`'s double (src a compile-time constant)
-__device__ __forceinline__ double dg_bcast(double v, int src) {
-  const unsigned long long b = __double_as_longlong(v);
-  const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, src);
-  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), src);
-  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
-}
-
-// 1/sqrt(p) from the hardware estimate plus one Newton step (< 1 ulp off the
-// correctly rounded value); sqrt(p) = p * rsq.  p > 0 is checked by the caller.
-__device__ __forceinline__ double dg_rsq(double p) {
-  double r = __builtin_amdgcn_rsq(p);
-  return r * fma(-0.5 * p * r, r, 1.5);
-}
-
-// one wave: factor + invert the 16x16 diagonal leaf at offset o.
-// Lane i (< 16) holds row i of L (a[]) and of X = L^-1 (x[]); column j of L and
-// row j of X are broadcast with v_readlane (no LDS round trip).
-__device__ __forceinline__ void dg_leaf(double* S, double* xd, int o, int lane, int* fail) {
-  const int i = lane;
-  const bool row = i < 16;
-  double a[16], x[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    a[k] = (row && k <= i) ? S[(o + i) + (o + k) * SP] : 0.0;
-    x[k] = (k == i) ? 1.0 : 0.0;
-  }
-  // Column j of L is final after factor step j, so inverse step j (row j of
-  // X = L^-1 scaled by 1/L(j,j), then X(i,c) -= L(i,j) X(j,c) below) runs right
-  // behind it.  Updates are unconditional (no selects): the factor's rank-1 update
-  // only spoils a[k] for k > i (the never-read upper part), and the inverse uses a
-  // zero coefficient on rows i <= j so their final X rows stay exact.
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const double piv = dg_bcast(a[j], j);
-    if (!(piv > 0.0)) {
-      if (lane == 0) *fail = o + j + 1;
-      return;  // wave-uniform
-    }
-    const double r = dg_rsq(piv);
-    const double lij = (i > j) ? a[j] * r : (i == j ? piv * r : 0.0);
-    a[j] = (i >= j) ? lij : a[j];
-#pragma unroll
-    for (int k = j + 1; k < 16; ++k) a[k] = fma(-lij, dg_bcast(lij, k), a[k]);
-    const double sj = (i == j) ? r : 1.0;
-#pragma unroll
-    for (int c = 0; c <= j; ++c) x[c] *= sj;
-    const double coef = (i > j) ? lij : 0.0;
-#pragma unroll
-    for (int c = 0; c <= j; ++c) x[c] = fma(-coef, dg_bcast(x[c], j), x[c]);
-  }
-  if (row) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      if (k <= i) S[(o + i) + (o + k) * SP] = a[k];
-      if (k < i) S[(o + k) + (o + i) * SP] = x[k];
-      if (k == i) xd[o + i] = x[k];
-    }
-  }
-}
-
-// D += A(i0.., k) B(k, j0..) for k in [k0,k1) on one 16x16 block (natural MFMA
-// orientation: lane l, reg r <-> D(i0 + (l>>4) + 4r, j0 + (l&15)))
-template <class FA, class FB>
-__device__ __forceinline__ void dg_mma(d4& acc, FA fa, FB fb, int i0, int j0, int k0, int k1,
-                                       int lane) {
-  // k ranges are multiples of 16: fetch a 16-deep slab of both operands, then 4 MFMAs
-  for (int k = k0; k < k1; k += 16) {
-    double av[4], bv[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      av[s] = fa(i0 + (lane & 15), k + 4 * s + (lane >> 4));
-      bv[s] = fb(k + 4 * s + (lane >> 4), j0 + (lane & 15));
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
-  }
-}
-
-template <int O, int SZ>
-__device__ void dg_node(double* S, double* xd, int* fail, int tid) {
-  const int lane = tid & 63, wave = tid >> 6;
-  if constexpr (SZ == 16) {
-#if !defined(DG_ABLATE) || (DG_ABLATE != 2 && DG_ABLATE != 3)
-    if (wave == 0) dg_leaf(S, xd, O, lane, fail);
-#endif
-    __syncthreads();
-  } else {
-    constexpr int H = SZ / 2, NB = H / 16, O2 = O + H;
-    dg_node<O, H>(S, xd, fail, tid);
-    if (*fail) return;
-#if defined(DG_ABLATE) && (DG_ABLATE == 1 || DG_ABLATE == 3)
-    dg_node<O2, H>(S, xd, fail, tid);
-    return;
-#endif
-    auto lget = [S](int i, int k) { return S[i + k * SP]; };
-    // 1. L21 = A21 X11^T  (X11(c,k) != 0 only for k <= c)
-    {
-      constexpr int PER = (NB * NB + 3) / 4;
-      d4 acc[PER];
-#pragma unroll
-      for (int u = 0; u < PER; ++u) {
-        const int b = wave + 4 * u;
-        acc[u] = d4{0.0, 0.0, 0.0, 0.0};
-        if (b < NB * NB) {
-          const int ib = b % NB, cb = b / NB;
-          dg_mma(acc[u], lget, [S, xd](int k, int n) { return dg_x(S, xd, n, k); }, O2 + ib * 16,
-                 O + cb * 16, O, O + (cb + 1) * 16, lane);
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int u = 0; u < PER; ++u) {
-        const int b = wave + 4 * u;
-        if (b < NB * NB) {
-          const int ib = b % NB, cb = b / NB;
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            S[(O2 + ib * 16 + (lane >> 4) + 4 * r) + (O + cb * 16 + (lane & 15)) * SP] = acc[u][r];
-        }
-      }
-      __syncthreads();
-    }
-    // 2. A22 -= L21 L21^T  (lower blocks)
-    {
-      constexpr int NLOW = NB * (NB + 1) / 2;
-      for (int b = wave; b < NLOW; b += 4) {
-        int ib = 0;
-        while ((ib + 1) * (ib + 2) / 2 <= b) ++ib;
-        const int jb = b - ib * (ib + 1) / 2;
-        d4 acc = d4{0.0, 0.0, 0.0, 0.0};
-        dg_mma(acc, lget, [S](int k, int n) { return S[n + k * SP]; }, O2 + ib * 16, O2 + jb * 16, O,
-               O2, lane);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          S[(O2 + ib * 16 + (lane >> 4) + 4 * r) + (O2 + jb * 16 + (lane & 15)) * SP] -= acc[r];
-      }
-      __syncthreads();
-    }
-    dg_node<O2, H>(S, xd, fail, tid);
-    if (*fail) return;
-    // 3. X21 = -X22 T, T = L21 X11; wave w owns column block w of T and X21.
-    //    The f64 accumulator layout of T(kb, cb) is the B fragment of k-steps 0..3.
-    if (wave < NB) {
-      const int cb = wave;
-      d4 T[NB];
-#pragma unroll
-      for (int ib = 0; ib < NB; ++ib) {
-        T[ib] = d4{0.0, 0.0, 0.0, 0.0};
-        dg_mma(T[ib], lget, [S, xd](int k, int n) { return dg_x(S, xd, k, n); }, O2 + ib * 16,
-               O + cb * 16, O + cb * 16, O + H, lane);
-      }
-#pragma unroll
-      for (int ib = 0; ib < NB; ++ib) {
-        d4 acc = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kb = 0; kb <= ib; ++kb)
-#pragma unroll
-          for (int st = 0; st < 4; ++st) {
-            const double av = dg_x(S, xd, O2 + ib * 16 + (lane & 15), O2 + kb * 16 + 4 * st + (lane >> 4));
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, T[kb][st], acc, 0, 0, 0);
-          }
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          S[(O + cb * 16 + (lane & 15)) + (O2 + ib * 16 + (lane >> 4) + 4 * r) * SP] = -acc[r];
-      }
-    }
-    __syncthreads();
-  }
-}
-
-static __global__ void __launch_bounds__(DIAG_THREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_potrf_diag(double* A, long long lda, int kt,
-                                                             double* Dinv, long long ldd,
-                                                             double* logdet, int* info) {
-  __shared__ double S[TILE * SP];
-  __shared__ double xd[TILE];
-  __shared__ double red[4];
-  __shared__ int fail;
-  if (*info) return;
-  const int t = threadIdx.x;
-  double* Akk = A + (long long)kt * TILE * (lda + 1);
-  // batched copy-in: 16 loads in flight per thread before the LDS stores
-  constexpr int PER = TILE * TILE / DIAG_THREADS;   // 64
-#pragma unroll
-  for (int b = 0; b < PER; b += 16) {
-    double v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int e = t + DIAG_THREADS * (b + u);
-      v[u] = Akk[(e & (TILE - 1)) + (long long)(e >> 7) * lda];
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int e = t + DIAG_THREADS * (b + u);
-      S[(e & (TILE - 1)) + (e >> 7) * SP] = v[u];
-    }
-  }
-  if (t == 0) fail = 0;
-  __syncthreads();
-  dg_node<0, TILE>(S, xd, &fail, t);
-  __syncthreads();
-  if (fail) {
-    if (t == 0) atomicCAS(info, 0, kt * TILE + fail);
-    return;
-  }
-  double lg = (t < TILE) ? log(S[t + t * SP]) : 0.0;
-  for (int off = 32; off > 0; off >>= 1) lg += __shfl_down(lg, off, 64);
-  if ((t & 63) == 0) red[t >> 6] = lg;
-  __syncthreads();
-  if (t == 0) logdet[kt] = (red[0] + red[1]) + (red[2] + red[3]);
-  double* Dkk = Dinv + (long long)kt * TILE * (ldd + 1);
-  // copy-out as 16-byte stores: thread -> (row pair, column)
-#pragma unroll 8
-  for (int b = 0; b < PER / 2; ++b) {
-    const int e = t + DIAG_THREADS * b;          // 0 .. 8191
-    const int i = (e & 63) * 2, k = e >> 6;
-    const double l0 = S[i + k * SP], l1 = S[i + 1 + k * SP];
-    const double x0 = dg_x(S, xd, i, k), x1 = dg_x(S, xd, i + 1, k);
-    double* ap = Akk + i + (long long)k * lda;
-    if (i >= k) *reinterpret_cast<double2*>(ap) = make_double2(l0, l1);
-    else if (i + 1 >= k) ap[1] = l1;
-    *reinterpret_cast<double2*>(Dkk + i + (long long)k * ldd) = make_double2(x0, x1);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// (A/B reference) register-blocked diagonal-block Cholesky + inverse.
-// In : A tile (kt,kt) lower part.  Out: L_kk (lower, in place), Dinv_kk = L_kk^-1
-// into tile (kt,kt) of the inverse buffer (upper part zeroed), sum log(L_jj) into
-// logdet[kt], info = 1-based global column of the first bad pivot (LAPACK dpotrf
-// convention) on failure.  Pivot test `!(p > 0)` rejects 0, negatives and NaN.
-// 1024 threads; thread t owns the 4x4 block (rows 4*(t%32).., cols 4*(t/32)..)
-// of L and of X = L^-1 in registers; only lower blocks are active.  Column j of L
-// and row j of X are broadcast through LDS: two barriers per column for the
-// right-looking factorisation, two per column for the forward-substitution
-// inverse [L | I] -> [I | L^-1].
-// ---------------------------------------------------------------------------
-constexpr int DIAG_ROWS_THREADS = 1024;
-
-static __global__ void __launch_bounds__(DIAG_ROWS_THREADS) k_potrf_diag_rows(double* A, long long lda, int kt,
-                                                             double* Dinv, long long ldd,
-                                                             double* logdet, int* info) {
-  __shared__ double colbuf[TILE];
-  __shared__ double rowbuf[TILE];
-  __shared__ double diagbuf[TILE];
-  __shared__ double red[16];
-  __shared__ double pivot_s;
-  __shared__ int fail_s;
-  if (*info) return;
-  const int t = threadIdx.x;
-  const int bi = t & 31, bk = t >> 5;
-  const bool active = bi >= bk;
-  double* Akk = A + (long long)kt * TILE * (lda + 1);
-  double a[4][4], x[4][4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      a[r][c] = active ? Akk[(4 * bi + r) + (long long)(4 * bk + c) * lda] : 0.0;
-      x[r][c] = (bi == bk && r == c) ? 1.0 : 0.0;
-    }
-  if (t == 0) {
-    pivot_s = a[0][0];
-    fail_s = 0;
-  }
-  __syncthreads();
-  for (int j = 0; j < TILE; ++j) {
-    const int jb = j >> 2, jr = j & 3;
-    const double piv = pivot_s;
-    if (!(piv > 0.0)) {
-      if (t == 0) fail_s = j + 1;
-      break;  // uniform: every thread read the same pivot
-    }
-    const double dj = sqrt(piv), rdj = 1.0 / dj;
-    if (active && bk == jb) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 4 * bi + r;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          if (c == jr) {
-            if (i > j) {
-              a[r][c] *= rdj;
-              colbuf[i] = a[r][c];
-            } else if (i == j) {
-              a[r][c] = dj;
-              diagbuf[j] = dj;
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();
-    if (active && bk >= jb) {
-      double ci[4], ck[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ci[r] = colbuf[4 * bi + r];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) ck[c] = colbuf[4 * bk + c];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int i = 4 * bi + r, k = 4 * bk + c;
-          if (k > j && i >= k) a[r][c] = fma(-ci[r], ck[c], a[r][c]);
-        }
-      const int jn = j + 1;
-      if (jn < TILE && bi == (jn >> 2) && bk == (jn >> 2)) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (r == (jn & 3)) pivot_s = a[r][r];
-      }
-    }
-    __syncthreads();
-  }
-  if (fail_s) {
-    if (t == 0) atomicCAS(info, 0, kt * TILE + fail_s);
-    return;
-  }
-  // log-determinant contribution (fixed reduction tree)
-  double lg = (t < TILE) ? log(diagbuf[t]) : 0.0;
-  for (int off = 32; off > 0; off >>= 1) lg += __shfl_down(lg, off, 64);
-  if ((t & 63) == 0) red[t >> 6] = lg;
-  // X = L^-1: row j of X is final once scaled; rows below get X(i,c) -= L(i,j) X(j,c)
-  for (int j = 0; j < TILE; ++j) {
-    const int jb = j >> 2, jr = j & 3;
-    const double rl = 1.0 / diagbuf[j];
-    if (active && bi == jb) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (r == jr) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const int col = 4 * bk + c;
-            if (col <= j) {
-              x[r][c] *= rl;
-              rowbuf[col] = x[r][c];
-            }
-          }
-        }
-    }
-    if (active && bk == jb) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 4 * bi + r;
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (c == jr && i > j) colbuf[i] = a[r][c];
-      }
-    }
-    __syncthreads();
-    if (active && bi >= jb && bk <= jb) {
-      double li[4], xc[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) li[r] = colbuf[4 * bi + r];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) xc[c] = rowbuf[4 * bk + c];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int i = 4 * bi + r, col = 4 * bk + c;
-          if (i > j && col <= j) x[r][c] = fma(-li[r], xc[c], x[r][c]);
-        }
-    }
-    __syncthreads();
-  }
-  if (t == 0) logdet[kt] = (red[0] + red[1]) + (red[2] + red[3]);
-  double* Dkk = Dinv + (long long)kt * TILE * (ldd + 1);
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = 4 * bi + r, k = 4 * bk + c;
-      if (active && i >= k) Akk[i + (long long)k * lda] = a[r][c];
-      Dkk[i + (long long)k * ldd] = (active && i >= k) ? x[r][c] : 0.0;
-    }
-}
-
-// ---------------------------------------------------------------------------
 // grouped fp64 MFMA GEMM:  C(m,n) = alpha * sum_k opA(m,k) opB(k,n) + beta * C(m,n)
 // over 128x128 output tiles; each problem of a group may skip upper tiles
 // (G_CLOWER) and restrict its K range to a triangular operand's support.
@@ -640,7 +190,9 @@ static __global__ void __launch_bounds__(DIAG_ROWS_THREADS) k_potrf_diag_rows(do
 // in LDS by the same workgroup (gpemu_diag.hpp): L over C, L^-1 into X,
 // sum log L_jj into *logdet, info = diag_col0 + bad column on failure.
 // G_PANEL: a panel tile updated like any other, then (after the G_DIAG workgroup of
-// the same launch released *flag) multiplied by X^T: L = (C - L L^T) X^T.
+// the same launch released *flag) solved against the factored diagonal tile by block
+// substitution: L = (C - L L^T) L_tt^-T (panel_subst; Ld / X point at L_tt and at
+// L_tt^-1's diagonal 16 x 16 blocks).
 enum : int { G_CLOWER = 1, G_KBEG_TI = 2, G_KEND_TI = 4, G_DIAG = 8, G_PANEL = 16 };
 
 struct GemmProb {
@@ -654,8 +206,8 @@ struct GemmProb {
   double* X;          // G_DIAG: X = L^-1 out; G_PANEL: X's diagonal 16 x 16 blocks in
   long long ldx;
   // G_PANEL: the factored diagonal tile L (its strictly lower 16 x 16 blocks), for the
-  // block substitution P = C L^-T; G_DIAG: non-null = release the panel tiles as soon
-  // as L and X's diagonal blocks are out (null: after all of X, for X-multiply panels)
+  // block substitution P = C L^-T (G_DIAG with a flag releases the panel tiles as soon as
+  // L and X's diagonal blocks are out)
   const double* Ld;
   long long ldd;
   double* logdet;
@@ -1156,10 +708,12 @@ __device__ __forceinline__ void gemm_publish_flag(int* flag, int v) {   // one l
 
 // bounded wait (one lane) for a G_DIAG workgroup's flag (1 = ready, 2 = failed);
 // returns the flag, or 0 after ~seconds (never expected: reported as an error)
-__device__ __forceinline__ int gemm_wait_flag(const int* flag) {
+// (an abort raised meanwhile -- a bad pivot elsewhere -- ends the wait as failed)
+__device__ __forceinline__ int gemm_wait_flag(const int* flag, const int* abort_flag) {
   int v = 0;
   for (long it = 0; it < (1l << 22) && v == 0; ++it) {
     v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v == 0 && abort_flag && __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) v = 2;
     if (v == 0) __builtin_amdgcn_s_sleep(8);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -1307,28 +861,44 @@ __device__ __forceinline__ void panel_subst(double* Cb, long long ldc, const dou
 // FUSED (only <false, false, true>): the fused Cholesky's launches, whose problems may be
 // G_DIAG / G_PANEL; the other instances hold no factor / panel code, so they stay well
 // inside the register budget and use the 16-byte C preload and epilogue.
+// ticket (FUSED launches with a tile list and in-launch waits): each workgroup claims its
+// list position with an atomic ticket when it starts, instead of taking blockIdx.x.  A
+// tile waits only on tiles earlier in the list (build_plan checks it), and every earlier
+// position was claimed by a workgroup that is already running, so the earliest unfinished
+// tile can always make progress whatever order the hardware dispatches the workgroups in
+// and whatever else occupies the CUs (other streams, other contexts' launches).
 template <bool AK, bool BK, bool FUSED = false, bool CDEF = false>
 static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restrict__ probs, int nprob,
                                                   const unsigned* __restrict__ tiles,
-                                                  int* __restrict__ abort_flag) {
+                                                  int* __restrict__ abort_flag, int* __restrict__ ticket) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
+  unsigned pos = blockIdx.x;
+  if constexpr (FUSED) {
+    if (ticket) {   // (LDS slot G_LDS_LAUNCH_DOUBLES - 3 is used by nothing else)
+      int* slot = reinterpret_cast<int*>(lds + G_LDS_LAUNCH_DOUBLES - 3);
+      if (threadIdx.x == 0)
+        *slot = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      pos = (unsigned)*slot;
+    }
+  }
   if (abort_flag && *abort_flag) return;
   int p = 0, ti, tj;
   if (tiles) {
-    tile_unpack(tiles[blockIdx.x], p, ti, tj);
+    tile_unpack(tiles[pos], p, ti, tj);
   } else {
     // last problem whose tile_begin <= blockIdx.x (tile_begin is non-decreasing)
     int lo = 0, hi = nprob - 1;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if ((int)blockIdx.x >= probs[mid].tile_begin) lo = mid;
+      if ((int)pos >= probs[mid].tile_begin) lo = mid;
       else hi = mid - 1;
     }
     p = lo;
   }
   const GemmProb P = probs[p];
   if (!tiles) {
-    const int local = blockIdx.x - P.tile_begin;
+    const int local = (int)pos - P.tile_begin;
     if (P.flags & G_CLOWER) {
       tri_decode(local, ti, tj);
     } else if ((P.flags & G_KEND_TI) && nprob == 1) {
@@ -1382,7 +952,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
     gemm_ttrace[e + 4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
     gemm_ttrace[e + 5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
     // [6] kind (0 plain tile, 1 diagonal, 2 panel) + 4 x blockIdx, [7] K of its own product
-    gemm_ttrace[e + 6] = ((P.flags & G_DIAG) ? 1 : ((P.flags & G_PANEL) ? 2 : 0)) + 4ull * blockIdx.x;
+    gemm_ttrace[e + 6] = ((P.flags & G_DIAG) ? 1 : ((P.flags & G_PANEL) ? 2 : 0)) + 4ull * pos;
     gemm_ttrace[e + 7] = (unsigned long long)(kend - kbeg);
   }
 #endif
@@ -1462,42 +1032,37 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
             if (m >= n) lds[db_off(m, n)] = P.alpha * acc[i][j][r];
           }
       __syncthreads();
-      // substitution panels (P.Ld set) are released once L and X's diagonal blocks are
-      // out; X-multiply panels after the whole of X
-      const bool early = P.flag && P.Ld;
+      // the panel tiles (block substitution with L and X's diagonal blocks) are released
+      // once those are out, before the rest of X is assembled
       const int bad = db_factor_invert(lds, Cb, P.ldc, P.X, P.ldx, P.logdet, [&] {
-        if (early) {
+        if (P.flag) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's L / X-block stores done
           __syncthreads();
           if (tid == 0) { gemm_publish_flag(P.flag, 1); GTRACE(P, 2); }
         }
       });
-      if (!early) GTRACE(P, 2);
       if (bad && tid == 0 && abort_flag) atomicCAS(abort_flag, 0, P.diag_col0 + bad);
-      if (P.flag && (bad || !early)) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's L / X stores done
+      if (P.flag && bad) {   // (on_factored is not called for a bad factor)
         __syncthreads();
-        if (tid == 0) gemm_publish_flag(P.flag, bad ? 2 : 1);
+        if (tid == 0) gemm_publish_flag(P.flag, 2);
       }
       GTRACE(P, 3);
       TTRACE(3);
       return;
     }
     if (P.flags & G_PANEL) {
-      // updated panel tile -> C; wait for the diagonal inverse X of this launch;
-      // then L = C X^T over the same tile
+      // updated panel tile -> C; wait for the diagonal factor of this launch; then
+      // L = C L_tt^-T over the same tile by block substitution
       if (ti == 0) GTRACE(P, 5);
       gemm_store<false>(Cb, P.ldc, P.alpha, acc);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       d4 pt[8][2];
-      if (P.Ld) {
-        // the C^T rows span every wave's stores: all of them landed, and no stale L1 line
-        __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        panel_subst_c(Cb, P.ldc, pt);
-      }
+      // the C^T rows span every wave's stores: all of them landed, and no stale L1 line
+      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      panel_subst_c(Cb, P.ldc, pt);
       int* ready = reinterpret_cast<int*>(lds + G_LDS_LAUNCH_DOUBLES - 1);   // staging is idle here
-      if (tid == 0) *ready = gemm_wait_flag(P.flag);
+      if (tid == 0) *ready = gemm_wait_flag(P.flag, abort_flag);
       __syncthreads();
       const int st = *ready;
       __syncthreads();
@@ -1507,16 +1072,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
         return;
       }
       TTRACE(1);   // (panel tiles: [1] = the diagonal inverse seen)
-      if (P.Ld) {
-        panel_subst(Cb, P.ldc, P.Ld, P.ldd, P.X, P.ldx, lds, pt, P, ti);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
-        gemm_kloop<false, false, true, false, false>(Cb, P.X, P.ldc, P.ldx, 0, TILE / GK, lds, acc);
-        gemm_store<false>(Cb, P.ldc, 1.0, acc);
-      }
+      panel_subst(Cb, P.ldc, P.Ld, P.ldd, P.X, P.ldx, lds, pt, P, ti);
       if (ti == 0) GTRACE(P, 7);
       if (P.post) gemm_post_count(P.post);
 #ifdef GEMM_TTRACE
@@ -1727,9 +1283,10 @@ static __global__ void __launch_bounds__(256) k_colnorm2_f32(const float* V, lon
 }
 
 // ---------------------------------------------------------------------------
-// skinny products with a lower-triangular (or full) tiled matrix M (ld = ldm):
-//   k_trmm_skinny_n : part[ch] = M[rows it, cols k in chunk] x R[k, 0:P]
-//   k_trmm_skinny_t : part[ch] = M[rows k in chunk, cols it]^T x R[k, 0:P]
+// skinny products with a lower-triangular (or full) tiled matrix M (ld = ldm),
+// k_skinny_mfma below:
+//   TR = false : part[ch] = M[rows it, cols k in chunk] x R[k, 0:P]
+//   TR = true  : part[ch] = M[rows k in chunk, cols it]^T x R[k, 0:P]
 // R column-major (ld = ldr), partials column-major [ch][P][ldp].
 // Chunks of CH k-tiles bound the partial buffer; k_reduce_chunks sums them
 // in a fixed order (bitwise reproducible).
@@ -1751,102 +1308,6 @@ struct SkinnyArgs {
   const int* abort_flag;
 };
 
-// grid: blockIdx.x = it + nit * ch
-template <int PM>
-static __global__ void __launch_bounds__(256) k_trmm_skinny_n(SkinnyArgs a) {
-  __shared__ double Rs[TILE * PM];
-  __shared__ double red[TILE * PM];
-  if (a.abort_flag && *a.abort_flag) return;
-  const int it = blockIdx.x % a.nit, ch = blockIdx.x / a.nit;
-  const int kt_end_all = a.lower ? it + 1 : a.ntr;
-  const int kt0 = ch * SK_CH;
-  if (kt0 >= kt_end_all) return;
-  const int kt1 = min(kt0 + SK_CH, kt_end_all);
-  const int tid = threadIdx.x, r = tid & (TILE - 1), h = tid >> 7;
-  const int P = a.P;
-  double acc[PM];
-#pragma unroll
-  for (int p = 0; p < PM; ++p) acc[p] = 0.0;
-  for (int kt = kt0; kt < kt1; ++kt) {
-    __syncthreads();
-    for (int e = tid; e < TILE * P; e += 256) {
-      int kk = e & (TILE - 1), p = e >> 7;
-      Rs[kk * PM + p] = a.R[(long long)(kt * TILE + kk) + (long long)p * a.ldr];
-    }
-    __syncthreads();
-    const double* mcol = a.M + (long long)(it * TILE + r) + (long long)(kt * TILE) * a.ldm;
-    for (int kk = h * 64; kk < h * 64 + 64; ++kk) {
-      const double x = mcol[(long long)kk * a.ldm];
-#pragma unroll
-      for (int p = 0; p < PM; ++p)
-        if (p < P) acc[p] = fma(x, Rs[kk * PM + p], acc[p]);
-    }
-  }
-  __syncthreads();
-  if (h == 1) {
-#pragma unroll
-    for (int p = 0; p < PM; ++p) red[r * PM + p] = acc[p];
-  }
-  __syncthreads();
-  if (h == 0) {
-    double* out = a.part + (long long)ch * a.pstride + it * TILE + r;
-#pragma unroll
-    for (int p = 0; p < PM; ++p)
-      if (p < P) out[(long long)p * a.ldp] = acc[p] + red[r * PM + p];
-  }
-}
-
-// grid: blockIdx.x = it + nit * ch ; k tiles: lower ? [it + ch*CH, ...) : [ch*CH, ...)
-template <int PM>
-static __global__ void __launch_bounds__(256) k_trmm_skinny_t(SkinnyArgs a) {
-  constexpr int KS = 64;            // k rows staged per pass
-  __shared__ double Ms[TILE * (KS + 1)];   // [col i][k]
-  __shared__ double Rs[KS * PM];
-  __shared__ double red[TILE * PM];
-  if (a.abort_flag && *a.abort_flag) return;
-  const int it = blockIdx.x % a.nit, ch = blockIdx.x / a.nit;
-  const int kbase = a.lower ? it : 0;
-  const int kt0 = kbase + ch * SK_CH;
-  if (kt0 >= a.ntr) return;
-  const int kt1 = min(kt0 + SK_CH, a.ntr);
-  const int tid = threadIdx.x, c = tid & (TILE - 1), h = tid >> 7;
-  const int P = a.P;
-  double acc[PM];
-#pragma unroll
-  for (int p = 0; p < PM; ++p) acc[p] = 0.0;
-  for (int k0 = kt0 * TILE; k0 < kt1 * TILE; k0 += KS) {
-    __syncthreads();
-    // stage M[k0:k0+KS, it*128 : +128] (column i contiguous in k)
-    for (int e = tid; e < TILE * KS; e += 256) {
-      int kk = e & (KS - 1), i = e >> 6;
-      Ms[i * (KS + 1) + kk] = a.M[(long long)(k0 + kk) + (long long)(it * TILE + i) * a.ldm];
-    }
-    for (int e = tid; e < KS * P; e += 256) {
-      int kk = e & (KS - 1), p = e >> 6;
-      Rs[kk * PM + p] = a.R[(long long)(k0 + kk) + (long long)p * a.ldr];
-    }
-    __syncthreads();
-    for (int kk = h * 32; kk < h * 32 + 32; ++kk) {
-      const double x = Ms[c * (KS + 1) + kk];
-#pragma unroll
-      for (int p = 0; p < PM; ++p)
-        if (p < P) acc[p] = fma(x, Rs[kk * PM + p], acc[p]);
-    }
-  }
-  __syncthreads();
-  if (h == 1) {
-#pragma unroll
-    for (int p = 0; p < PM; ++p) red[c * PM + p] = acc[p];
-  }
-  __syncthreads();
-  if (h == 0) {
-    double* out = a.part + (long long)ch * a.pstride + it * TILE + c;
-#pragma unroll
-    for (int p = 0; p < PM; ++p)
-      if (p < P) out[(long long)p * a.ldp] = acc[p] + red[c * PM + p];
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Z = L^-1 F by blocked forward substitution, without forming L^-1: the value-only
 // objective and gpe_beta need only L, L^-1 f and L^-1 H (_emulatoroptimise.py:382-408,
@@ -1857,7 +1318,7 @@ static __global__ void __launch_bounds__(256) k_trmm_skinny_t(SkinnyArgs a) {
 // as row j is published, then Z_i = D_i acc, published by raising the row counter
 // *flags to i + 1.  Rows publish in order (row i only after reading *flags >= i), so the
 // counter is monotone, one poll tells a lagging row every tile it may take, and every
-// wait is on a workgroup dispatched before the waiting one (no dispatch-order deadlock).
+// wait is on a row claimed (by ticket) before the waiting one's (no dispatch-order deadlock).
 // Thread (r, h), 512 threads: row r of the tile row, k quarter h of every 128 x 128 x P
 // product (L_ij's 32 values are loaded before the wait; D_i's 32 are held from the
 // start), partial sums combined through LDS.  L is read once (n^2/2 x 8 B, HBM-bound);
@@ -1897,12 +1358,17 @@ __device__ __forceinline__ void ts_reduce(double (&v)[TS_PM], double* b0, double
 static __global__ void __launch_bounds__(512) k_trsv_lower(const double* __restrict__ L, long long ld,
                                                    const double* __restrict__ Dinv,
                                                    const double* __restrict__ F, long long ldf, double* Z,
-                                                   long long ldz, int P, int* flags, int* abort_flag) {
+                                                   long long ldz, int P, int* flags, int* ticket,
+                                                   int* abort_flag) {
   constexpr int PM = TS_PM, KQ = TS_KQ;
   __shared__ double Zs[2][TILE * PM];   // [k][p]; after the loop: reduction buffers
-  __shared__ int st;
+  __shared__ int st, row;
   if (abort_flag && *abort_flag) return;   // set by an earlier launch: every workgroup sees it
-  const int i = blockIdx.x;
+  // the tile row by ticket, not blockIdx.x: every row this one waits on was claimed by a
+  // workgroup that is already running (no dependence on the hardware's dispatch order)
+  if (threadIdx.x == 0) row = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int i = row;
   const int tid = threadIdx.x, r = tid & (TILE - 1), h = tid >> 7;
   // D_i(r, k) for this thread's k quarter (the upper triangle is stored as zeros)
   double dv[KQ];
@@ -1987,8 +1453,8 @@ static __global__ void __launch_bounds__(512) k_trsv_lower(const double* __restr
   if (tid == 0) __hip_atomic_store(flags, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// MFMA form of the skinny products (same grid, chunks and partial layout as the
-// VALU kernels above): D(p, i) = sum_k R(k, p) op(M)(k, i) on v_mfma_f64_16x16x4_f64,
+// The skinny products on MFMA (grid: blockIdx.x = it + nit * ch; partials as
+// described above): D(p, i) = sum_k R(k, p) op(M)(k, i) on v_mfma_f64_16x16x4_f64,
 // p = rows of the MFMA tile (P <= PM, zero-padded), i = 128 output rows per
 // workgroup (32 per wave).  TR: op(M)(k,i) = M(k,i) (k contiguous: LDS image [i][k],
 // pitch 34); else op(M)(k,i) = M(i,k) (i contiguous: image [k][i], pitch 144).

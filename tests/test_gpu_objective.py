@@ -141,11 +141,12 @@ def test_objective_vs_oracle_ragged(ctx, n, d):
 
 
 def test_forward_substitution_fallback(monkeypatch):
-    """With the two-stream look-ahead Cholesky (GPEMU_POTRF=lookahead, an A/B switch)
-    the sweep carries no augmented row: L^-1 [f H] then comes from the flag-chained
-    forward substitution (k_trsv_lower) over the diagonal-tile inverses.  Value, gradient
-    and beta against the oracle, ragged n over 11 tile rows."""
-    monkeypatch.setenv("GPEMU_POTRF", "lookahead")
+    """Without the augmented [f H]^T row in the Cholesky (GPEMU_AUG=0; the row is also
+    absent beyond 128 basis columns) L^-1 [f H] for the value-only objective and beta comes
+    from the ticketed, flag-chained forward substitution (k_trsv_lower) over the diagonal-
+    tile inverses.  Value, gradient, beta and the gpe_factor path against the oracle,
+    ragged n over 11 tile rows."""
+    monkeypatch.setenv("GPEMU_AUG", "0")
     c = native.Context(0)
     try:
         X, f, H = orc.synthetic_problem(1300, 5, seed=4)
@@ -173,49 +174,30 @@ def test_forward_substitution_fallback(monkeypatch):
         c.close()
 
 
-def test_kbuild_shuffle_reduction_variant(monkeypatch):
-    """Deliberate deviation from north_star's wording, kept measurable: the K-build's sum
-    over d runs serially in one lane's registers (k_pairs); GPEMU_KPAIRS=shuffle builds the
-    training matrix with the d-sum split over 8 lanes and a shuffle tree instead
-    (k_pairs_shfl).  Both give the reference's objective (G2); DESIGN.md section 6 has
-    the timing that decided for the register form (tools/kpairs_ab.py)."""
-    z = np.load(os.path.join(GOLD, "objective_n1024_d10.npz"))
-    X, f = z["X"], z["f"]
-    key = "std_gp4ml_fitnug_p0"
-    monkeypatch.setenv("GPEMU_KPAIRS", "shuffle")
-    c = native.Context(0)
-    try:
-        c.set_data(X, f, orc.linear_basis(X))
-        llh, g, _ = c.objective(orc.GP4ML, orc.STD, z[key + "_hp"])
-    finally:
-        c.close()
-    ref = float(z[key + "_llh"])
-    assert abs(llh - ref) <= 1e-10 * abs(ref), (llh, ref)
-    ok, err = _grad_ok(g, z[key + "_grad"])
-    assert ok, err
-
-
-_SCHEDULES = [
-    {"GPEMU_CHOL_PRIO": "0"},
-    {"GPEMU_CHOL_PRIO": "2"},
-    {"GPEMU_POTRF": "g2s"},
+# schedules that run the same tiles with the same K ranges, only in other launches, list
+# positions or streams: every tile's arithmetic is the same, so the results are bit-identical
+# (train() relies on it: `auto` picks the group or the per-step launches per call, by what
+# else is in flight on the device)
+_SAME_ARITHMETIC = [
     {"GPEMU_POTRF": "fused"},
     {"GPEMU_POTRF": "group"},
-    {"GPEMU_POTRF": "fused", "GPEMU_POTRF_FIRST": "1"},
-    {"GPEMU_GROUP_STRIDE": "0", "GPEMU_GROUP_P0": "1"},
-    {"GPEMU_GROUP_STRIDE": "5000"},
+    {"GPEMU_CHOL_PRIO": "0"},
+    {"GPEMU_POTRF": "group", "GPEMU_GROUP_STRIDE": "0", "GPEMU_GROUP_P0": "1"},
+    {"GPEMU_POTRF": "group", "GPEMU_GROUP_STRIDE": "5000"},
+]
+# other column-group widths (other K splits of the trailing updates) and the value path
+# without the augmented row: the same results up to rounding
+_OTHER_ARITHMETIC = [
     {"GPEMU_POTRF_W": "8:40,3:20", "GPEMU_GROUP_STRIDE": "300"},
-    {"GPEMU_POTRF_FIRST": "1"},
-    {"GPEMU_TAIL_OVERLAP": "1"},
-    {"GPEMU_TAIL_OVERLAP": "2", "GPEMU_TAIL_SPLIT": "48"},
-    {"GPEMU_TAIL_OVERLAP": "2", "GPEMU_TAIL_SPLIT": "48", "GPEMU_CHOL_PRIO": "0"},
+    {"GPEMU_POTRF_W": "8:40,3:20", "GPEMU_POTRF": "fused"},
+    {"GPEMU_AUG": "0"},
 ]
 
 
 @pytest.fixture(scope="module")
 def schedule_problem():
-    """n = 8448 (66 tile columns: groups of width 4, 2 and 1, and a tail long enough for
-    the overlapped schedules), d = 10, with the default schedule's results."""
+    """n = 8448 (66 tile columns: groups of width 4, 2 and 1), d = 10, with the default
+    schedule's results."""
     X, f, H = orc.synthetic_problem(8448, 10, seed=12)
     hp = np.concatenate([np.linspace(0.8, 1.6, 10), [3e-3, 0.9]])
     c = native.Context(0)
@@ -232,14 +214,8 @@ def schedule_problem():
     return X, f, H, hp, v, llh, g, s2
 
 
-@pytest.mark.parametrize("env", _SCHEDULES, ids=lambda e: ",".join(f"{k[6:]}={v}" for k, v in e.items()))
-def test_schedule_switches_match_default(monkeypatch, schedule_problem, env):
-    """Every A/B schedule switch (the Cholesky's stream priority,
-    one launch per step instead of per column group, the group launch's chain positions
-    and widths, the two-stream group schedule, the first group's width, the overlapped
-    tail on CU-masked halves or a plain stream) computes the default schedule's value,
-    gradient and sigma^2: the same tiles in another order, launch or stream."""
-    X, f, H, hp, v0, llh0, g0, s20 = schedule_problem
+def _run_schedule(monkeypatch, schedule_problem, env):
+    X, f, H, hp = schedule_problem[:4]
     for k, val in env.items():
         monkeypatch.setenv(k, val)
     c = native.Context(0)
@@ -247,8 +223,33 @@ def test_schedule_switches_match_default(monkeypatch, schedule_problem, env):
         c.set_data(X, f, H)
         v = c.objective(orc.GP4ML, orc.STD, hp, want_grad=False)[0]
         llh, g, s2 = c.objective(orc.GP4ML, orc.STD, hp)
+        vm, _, s2m = c.objective(orc.MUCM, orc.STD, hp[:-1], want_grad=False)
     finally:
         c.close()
+    return v, llh, g, s2, vm, s2m
+
+
+@pytest.mark.parametrize("env", _SAME_ARITHMETIC, ids=lambda e: ",".join(f"{k[6:]}={v}" for k, v in e.items()))
+def test_schedule_switches_bit_identical(monkeypatch, schedule_problem, env):
+    """The Cholesky's stream, one launch per step or per column group, and the group
+    launch's chain positions give bit-identical value, gradient and
+    sigma^2 (gp4ml) and MUCM value and sigma-hat^2."""
+    X, f, H, hp, v0, llh0, g0, s20 = schedule_problem
+    base = _run_schedule(monkeypatch, schedule_problem, {})
+    got = _run_schedule(monkeypatch, schedule_problem, env)
+    assert base[0] == v0 and base[1] == llh0 and np.array_equal(base[2], g0) and base[3] == s20
+    assert got[0] == base[0], (got[0], base[0])
+    assert got[1] == base[1], (got[1], base[1])
+    assert np.array_equal(got[2], base[2]), (got[2] - base[2])
+    assert got[3] == base[3] and got[4] == base[4] and got[5] == base[5]
+
+
+@pytest.mark.parametrize("env", _OTHER_ARITHMETIC, ids=lambda e: ",".join(f"{k[6:]}={v}" for k, v in e.items()))
+def test_schedule_widths_match_default(monkeypatch, schedule_problem, env):
+    """Other column-group widths (the trailing updates' K split differently) and the value
+    path without the augmented row: the default's results to rounding."""
+    X, f, H, hp, v0, llh0, g0, s20 = schedule_problem
+    v, llh, g, s2, _, _ = _run_schedule(monkeypatch, schedule_problem, env)
     assert abs(v - v0) <= 1e-11 * abs(v0), (v, v0)
     assert abs(llh - llh0) <= 1e-11 * abs(llh0), (llh, llh0)
     assert abs(s2 - s20) <= 1e-11 * abs(s20)

@@ -161,7 +161,7 @@ int main() {
       float ms = 0;
       CK(hipEventRecord(e0));
       for (int r = 0; r < reps; ++r) {
-        if (v == 0) hipLaunchKernelGGL((k_gemm<true, true>), dim3(mt * mt), dim3(256), lds4, 0, dp, 1, nullptr, nullptr);
+        if (v == 0) hipLaunchKernelGGL((k_gemm<true, true>), dim3(mt * mt), dim3(256), lds4, 0, dp, 1, nullptr, nullptr, nullptr);
         else if (v == 1) hipLaunchKernelGGL(k_pp_tt<1>, dim3(mt * (mt / 2)), dim3(512), PP_LDS * 8, 0, A, (long long)K, B,
                                             (long long)K, C1, (long long)N, mt, K, -1.0, 1.0);
         else hipLaunchKernelGGL(k_pp_tt<2>, dim3(mt * (mt / 2)), dim3(512), PP_LDS * 8, 0, A, (long long)K, B,

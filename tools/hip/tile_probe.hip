@@ -62,7 +62,7 @@ int main(int argc, char** argv) {
       CK(hipMemcpyToSymbol(HIP_SYMBOL(gemm_ttrace_n), &z, sizeof(z)));
     }
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL(kern, dim3(tiles), dim3(256), lds, 0, dp, 1, (const unsigned*)nullptr, (int*)nullptr);
+    hipLaunchKernelGGL(kern, dim3(tiles), dim3(256), lds, 0, dp, 1, (const unsigned*)nullptr, (int*)nullptr, (int*)nullptr);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(&ms, e0, e1));
