@@ -65,8 +65,9 @@ struct Plan {
 };
 
 // F.flags: NB ints each of the diagonal-inverse flags, the group schedule's column and
-// panel counters, and the list tickets of the Cholesky launches (one per column step)
-constexpr int FACT_FLAG_INTS = 4;
+// panel counters, the list tickets of the Cholesky launches (one per column step) and the
+// diagonal tiles' quadrant counters (G_DQUAD)
+constexpr int FACT_FLAG_INTS = 5;
 
 // A factorisation workspace: two n_pad x n_pad buffers and their GEMM schedule.
 struct Fact {
@@ -400,8 +401,19 @@ std::vector<unsigned> order_tiles(const std::vector<GemmProb>& probs) {
     for (int tj : r.tj) bins[x].push_back(((unsigned)r.p << 24) | ((unsigned)r.ti << 12) | (unsigned)tj);
   }
   std::vector<unsigned> out;
-  for (int p = 0; p < (int)probs.size(); ++p)   // a factored diagonal tile starts first
+  // a factored diagonal tile starts first, after the quadrants of its pending update
+  for (int p = 0; p < (int)probs.size(); ++p)
+    if (probs[p].flags & G_DQUAD) {
+      for (int ti = 0; ti < probs[p].mt; ++ti) {
+        const unsigned code = ((unsigned)p << 24) | ((unsigned)ti << 12);
+        out.push_back(code);
+        for (auto& b : bins) b.erase(std::remove(b.begin(), b.end(), code), b.end());
+      }
+    }
+  size_t diag_at = out.size();
+  for (int p = 0; p < (int)probs.size(); ++p)
     if (probs[p].flags & G_DIAG) {
+      diag_at = out.size();
       out.push_back((unsigned)p << 24);
       for (auto& b : bins) b.erase(std::remove(b.begin(), b.end(), (unsigned)p << 24), b.end());
     }
@@ -411,25 +423,15 @@ std::vector<unsigned> order_tiles(const std::vector<GemmProb>& probs) {
     for (int x = 0; x < NX; ++x)
       if (j < bins[x].size()) out.push_back(bins[x][j]);
   // The launch starts on an idle GPU and its first 512 workgroups fill two slots per CU
-  // in order: workgroup 256 lands on the CU of workgroup 0, the G_DIAG tile
+  // in order: workgroup 256 + k lands on the CU of workgroup k, here the G_DIAG tile's
   // (tools/hip/placement_probe.hip: 256 of 256 pairs i, i - 256 share a CU).  Give
   // that slot the first panel tile: after its own update it waits on the flag and
   // leaves the SIMDs to the diagonal factorisation, which beside a bulk tile's MFMAs
   // runs ~1.7x slower.
-  if (!out.empty() && (probs[out[0] >> 24].flags & G_DIAG) && !tail.empty() && out.size() > 256) {
-    out.insert(out.begin() + 256, tail.front());
+  if (diag_at < out.size() && (probs[out[diag_at] >> 24].flags & G_DIAG) && !tail.empty() &&
+      out.size() > diag_at + 256) {
+    out.insert(out.begin() + diag_at + 256, tail.front());
     tail.erase(tail.begin());
-  }
-  // A/B (GPEMU_PANEL_POS = list position): the panel tiles' own pending update does not
-  // wait on the flag; dispatched early, it no longer runs in the launch's drain
-  static const int panel_pos = [] {
-    const char* e = std::getenv("GPEMU_PANEL_POS");
-    return e ? std::atoi(e) : -1;
-  }();
-  if (panel_pos >= 0) {
-    const size_t at = std::min(out.size(), (size_t)panel_pos);
-    out.insert(out.begin() + at, tail.begin(), tail.end());
-    return out;
   }
   out.insert(out.end(), tail.begin(), tail.end());
   return out;
@@ -544,8 +546,24 @@ int build_plan(gpe_ctx* c, Fact& F) {
   //   bulk:     part h of the trailing update by the previous group (K = its width
   //             x 128) over columns j > start(g): part h holds column start(g)+h+1
   //             (factored next) plus a balanced share of the columns after g.
+  // the diagonal tile of step t with K pending columns (from Lp): the pending update runs
+  // as three G_DQUAD workgroups (dquad, pushed before the tile; none for K = 0) and the
+  // G_DIAG workgroup waits for them, loads the updated tile and factors it
+  int* cnt_dq = F.flags + 4 * NB;
+  auto dquad = [&](int t, const double* Lp, int K, double alpha) {
+    GemmProb p = mkprob(Lp, ld, nullptr, 0, tile(A, t, t), ld, 3, 1, K, G_DQUAD, alpha, 1.0);
+    p.post = cnt_dq + t;
+    p.diag_col0 = t * TILE;
+    return p;
+  };
   auto diagprob = [&](int t, const double* Lp, int K, double alpha) {
-    GemmProb p = mkprob(Lp, ld, Lp, ld, tile(A, t, t), ld, 1, 1, K, G_DIAG, alpha, 1.0);
+    (void)Lp;
+    (void)alpha;
+    GemmProb p = mkprob(nullptr, ld, nullptr, ld, tile(A, t, t), ld, 1, 1, 0, G_DIAG, 1.0, 1.0);
+    if (K > 0) {
+      p.pre0 = cnt_dq + t;
+      p.pre0_n = 3;
+    }
     p.X = tile(B, t, t);
     p.ldx = ld;
     p.logdet = F.logdet + t;
@@ -630,7 +648,9 @@ int build_plan(gpe_ctx* c, Fact& F) {
       const int K = (t - p0) * TILE;
       const double al = K ? -1.0 : 1.0;
       const int m = NB - t - 1;
-      std::vector<GemmProb> fp = {diagprob(t, K ? tile(A, t, p0) : nullptr, K, al)};
+      std::vector<GemmProb> fp;
+      if (K) fp.push_back(dquad(t, tile(A, t, p0), K, al));
+      fp.push_back(diagprob(t, K ? tile(A, t, p0) : nullptr, K, al));
       double fl = T * (T + 1.0) * K;
       if (m >= 1) {
         fp.push_back(panelprob(t, K ? tile(A, t + 1, p0) : nullptr, K ? tile(A, t, p0) : nullptr, K, al));
@@ -704,8 +724,14 @@ int build_plan(gpe_ctx* c, Fact& F) {
             q.pre1_n = ncol[h];
           }
         };
+        if (K) {   // the step's hand-offs gate its diagonal tile's quadrants
+          GemmProb dq = dquad(t, tile(A, t, p0), K, al);
+          wire(dq);
+          fp.push_back(dq);
+          codes((int)fp.size() - 1, seg[h]);
+        }
         GemmProb d = diagprob(t, K ? tile(A, t, p0) : nullptr, K, al);
-        wire(d);
+        if (!K) wire(d);
         fp.push_back(d);
         codes((int)fp.size() - 1, seg[h]);
         fl += T * (T + 1.0) * K;
@@ -733,13 +759,13 @@ int build_plan(gpe_ctx* c, Fact& F) {
         std::vector<GemmProb> sub(fp.begin() + b0, fp.end());
         for (unsigned code : order_tiles(sub)) bulkc.push_back(code + ((unsigned)b0 << 24));
       }
-      // assemble: diag(gb), early, bulk; step 0's panels at grp_p0 (its first at 256),
-      // step h's chain at grp_p0 + h grp_stride
-      std::vector<unsigned> base;
-      base.push_back(seg[0][0]);
+      // assemble: diag(gb) (after its quadrants), early, bulk; step 0's panels at grp_p0
+      // (its first beside the diagonal tile), step h's chain at grp_p0 + h grp_stride
+      const size_t head = gi > 0 ? 4 : 1;   // step 0: quadrants (when K > 0) and diagonal tile
+      std::vector<unsigned> base(seg[0].begin(), seg[0].begin() + head);
       base.insert(base.end(), early.begin(), early.end());
       base.insert(base.end(), bulkc.begin(), bulkc.end());
-      std::vector<unsigned> rest0(seg[0].begin() + 1, seg[0].end());
+      std::vector<unsigned> rest0(seg[0].begin() + head, seg[0].end());
       // step h's tiles go before base position min(|base|, p0 + h stride), for h >= 1 not
       // before the column updates they wait on: the positions do not decrease with h, so
       // the steps stay in order even where they clamp
@@ -747,7 +773,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
       order.reserve(base.size() + tiles_total_hint(seg));
       auto pos = [&](int h) {
         size_t at = (size_t)c->grp_p0 + (size_t)h * c->grp_stride;
-        if (h >= 1) at = std::max(at, 1 + early.size());
+        if (h >= 1) at = std::max(at, head + early.size());
         return std::min(base.size(), at);
       };
       int h = 0;
@@ -761,17 +787,17 @@ int build_plan(gpe_ctx* c, Fact& F) {
       }
       // The first 512 workgroups of a launch on an idle GPU fill two slots per CU in
       // order, workgroup 256 + k beside workgroup k (tools/hip/placement_probe.hip): step
-      // 0's first panel tile goes to 256, beside the diagonal tile 0, so the factorisation
-      // has its CU's SIMDs to itself.  (Pinning the later steps' diagonal tiles the same
-      // way, to slots 1 .. W-1, measured no faster: DESIGN.md section 10.)
+      // 0's first panel tile goes to 256 + (head - 1), beside the diagonal tile, so the
+      // factorisation has its CU's SIMDs to itself.  (Pinning the later steps' diagonal
+      // tiles the same way measured no faster: DESIGN.md section 10.)
       auto move_to = [&](unsigned code, size_t at) {
         const auto it = std::find(order.begin(), order.end(), code);
         order.erase(it);
         order.insert(order.begin() + std::min(at, order.size()), code);
       };
-      if (!rest0.empty() && order.size() > 257) {   // the first panel tile to slot 256
+      if (!rest0.empty() && order.size() > 256 + head) {   // the first panel tile beside the diagonal
         const auto it = std::find(order.begin(), order.end(), rest0.front());
-        if (it - order.begin() > 256) move_to(rest0.front(), 256);
+        if ((size_t)(it - order.begin()) > 255 + head) move_to(rest0.front(), 255 + head);
       }
       // every tile may wait only on tiles before it in the list (the dispatch order):
       // then the earliest unfinished tile can always run.  Checked, not assumed.

@@ -131,6 +131,69 @@ __device__ __forceinline__ void db_leaf(double* lb, double* xs, double* xdiag, i
   }
 }
 
+// The same leaf with the column updates on the MFMA pipe.  v_mfma_f64_16x16x4f64(a, b, c)
+// gives D(i, j) = c(i, j) + sum_k a[lane i + 16 k] b[lane j + 16 k], D(i, j) held by lane
+// j + 16 (i & 3) in register i >> 2.  The symmetric block S sits in that layout (acc), so
+// row c of S -- which is column c -- is one register (c >> 2) of one lane group (c & 3),
+// indexed by the lane's column j: scaled by rsq(S(c, c)) it is L(j, c), and as the a and b
+// operands of one MFMA (every other lane group zero) it is the rank-1 update
+// S -= L(., c) L(., c)^T, with no data moved between lanes.  X = L^-1 rides along the same
+// way: Y starts as I, X(c, .) = r Y(c, .) and Y -= L(., c) X(c, .) (a second, independent
+// MFMA per column).  The pivot chain per column is the MFMA, a readlane of the next pivot,
+// rsq + one Newton step and the scaling, against ~325 shader cycles of bpermute round
+// trips in db_leaf, and it leaves the LDS to the other waves' trailing update.
+// Row c of acc is overwritten by L^T's row (L(j, c), j >= c) and row c of Y by X(c, .),
+// so at the end acc's upper triangle is L^T and Y's lower triangle is X.  Same outputs
+// as db_leaf.
+__device__ __forceinline__ void db_leaf_mfma(double* lb, double* xs, double* xdiag, int jb, int* flag) {
+  const int lane = threadIdx.x & 63;
+  const int j = lane & 15, q = lane >> 4;
+  const int base = (jb * (jb + 1) / 2 + jb) * 256;
+  d4 acc, Y;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = q + 4 * r;   // this register's row
+    acc[r] = (i >= j) ? lb[base + i + 16 * j] : lb[base + j + 16 * i];
+    Y[r] = (i == j) ? 1.0 : 0.0;
+  }
+  int bad = 0;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const int k0 = c & 3, rc = c >> 2;
+    const double piv = db_bcast(acc[rc], c + 16 * k0);
+    if (!(piv > 0.0) && bad == 0) bad = c + 1;   // wave-uniform; later columns are NaN garbage
+    const double r = db_rsq(piv);
+    const bool mine = q == k0;
+    const double u = acc[rc] * r;                  // lane group k0: L(j, c) for j > c
+    const double xr = Y[rc] * r;                   // lane group k0: X(c, j)
+    const bool act = mine && j > c;
+    const double ua = act ? -u : 0.0, ub = act ? u : 0.0;
+    const double xb = mine ? xr : 0.0;
+    acc[rc] = (mine && j >= c) ? (j == c ? piv * r : u) : acc[rc];   // row c -> L^T
+    Y[rc] = mine ? xr : Y[rc];                                        // row c -> X(c, .)
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ua, ub, acc, 0, 0, 0);
+    Y = __builtin_amdgcn_mfma_f64_16x16x4f64(ua, xb, Y, 0, 0, 0);
+  }
+  if (bad) {
+    if (lane == 0) *flag = jb * 16 + bad;
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int c = q + 4 * r;   // this register's row of acc / Y: L(j, c) or X(c, j)
+    lb[base + j + 16 * c] = (j >= c) ? acc[r] : Y[r];   // L lower / X(c, j) at (j, c), upper
+    xs[c + 16 * j] = Y[r];                              // X(c, j), zero for j > c
+    if (j == c) xdiag[jb * 16 + c] = Y[r];
+  }
+}
+
+// the leaf of db_factor_invert (-DDB_LEAF_PERMUTE: the bpermute leaf, dev A/B)
+#ifdef DB_LEAF_PERMUTE
+#define DB_LEAF db_leaf
+#else
+#define DB_LEAF db_leaf_mfma
+#endif
+
 // A(po) -= L(pa) L(pb)^T for 16 x 16 blocks at LDS offsets pa, pb, po (one wave)
 __device__ __forceinline__ void db_syrk_block(double* lb, int pa, int pb, int po) {
   const int lane = threadIdx.x & 63;
@@ -292,7 +355,7 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
   DB_TN(0);
   DB_TN(1);
   if (wave == 0) {
-    db_leaf(lb, xs, xdiag, 0, flag);
+    DB_LEAF(lb, xs, xdiag, 0, flag);
   } else {
     // X's 28 strictly-upper blocks are zero
     for (int b = wave - 1; b < 28; b += 3) {
@@ -339,7 +402,7 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
       db_syrk_block(lb, p1, p1, db_blk(jb + 1, jb + 1));
       DB_T(6);
       DB_TN(5);
-      db_leaf(lb, xs, xdiag, jb + 1, flag);
+      DB_LEAF(lb, xs, xdiag, jb + 1, flag);
       DB_T(5);
     } else {
       DB_TN(7);

@@ -193,7 +193,11 @@ static __global__ void __launch_bounds__(256) k_pairs_wide(PairArgs a) {
 // the same launch released *flag) solved against the factored diagonal tile by block
 // substitution: L = (C - L L^T) L_tt^-T (panel_subst; Ld / X point at L_tt and at
 // L_tt^-1's diagonal 16 x 16 blocks).
-enum : int { G_CLOWER = 1, G_KBEG_TI = 2, G_KEND_TI = 4, G_DIAG = 8, G_PANEL = 16 };
+// G_DQUAD: the pending update of a G_DIAG tile split over three workgroups, one per
+// 64 x 64 quadrant of its lower half (tiles ti = 0, 1, 2: quadrants (0,0), (1,0), (1,1);
+// dq_update); each posts *post when stored, and the G_DIAG workgroup (K = 0) waits for
+// all three, then loads the updated tile.
+enum : int { G_CLOWER = 1, G_KBEG_TI = 2, G_KEND_TI = 4, G_DIAG = 8, G_PANEL = 16, G_DQUAD = 32 };
 
 struct GemmProb {
   const double* A;
@@ -759,6 +763,99 @@ __device__ unsigned long long gemm_trace[8 * 4096];
 #define GTRACE(P, slot) do {} while (0)
 #endif
 
+// One 64 x 64 quadrant (qr, qc) of a diagonal tile's pending update, C -= L_r L_c^T over K
+// (L_r / L_c: rows 64 qr / 64 qc of the tile row's pending columns, A = their top-left,
+// column-major, lda), by one workgroup: the diagonal tile's update is on the Cholesky's
+// critical chain, and on one CU its 128 x 128 x K product (4.2 MFLOP at K = 128, ~14 us at
+// one CU's fp64 MFMA rate, plus the cold C preload) was the step's second-longest link.
+// Three workgroups take the lower half's quadrants at once (1 MFLOP each at K = 128).
+// Waves 2 x 2, 32 x 32 each; K staged 16 deep through a 4-slot LDS ring ([k][m] images,
+// pitch 64, global_load_lds: one wave instruction = two k rows of 64 doubles), three
+// chunks in flight (the operands were just written by other CUs: L2 misses).
+// The quadrant's C is loaded before the first chunk and added after the K loop.
+// Diagonal quadrants skip their upper-right 32 x 32 (never read: only the tile's lower
+// half is factored).
+constexpr int DQ_P = 64;               // image pitch (doubles)
+constexpr int DQ_IMG = GK * DQ_P;      // one operand image, 1024 doubles
+constexpr int DQ_SLOT = 2 * DQ_IMG;    // A + B
+constexpr int DQ_RING = 4;             // 64 KB of the 72 KB staging space
+static_assert(DQ_RING * DQ_SLOT <= G_LDS_DOUBLES, "dq ring");
+__device__ __forceinline__ void dq_stage(const double* La, const double* Lb, long long lda, int k0, double* lds,
+                                         int slot, int lane) {
+  const int wave = gemm_wave();   // the LDS targets (M0) are wave-uniform
+  double* As = lds + slot * DQ_SLOT;
+  double* Bs = As + DQ_IMG;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {   // wave instruction w = 2 wave + h: k rows 2w, 2w + 1
+    const int w = 2 * wave + h;
+    const long long off = 2 * (lane & 31) + (long long)(k0 + 2 * w + (lane >> 5)) * lda;
+    glds16(La + off, As + w * 2 * DQ_P);
+    glds16(Lb + off, Bs + w * 2 * DQ_P);
+  }
+}
+
+template <class Prob>
+__device__ __forceinline__ void dq_update(const Prob& P, int quad, double* lds) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int qr = quad >= 1 ? 1 : 0, qc = quad == 2 ? 1 : 0;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const bool skip = qr == qc && wm < wn;   // upper-right 32 x 32 of a diagonal quadrant
+  const double* La = P.A + 64 * qr;
+  const double* Lb = P.A + 64 * qc;
+  double* Cq = P.C + 64 * qr + (long long)(64 * qc) * P.ldc;
+  const int nk = P.K / GK;
+  // this wave's C (2 x 2 blocks, 4 values each), in flight while the operands stream in
+  double cv[2][2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        cv[i][j][r] = gld1(Cq + (wm + 16 * i + (lane & 15)) + (long long)(wn + 16 * j + mfma64_row(lane, r)) * P.ldc);
+  for (int c = 0; c < 3 && c < nk; ++c) dq_stage(La, Lb, P.lda, c * GK, lds, c, lane);
+  d4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int c = 0; c < nk; ++c) {
+    // chunk c landed (4 loads per wave per chunk; the later chunks may stay in flight)
+    const int ahead = min(2, nk - 1 - c);
+    if (ahead == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();   // every wave's pieces of chunk c; every wave is done with chunk c - 1
+    if (c + 3 < nk) dq_stage(La, Lb, P.lda, (c + 3) * GK, lds, (c + 3) % DQ_RING, lane);
+    const double* As = lds + (c % DQ_RING) * DQ_SLOT;
+    const double* Bs = As + DQ_IMG;
+    if (!skip) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int krow = 4 * ks + (lane >> 4);
+        double af[2], bf[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = As[krow * DQ_P + wm + 16 * i + (lane & 15)];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bf[j] = Bs[krow * DQ_P + wn + 16 * j + (lane & 15)];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(bf[j], af[i], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  if (skip) return;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        gst1(Cq + (wm + 16 * i + (lane & 15)) + (long long)(wn + 16 * j + mfma64_row(lane, r)) * P.ldc,
+             P.beta * cv[i][j][r] + P.alpha * acc[i][j][r]);
+}
+
 // Panel tile of the fused Cholesky by block substitution: P = C L^-T for a 128 x 128
 // tile C (in place, ldc) against the factored diagonal tile L (ldd) and its diagonal
 // blocks' inverses X_b (X's diagonal 16 x 16 blocks, ldx).  As transposes, P^T(jb) =
@@ -956,6 +1053,13 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
     gemm_ttrace[e + 7] = (unsigned long long)(kend - kbeg);
   }
 #endif
+  if constexpr (FUSED) {
+    if (P.flags & G_DQUAD) {   // one quadrant of a diagonal tile's pending update
+      dq_update(P, ti, lds);
+      if (P.post) gemm_post_count(P.post);
+      return;
+    }
+  }
   if (P.flags & G_DIAG) GTRACE(P, 0);
   if ((P.flags & G_PANEL) && ti == 0) GTRACE(P, 4);
 

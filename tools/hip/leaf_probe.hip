@@ -176,7 +176,8 @@ __device__ __forceinline__ void leaf_lds(double* lb, double* xs, double* xdiag, 
 }
 
 // mode 0: db_leaf (permutes), 1: db_leaf_sc (readlanes), 2: loads + stores only,
-// 3/4: leaf_sc2 (pipelined next pivot; 4 also splits the update run), 5: leaf_lds
+// 3/4: leaf_sc2 (pipelined next pivot; 4 also splits the update run), 5: leaf_lds,
+// 6: db_leaf_mfma (column updates as rank-1 MFMAs in the accumulator layout)
 template <int MODE>
 __global__ void __launch_bounds__(64) k_leaf(const double* A, double* out, unsigned long long* t, int reps) {
   __shared__ __attribute__((aligned(16))) double lb[DB_LDS_DOUBLES + DB_EXTRA_DOUBLES];
@@ -196,6 +197,7 @@ __global__ void __launch_bounds__(64) k_leaf(const double* A, double* out, unsig
     else if (MODE == 3) leaf_sc2<0>(lb, xs, xdiag, 0, flag);
     else if (MODE == 4) leaf_sc2<1>(lb, xs, xdiag, 0, flag);
     else if (MODE == 5) leaf_lds(lb, xs, xdiag, 0, flag, lb + 1024);
+    else if (MODE == 6) db_leaf_mfma(lb, xs, xdiag, 0, flag);
     else {
       double v = lb[lane] + lb[lane + 64];
       xs[lane] = v;
@@ -219,7 +221,7 @@ int main() {
   hipMalloc(&A, 256 * 8); hipMalloc(&out, 512 * 8); hipMalloc(&t, 16);
   hipMemcpy(A, h, 256 * 8, hipMemcpyHostToDevice);
   const int reps = 200;
-  for (int m = 0; m < 6; ++m) {
+  for (int m = 0; m < 7; ++m) {
     for (int it = 0; it < 2; ++it) {
       if (m == 0) hipLaunchKernelGGL(k_leaf<0>, dim3(1), dim3(64), 0, 0, A, out, t, reps);
       if (m == 1) hipLaunchKernelGGL(k_leaf<1>, dim3(1), dim3(64), 0, 0, A, out, t, reps);
@@ -227,6 +229,7 @@ int main() {
       if (m == 3) hipLaunchKernelGGL(k_leaf<3>, dim3(1), dim3(64), 0, 0, A, out, t, reps);
       if (m == 4) hipLaunchKernelGGL(k_leaf<4>, dim3(1), dim3(64), 0, 0, A, out, t, reps);
       if (m == 5) hipLaunchKernelGGL(k_leaf<5>, dim3(1), dim3(64), 0, 0, A, out, t, reps);
+      if (m == 6) hipLaunchKernelGGL(k_leaf<6>, dim3(1), dim3(64), 0, 0, A, out, t, reps);
       hipDeviceSynchronize();
     }
     unsigned long long th[2];
