@@ -65,9 +65,10 @@ struct Plan {
 };
 
 // F.flags: NB ints each of the diagonal-inverse flags, the group schedule's column and
-// panel counters, the list tickets of the Cholesky launches (one per column step) and the
-// diagonal tiles' quadrant counters (G_DQUAD)
-constexpr int FACT_FLAG_INTS = 5;
+// panel counters, the list tickets of the Cholesky launches (one per column step), the
+// diagonal tiles' quadrant counters (G_DQUAD) and the panel tiles' stored-update counters
+// (G_PHALF0)
+constexpr int FACT_FLAG_INTS = 6;
 
 // A factorisation workspace: two n_pad x n_pad buffers and their GEMM schedule.
 struct Fact {
@@ -511,6 +512,7 @@ GemmProb mkprob(const double* A, long long lda, const double* B, long long ldb, 
   p.X = nullptr; p.ldx = 0; p.logdet = nullptr; p.diag_col0 = 0; p.flag = nullptr;
   p.Ld = nullptr; p.ldd = 0;
   p.pre0 = p.pre1 = p.post = nullptr; p.pre0_n = p.pre1_n = 0;
+  p.cpost = nullptr;
   return p;
 }
 
@@ -573,8 +575,13 @@ int build_plan(gpe_ctx* c, Fact& F) {
     p.ldd = ld;
     return p;
   };
+  // panel tiles: the G_PHALF0 problem (pending update + rows 0-63 of the substitution) and,
+  // from it, the G_PHALF1 problem (rows 64-127, after every G_PHALF0 tile of the step
+  // stored its update: pc_n of them)
+  int* cnt_pc = F.flags + 5 * NB;
   auto panelprob = [&](int t, const double* Lp, const double* Lt, int K, double alpha) {
-    GemmProb p = mkprob(Lp, ld, Lt, ld, tile(A, t + 1, t), ld, NB - t - 1, 1, K, G_PANEL, alpha, 1.0);
+    GemmProb p = mkprob(Lp, ld, Lt, ld, tile(A, t + 1, t), ld, NB - t - 1, 1, K, G_PANEL | G_PHALF0, alpha, 1.0);
+    p.cpost = cnt_pc + t;
     p.X = tile(B, t, t);
     p.ldx = ld;
     p.flag = F.flags + t;
@@ -586,13 +593,28 @@ int build_plan(gpe_ctx* c, Fact& F) {
   // the augmented row's panel tile (aug, t): pending columns [p0, t), then x L_tt^-T
   auto augpanel = [&](int t, int p0, int K, double alpha) {
     GemmProb p = mkprob(K ? atile(p0) : nullptr, TILE, K ? tile(A, t, p0) : nullptr, ld, atile(t), TILE, 1, 1, K,
-                        G_PANEL, alpha, 1.0);
+                        G_PANEL | G_PHALF0, alpha, 1.0);
+    p.cpost = cnt_pc + t;
     p.X = tile(B, t, t);
     p.ldx = ld;
     p.flag = F.flags + t;
     p.Ld = tile(A, t, t);
     p.ldd = ld;
     p.diag_col0 = -TILE;   // (no GEMM_TRACE slot)
+    return p;
+  };
+  auto half1 = [&](const GemmProb& h0, int pc_n) {
+    GemmProb p = h0;
+    p.flags = G_PANEL | G_PHALF1;
+    p.A = p.B = nullptr;
+    p.K = 0;
+    p.alpha = 1.0;
+    p.beta = 0.0;
+    p.pre0 = h0.cpost;
+    p.pre0_n = pc_n;
+    p.pre1 = nullptr;
+    p.pre1_n = 0;
+    p.cpost = nullptr;
     return p;
   };
   // bulk problems: tiles (i, j), i >= j, j in [a, b), updated by columns [g0, g0 + K/128);
@@ -652,11 +674,14 @@ int build_plan(gpe_ctx* c, Fact& F) {
       if (K) fp.push_back(dquad(t, tile(A, t, p0), K, al));
       fp.push_back(diagprob(t, K ? tile(A, t, p0) : nullptr, K, al));
       double fl = T * (T + 1.0) * K;
+      const int pc_n = (m >= 1 ? m : 0) + (aug ? 1 : 0);
+      const size_t h0at = fp.size();
       if (m >= 1) {
         fp.push_back(panelprob(t, K ? tile(A, t + 1, p0) : nullptr, K ? tile(A, t, p0) : nullptr, K, al));
         fl += 2.0 * m * T * T * K + (double)m * T * T * T;
       }
       if (aug) fp.push_back(augpanel(t, p0, K, al));
+      for (size_t k = h0at, e = fp.size(); k < e; ++k) fp.push_back(half1(fp[k], pc_n));
       if (gi > 0) {
         const int g0 = gs[gi - 1], Kb = (gb - g0) * TILE;
         if (h + 1 < W1) bulk(fp, fl, t + 1, t + 2, g0, Kb);   // the column factored next
@@ -735,13 +760,14 @@ int build_plan(gpe_ctx* c, Fact& F) {
         fp.push_back(d);
         codes((int)fp.size() - 1, seg[h]);
         fl += T * (T + 1.0) * K;
+        const int pc_n = (m >= 1 ? m : 0) + (aug ? 1 : 0);
+        const size_t h0at = fp.size();
         if (m >= 1) {
           GemmProb q = panelprob(t, K ? tile(A, t + 1, p0) : nullptr, K ? tile(A, t, p0) : nullptr, K, al);
           wire(q);
           q.post = cnt_pan + t;
           fp.push_back(q);
           codes((int)fp.size() - 1, seg[h]);
-          npan[h] += m;
           fl += 2.0 * m * T * T * K + (double)m * T * T * T;
         }
         if (aug) {
@@ -750,8 +776,12 @@ int build_plan(gpe_ctx* c, Fact& F) {
           pa.post = cnt_pan + t;
           fp.push_back(pa);
           codes((int)fp.size() - 1, seg[h]);
-          npan[h] += 1;
         }
+        for (size_t k = h0at, e = fp.size(); k < e; ++k) {   // the rows 64-127 halves
+          fp.push_back(half1(fp[k], pc_n));
+          codes((int)fp.size() - 1, seg[h]);
+        }
+        npan[h] += 2 * pc_n;   // both halves of every panel tile post cnt_pan
       }
       if (gi > 0 && ge < NB) {   // the columns after the group by the previous group
         const size_t b0 = fp.size();
@@ -806,6 +836,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
         for (size_t i = 0; i < order.size(); ++i) {
           const GemmProb& q = fp[order[i] >> 24];
           if (q.post) last_post[q.post] = i;
+          if (q.cpost) last_post[q.cpost] = i;
           if (q.flags & G_DIAG) diag_at[q.flag] = i;
         }
         for (size_t i = 0; i < order.size(); ++i) {

@@ -197,7 +197,12 @@ static __global__ void __launch_bounds__(256) k_pairs_wide(PairArgs a) {
 // 64 x 64 quadrant of its lower half (tiles ti = 0, 1, 2: quadrants (0,0), (1,0), (1,1);
 // dq_update); each posts *post when stored, and the G_DIAG workgroup (K = 0) waits for
 // all three, then loads the updated tile.
-enum : int { G_CLOWER = 1, G_KBEG_TI = 2, G_KEND_TI = 4, G_DIAG = 8, G_PANEL = 16, G_DQUAD = 32 };
+// G_PHALF0 / G_PHALF1 (with G_PANEL): every panel tile is two workgroups, one per 64-row
+// half of its substitution.  The G_PHALF0 workgroup runs the tile's pending update, stores
+// it and posts *cpost, then substitutes rows 0-63; the G_PHALF1 workgroup (K = 0) waits
+// for all of its step's G_PHALF0 tiles to post (pre0), then substitutes rows 64-127.
+enum : int { G_CLOWER = 1, G_KBEG_TI = 2, G_KEND_TI = 4, G_DIAG = 8, G_PANEL = 16, G_DQUAD = 32,
+             G_PHALF0 = 64, G_PHALF1 = 128 };
 
 struct GemmProb {
   const double* A;
@@ -225,6 +230,7 @@ struct GemmProb {
   int* pre1;
   int* post;
   int pre0_n, pre1_n;
+  int* cpost;         // G_PHALF0: counted once the tile's pending update is stored
 };
 
 // dev-tool per-tile timeline (-DGEMM_TTRACE build only, tools/hip/tile_probe.hip): per
@@ -860,21 +866,47 @@ __device__ __forceinline__ void dq_update(const Prob& P, int quad, double* lds) 
 // tile C (in place, ldc) against the factored diagonal tile L (ldd) and its diagonal
 // blocks' inverses X_b (X's diagonal 16 x 16 blocks, ldx).  As transposes, P^T(jb) =
 // X_jb (C^T(jb) - sum_{kb<jb} L(jb,kb) P^T(kb)) for the eight 16-row blocks jb.
-// Wave w owns the tile's rows 32w .. 32w+31 (two 16-column blocks cb of P^T), so the
-// waves never exchange data; an MFMA result (row (lane>>4)+4r, column lane&15) is
+// A tile's rows are split over two workgroups (G_PHALF0 / G_PHALF1: rows row_base ..
+// row_base + 63); wave w owns rows row_base + 16w .. + 15 (one 16-column block of P^T), so
+// the waves never exchange data; an MFMA result (row (lane>>4)+4r, column lane&15) is
 // already the B operand of the next product (k = 4s + (lane>>4), n = lane&15 at s = r).
+// On one CU the substitution is its 144 MFMAs per wave (64 cycles each): two workgroups
+// per tile halve the chain's panel link against one workgroup of 32 rows per wave.
 // panel_subst_c: this wave's C^T blocks into pt -- issued before the flag wait (C is
-// the tile's own update, stored just before by all four waves: the caller has them
-// land first), so they arrive while the factor finishes.
-__device__ __forceinline__ void panel_subst_c(const double* Cb, long long ldc, d4 (&pt)[8][2]) {
-  const int lane = threadIdx.x & 63, row0 = (threadIdx.x >> 6) * 32 + (lane & 15);
+// the tile's own update, stored before by the G_PHALF0 workgroup's four waves: the
+// caller has them land first), so they arrive while the factor finishes.
+// The tile's loads and stores are buffer accesses off one SGPR resource at the tile's
+// corner: one 32-bit lane offset (row, column lane >> 4) and a uniform offset per
+// (jb, r), where 64-bit per-access addresses kept all 32 of them live (and spilled).
+// (Offsets fit 32 bits: n <= 2^20, so ldc * 8 * 128 < 2^31.)
+struct PanelAddr {
+  __amdgpu_buffer_rsrc_t rsrc;
+  int voff, ldc8;
+};
+__device__ __forceinline__ PanelAddr panel_addr(const double* Cb, long long ldc, int row_base) {
+  PanelAddr a;
+  const unsigned long long cb = (unsigned long long)Cb;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)cb), hi = __builtin_amdgcn_readfirstlane((unsigned)(cb >> 32));
+  a.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0, -1, 0x00020000);
+  const int lane = threadIdx.x & 63, row0 = row_base + (threadIdx.x >> 6) * 16 + (lane & 15);
+  a.ldc8 = (int)(ldc * 8);
+  a.voff = row0 * 8 + (lane >> 4) * a.ldc8;
+  return a;
+}
+__device__ __forceinline__ double panel_ld(const PanelAddr& a, int col) {   // col: jb * 16 + 4 r
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(a.rsrc, a.voff, col * a.ldc8, 0);
+  return __longlong_as_double(((long long)v[1] << 32) | v[0]);
+}
+__device__ __forceinline__ void panel_st(const PanelAddr& a, int col, double x) {
+  const unsigned long long b = __double_as_longlong(x);
+  __builtin_amdgcn_raw_buffer_store_b64((__attribute__((ext_vector_type(2))) unsigned){(unsigned)b, (unsigned)(b >> 32)},
+                                        a.rsrc, a.voff, col * a.ldc8, 0);
+}
+__device__ __forceinline__ void panel_subst_c(const PanelAddr& pa, d4 (&pt)[8]) {
 #pragma unroll
   for (int jb = 0; jb < 8; ++jb)
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        pt[jb][cb][r] = gld1(Cb + (row0 + cb * 16) + (long long)(jb * 16 + (lane >> 4) + 4 * r) * ldc);
+    for (int r = 0; r < 4; ++r) pt[jb][r] = panel_ld(pa, jb * 16 + 4 * r);
 }
 
 typedef double dv2 __attribute__((ext_vector_type(2)));
@@ -888,22 +920,28 @@ __host__ __device__ constexpr int tri_row(int b) {   // bi of packed lower block
 // LDS: L(jb,kb) (kb < jb) and X_jb, block-packed (db_blk) -- 72 KB, the staging space;
 // every thread's 18 16-byte pieces are loaded together (one round trip), then stored.
 template <class Prob>
-__device__ __forceinline__ void panel_subst(double* Cb, long long ldc, const double* Ld, long long ldd,
-                                            const double* Xd, long long ldx, double* lb, d4 (&pt)[8][2],
+__device__ __forceinline__ void panel_subst(const PanelAddr& pa, const double* Ld, long long ldd,
+                                            const double* Xd, long long ldx, double* lb, d4 (&pt)[8],
                                             const Prob& P, int ti) {
   const int tid = threadIdx.x, lane = tid & 63;
   {
+    // one SGPR resource per source (L, X's diagonal blocks), a 32-bit lane offset each and
+    // a uniform offset per block: no per-load 64-bit addresses live across the batch
     const int hi = tid >> 7, w = tid & 127, r = (w & 7) * 2, c = w >> 3;
+    const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)Ld, 0, -1, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)Xd, 0, -1, 0x00020000);
+    const int ldd8 = (int)(ldd * 8), ldx8 = (int)(ldx * 8);
+    const int vl = r * 8 + c * ldd8, vx = r * 8 + c * ldx8;
     dv2 v[18];
 #pragma unroll
     for (int i = 0; i < 18; ++i) {   // block b = 2i + hi (both candidates fold at compile time)
       const int bi0 = tri_row(2 * i), bk0 = 2 * i - bi0 * (bi0 + 1) / 2;
       const int bi1 = tri_row(2 * i + 1), bk1 = 2 * i + 1 - bi1 * (bi1 + 1) / 2;
-      const long long off0 = (bi0 * 16 + r) + (long long)(bk0 * 16 + c) * (bi0 == bk0 ? ldx : ldd);
-      const long long off1 = (bi1 * 16 + r) + (long long)(bk1 * 16 + c) * (bi1 == bk1 ? ldx : ldd);
-      const double* b0 = bi0 == bk0 ? Xd : Ld;
-      const double* b1 = bi1 == bk1 ? Xd : Ld;
-      v[i] = *(__attribute__((address_space(1))) const dv2*)(hi ? b1 + off1 : b0 + off0);
+      const int bi = hi ? bi1 : bi0, bk = hi ? bk1 : bk0;   // (hi is wave-uniform)
+      const bool xb = bi == bk;
+      const auto u = __builtin_amdgcn_raw_buffer_load_b128(xb ? rx : rl, xb ? vx : vl,
+                                                            bi * 128 + bk * 16 * (xb ? ldx8 : ldd8), 0);
+      v[i] = dv2{__longlong_as_double(((long long)u[1] << 32) | u[0]), __longlong_as_double(((long long)u[3] << 32) | u[2])};
     }
 #pragma unroll
     for (int i = 0; i < 18; ++i) *reinterpret_cast<dv2*>(lb + (2 * i + hi) * 256 + r + c * 16) = v[i];
@@ -912,7 +950,6 @@ __device__ __forceinline__ void panel_subst(double* Cb, long long ldc, const dou
 #ifdef PANEL_PHASES   // dev probe: GEMM_TRACE slot 5 = staging done
   if (ti == 0) GTRACE(P, 5);
 #endif
-  const int row0 = (tid >> 6) * 32 + (lane & 15);
   const int ao = (lane & 15) + (lane >> 4) * 16;   // A operand (m = lane&15, k = 4s + lane>>4) at ao + 64 s
 #pragma unroll
   for (int jb = 0; jb < 8; ++jb) {
@@ -926,32 +963,25 @@ __device__ __forceinline__ void panel_subst(double* Cb, long long ldc, const dou
       for (int s = 0; s < 4; ++s) av[kb][s] = arow[kb * 256 + 64 * s];
 #pragma unroll
     for (int s = 0; s < 4; ++s) xv[s] = arow[jb * 256 + 64 * s];
-    d4 t0[2], t1[2];
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) { t0[cb] = d4{0.0, 0.0, 0.0, 0.0}; t1[cb] = t0[cb]; }
+    // two accumulation chains (even / odd kb) keep two MFMAs in flight
+    d4 t0 = d4{0.0, 0.0, 0.0, 0.0}, t1 = t0;
 #pragma unroll
     for (int kb = 0; kb < jb; ++kb) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
-          if (kb & 1) t1[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kb][s], pt[kb][cb][s], t1[cb], 0, 0, 0);
-          else t0[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kb][s], pt[kb][cb][s], t0[cb], 0, 0, 0);
-        }
+        if (kb & 1) t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kb][s], pt[kb][s], t1, 0, 0, 0);
+        else t0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kb][s], pt[kb][s], t0, 0, 0, 0);
       }
     }
+    const d4 t = pt[jb] - (t0 + t1);
+    d4 o = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const d4 t = pt[jb][cb] - (t0[cb] + t1[cb]);
-      d4 o = d4{0.0, 0.0, 0.0, 0.0};
+    for (int s = 0; s < 4; ++s) o = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[s], t[s], o, 0, 0, 0);
+    pt[jb] = o;
+    // buffer stores (a FLAT store would also count in lgkmcnt, and the next step's LDS
+    // wait would wait for it to land)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) o = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[s], t[s], o, 0, 0, 0);
-      pt[jb][cb] = o;
-      // global stores: a FLAT store also counts in lgkmcnt, and the next step's LDS
-      // wait would wait for it to land
-#pragma unroll
-      for (int r = 0; r < 4; ++r) gst1(Cb + (row0 + cb * 16) + (long long)(jb * 16 + (lane >> 4) + 4 * r) * ldc, o[r]);
-    }
+    for (int r = 0; r < 4; ++r) panel_st(pa, jb * 16 + 4 * r, o[r]);
   }
 }
 
@@ -1061,7 +1091,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
     }
   }
   if (P.flags & G_DIAG) GTRACE(P, 0);
-  if ((P.flags & G_PANEL) && ti == 0) GTRACE(P, 4);
+  if ((P.flags & G_PHALF0) && ti == 0) GTRACE(P, 4);
 
   const double* Ab = AK ? P.A + (long long)ti * TILE * P.lda : P.A + (long long)ti * TILE;
   const double* Bb = BK ? P.B + (long long)tj * TILE * P.ldb : P.B + (long long)tj * TILE;
@@ -1155,29 +1185,34 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
       return;
     }
     if (P.flags & G_PANEL) {
-      // updated panel tile -> C; wait for the diagonal factor of this launch; then
-      // L = C L_tt^-T over the same tile by block substitution
-      if (ti == 0) GTRACE(P, 5);
-      gemm_store<false>(Cb, P.ldc, P.alpha, acc);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      d4 pt[8][2];
+      // G_PHALF0: updated panel tile -> C, posted; both halves: wait for the diagonal
+      // factor of this launch, then L = C L_tt^-T over their 64 rows by block substitution
+      const bool h0 = (P.flags & G_PHALF0) != 0;
+      const int row_base = h0 ? 0 : 64;
+      if (h0) {
+        if (ti == 0) GTRACE(P, 5);
+        gemm_store<false>(Cb, P.ldc, P.alpha, acc);
+        gemm_post_count(P.cpost);   // (every wave's stores landed: the barrier inside)
+      }
+      d4 pt[8];
       // the C^T rows span every wave's stores: all of them landed, and no stale L1 line
       __syncthreads();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      panel_subst_c(Cb, P.ldc, pt);
+      const PanelAddr pa = panel_addr(Cb, P.ldc, row_base);
+      panel_subst_c(pa, pt);
       int* ready = reinterpret_cast<int*>(lds + G_LDS_LAUNCH_DOUBLES - 1);   // staging is idle here
       if (tid == 0) *ready = gemm_wait_flag(P.flag, abort_flag);
       __syncthreads();
       const int st = *ready;
       __syncthreads();
-      if (ti == 0) GTRACE(P, 6);
+      if (h0 && ti == 0) GTRACE(P, 6);
       if (st != 1) {
         if (st == 0 && tid == 0 && abort_flag) atomicCAS(abort_flag, 0, GEMM_WAIT_TIMEOUT);
         return;
       }
       TTRACE(1);   // (panel tiles: [1] = the diagonal inverse seen)
-      panel_subst(Cb, P.ldc, P.Ld, P.ldd, P.X, P.ldx, lds, pt, P, ti);
-      if (ti == 0) GTRACE(P, 7);
+      panel_subst(pa, P.Ld, P.ldd, P.X, P.ldx, lds, pt, P, ti);
+      if (h0 && ti == 0) GTRACE(P, 7);
       if (P.post) gemm_post_count(P.post);
 #ifdef GEMM_TTRACE
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
