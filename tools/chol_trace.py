@@ -37,10 +37,13 @@ if os.environ.get("PANEL_PHASES"):   # libgpemu_trace built with -DPANEL_PHASES:
     print("panel substitution: staging %.1f us, products + stores %.1f us (mean over steps)"
           % (np.mean(first[1:]), np.mean(second[1:])))
 print(" k   d.upd  d.fac  d.pub  p.upd  p.wait  p.mul  seen-pub  gap   step")
-for r in rows[:3] + rows[60:63] + rows[100:103] + rows[-6:]:
+show = sorted(set(list(range(min(3, NB))) + list(range(60, min(63, NB))) + list(range(100, min(103, NB)))
+                  + list(range(max(0, NB - 6), NB))))
+for k in show:
+    r = rows[k]
     print("%3d " % r[0] + " ".join("%6.1f" % v for v in r[1:]))
-for lo, hi in ((1, 48), (48, 88), (88, NB - 1)):
-    if hi > NB - 1 or lo >= hi:
-        lo, hi = 1, NB - 1
+segs = ((1, 48), (48, 88), (88, NB - 1)) if NB >= 96 else ((1, NB - 1),)
+for lo, hi in segs:
     seg = np.array([r[1:] for r in rows[lo:hi]])
-    print("mean over steps %3d..%3d:" % (lo, hi - 1), " ".join("%6.1f" % v for v in seg.mean(axis=0)))
+    if len(seg):
+        print("mean over steps %3d..%3d:" % (lo, hi - 1), " ".join("%6.1f" % v for v in seg.mean(axis=0)))

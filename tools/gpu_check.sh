@@ -10,3 +10,8 @@ tail -3 gpurun_out/gputest_$TAG.log
 [ $rc -eq 0 ] || exit $rc
 for n in 16384 4096; do timeout -k 10 120 python3 tools/quick_time.py $n 10 || exit 1; done 2>&1 | tee gpurun_out/qt_$TAG.log
 timeout -k 10 120 python3 tools/small_n_time.py 2>&1 | tee gpurun_out/small_n_$TAG.log
+if [ -f gp_emu_uqsa_amd/libgpemu_trace.so ]; then
+  for n in 16384 4096; do
+    GPEMU_LIB=gp_emu_uqsa_amd/libgpemu_trace.so timeout -k 10 120 python3 tools/chol_trace.py $n || exit 1
+  done 2>&1 | tee gpurun_out/chol_trace_$TAG.log
+fi
