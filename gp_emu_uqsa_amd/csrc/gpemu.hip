@@ -803,7 +803,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
       order.reserve(base.size() + tiles_total_hint(seg));
       auto pos = [&](int h) {
         size_t at = (size_t)c->grp_p0 + (size_t)h * c->grp_stride;
-        if (h >= 1) at = std::max(at, head + early.size());
+        at = std::max(at, h >= 1 ? head + early.size() : head);   // after the step's diagonal tile
         return std::min(base.size(), at);
       };
       int h = 0;
