@@ -187,11 +187,101 @@ __device__ __forceinline__ void db_leaf_mfma(double* lb, double* xs, double* xdi
   }
 }
 
-// the leaf of db_factor_invert (-DDB_LEAF_PERMUTE: the bpermute leaf, dev A/B)
-#ifdef DB_LEAF_PERMUTE
+
+// The leaf by 4-column blocks: per block p the 4 x 4 diagonal block is broadcast (its 10
+// values by readlane) and factored and inverted by every lane on uniform values (Li =
+// L_pp^-1, four dependent rsq's), and everything else is four MFMAs on the accumulator
+// layout of db_leaf_mfma.  Rows 4p .. 4p+3 of S are register p of the four lane groups
+// (lane j + 16 q holds S(4p + q, j)), so with a[lane i + 16 k] = Li(i - 4p, k) (rows of
+// the block only) and b = acc[p]:
+//   MFMA(a, acc[p])   = Li S(block rows, .)  -> rows 4p.. of L^T (the block and the panel)
+//   MFMA(a, Y[p])     = Li Y(block rows, .)  -> rows 4p.. of X = L^-1
+//   S -= P P^T, Y -= P X(block rows, .)     (P = the new acc[p] past the block: the panel)
+// Two MFMAs and the 4 x 4 factor per four columns on the pivot chain, against one MFMA
+// and a rsq per column in db_leaf_mfma.  Same outputs as db_leaf.
+__device__ __forceinline__ void db_leaf_blk(double* lb, double* xs, double* xdiag, int jb, int* flag) {
+  const int lane = threadIdx.x & 63;
+  const int j = lane & 15, q = lane >> 4;
+  const int base = (jb * (jb + 1) / 2 + jb) * 256;
+  d4 acc, Y;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = q + 4 * r;   // this register's row
+    acc[r] = (i >= j) ? lb[base + i + 16 * j] : lb[base + j + 16 * i];
+    Y[r] = (i == j) ? 1.0 : 0.0;
+  }
+  int bad = 0;
+  const d4 z4 = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int c0 = 4 * p;
+    // S(c0 + k, c0 + l), l <= k: lane c0 + l of group k, register p
+    const double a00 = db_bcast(acc[p], c0);
+    const double a10 = db_bcast(acc[p], c0 + 16), a11 = db_bcast(acc[p], c0 + 17);
+    const double a20 = db_bcast(acc[p], c0 + 32), a21 = db_bcast(acc[p], c0 + 33), a22 = db_bcast(acc[p], c0 + 34);
+    const double a30 = db_bcast(acc[p], c0 + 48), a31 = db_bcast(acc[p], c0 + 49), a32 = db_bcast(acc[p], c0 + 50),
+                 a33 = db_bcast(acc[p], c0 + 51);
+    // 4 x 4 Cholesky (uniform values) and its inverse Li
+    if (!(a00 > 0.0) && bad == 0) bad = c0 + 1;
+    const double r0 = db_rsq(a00);
+    const double l10 = a10 * r0, l20 = a20 * r0, l30 = a30 * r0;
+    const double d1 = fma(-l10, l10, a11);
+    if (!(d1 > 0.0) && bad == 0) bad = c0 + 2;
+    const double r1 = db_rsq(d1);
+    const double l21 = fma(-l20, l10, a21) * r1, l31 = fma(-l30, l10, a31) * r1;
+    const double d2 = fma(-l21, l21, fma(-l20, l20, a22));
+    if (!(d2 > 0.0) && bad == 0) bad = c0 + 3;
+    const double r2 = db_rsq(d2);
+    const double l32 = fma(-l31, l21, fma(-l30, l20, a32)) * r2;
+    const double d3 = fma(-l32, l32, fma(-l31, l31, fma(-l30, l30, a33)));
+    if (!(d3 > 0.0) && bad == 0) bad = c0 + 4;
+    const double r3 = db_rsq(d3);
+    const double i10 = -l10 * r0 * r1;
+    const double i21 = -l21 * r1 * r2;
+    const double i20 = -(l20 * r0 + l21 * i10) * r2;
+    const double i32 = -l32 * r2 * r3;
+    const double i31 = -(l31 * r1 + l32 * i21) * r3;
+    const double i30 = -(l30 * r0 + l31 * i10 + l32 * i20) * r3;
+    // a[lane i + 16 k] = Li(i - c0, k) for rows i of the block
+    const int ib = j - c0;   // row of Li this lane supplies (valid 0..3)
+    double li;
+    if (q == 0) li = ib == 0 ? r0 : (ib == 1 ? i10 : (ib == 2 ? i20 : i30));
+    else if (q == 1) li = ib == 1 ? r1 : (ib == 2 ? i21 : i31);
+    else if (q == 2) li = ib == 2 ? r2 : i32;
+    else li = r3;
+    const double aL = (ib >= q && ib < 4) ? li : 0.0;
+    const d4 Lr = __builtin_amdgcn_mfma_f64_16x16x4f64(aL, acc[p], z4, 0, 0, 0);   // rows c0.. of L^T
+    const d4 Xr = __builtin_amdgcn_mfma_f64_16x16x4f64(aL, Y[p], z4, 0, 0, 0);     // rows c0.. of X
+    const double pv = Lr[p];                      // L(j, c0 + q) for j past the block
+    const double pa = j >= c0 + 4 ? pv : 0.0;
+    acc[p] = (j >= c0) ? pv : acc[p];             // rows c0.. -> L^T (upper part)
+    Y[p] = Xr[p];
+    if (p < 3) {
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-pa, pa, acc, 0, 0, 0);
+      Y = __builtin_amdgcn_mfma_f64_16x16x4f64(-pa, Y[p], Y, 0, 0, 0);
+    }
+  }
+  if (bad) {
+    if (lane == 0) *flag = jb * 16 + bad;
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int c = q + 4 * r;   // this register's row of acc / Y: L(j, c) or X(c, j)
+    lb[base + j + 16 * c] = (j >= c) ? acc[r] : Y[r];   // L lower / X(c, j) at (j, c), upper
+    xs[c + 16 * j] = Y[r];                              // X(c, j), zero for j > c
+    if (j == c) xdiag[jb * 16 + c] = Y[r];
+  }
+}
+
+// the leaf of db_factor_invert (dev A/B: -DDB_LEAF_PERMUTE the bpermute leaf, -DDB_LEAF_COLUMN
+// the rank-1 MFMA leaf)
+#if defined(DB_LEAF_PERMUTE)
 #define DB_LEAF db_leaf
-#else
+#elif defined(DB_LEAF_COLUMN)
 #define DB_LEAF db_leaf_mfma
+#else
+#define DB_LEAF db_leaf_blk
 #endif
 
 // A(po) -= L(pa) L(pb)^T for 16 x 16 blocks at LDS offsets pa, pb, po (one wave)

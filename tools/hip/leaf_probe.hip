@@ -175,9 +175,58 @@ __device__ __forceinline__ void leaf_lds(double* lb, double* xs, double* xdiag, 
   }
 }
 
+
+// probes of the MFMA leaf's chain (db_leaf_mfma): VARIANT 1 drops the X (Y) MFMA,
+// VARIANT 2 drops both MFMAs (the pivot chain alone: readlane, rsq, scaling)
+template <int VARIANT>
+__device__ __forceinline__ void leaf_mfma_probe(double* lb, double* xs, double* xdiag, int jb, int* flag) {
+  const int lane = threadIdx.x & 63;
+  const int j = lane & 15, q = lane >> 4;
+  const int base = (jb * (jb + 1) / 2 + jb) * 256;
+  d4 acc, Y;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = q + 4 * r;
+    acc[r] = (i >= j) ? lb[base + i + 16 * j] : lb[base + j + 16 * i];
+    Y[r] = (i == j) ? 1.0 : 0.0;
+  }
+  int bad = 0;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const int k0 = c & 3, rc = c >> 2;
+    const double piv = db_bcast(acc[rc], c + 16 * k0);
+    if (!(piv > 0.0) && bad == 0) bad = c + 1;
+    const double r = db_rsq(piv);
+    const bool mine = q == k0;
+    const double u = acc[rc] * r;
+    const double xr = Y[rc] * r;
+    const bool act = mine && j > c;
+    const double ua = act ? -u : 0.0, ub = act ? u : 0.0;
+    const double xb = mine ? xr : 0.0;
+    acc[rc] = (mine && j >= c) ? (j == c ? piv * r : u) : acc[rc];
+    Y[rc] = mine ? xr : Y[rc];
+    if (VARIANT < 2) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ua, ub, acc, 0, 0, 0);
+    else acc[(rc + 1) & 3] = acc[(rc + 1) & 3] - ua * ub;   // keep a dependence on the column
+    if (VARIANT < 1) Y = __builtin_amdgcn_mfma_f64_16x16x4f64(ua, xb, Y, 0, 0, 0);
+  }
+  if (bad) {
+    if (lane == 0) *flag = jb * 16 + bad;
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int c = q + 4 * r;
+    lb[base + j + 16 * c] = (j >= c) ? acc[r] : Y[r];
+    xs[c + 16 * j] = Y[r];
+    if (j == c) xdiag[jb * 16 + c] = Y[r];
+  }
+}
+
 // mode 0: db_leaf (permutes), 1: db_leaf_sc (readlanes), 2: loads + stores only,
 // 3/4: leaf_sc2 (pipelined next pivot; 4 also splits the update run), 5: leaf_lds,
-// 6: db_leaf_mfma (column updates as rank-1 MFMAs in the accumulator layout)
+// 6: db_leaf_mfma (column updates as rank-1 MFMAs in the accumulator layout), 7: its chain
+// without the X MFMA, 8: without either MFMA (wrong results: chain latency only),
+// 9: db_leaf_blk (4-column blocks: 4 x 4 factor on uniform values, four MFMAs per block)
 template <int MODE>
 __global__ void __launch_bounds__(64) k_leaf(const double* A, double* out, unsigned long long* t, int reps) {
   __shared__ __attribute__((aligned(16))) double lb[DB_LDS_DOUBLES + DB_EXTRA_DOUBLES];
@@ -198,6 +247,9 @@ __global__ void __launch_bounds__(64) k_leaf(const double* A, double* out, unsig
     else if (MODE == 4) leaf_sc2<1>(lb, xs, xdiag, 0, flag);
     else if (MODE == 5) leaf_lds(lb, xs, xdiag, 0, flag, lb + 1024);
     else if (MODE == 6) db_leaf_mfma(lb, xs, xdiag, 0, flag);
+    else if (MODE == 7) leaf_mfma_probe<1>(lb, xs, xdiag, 0, flag);
+    else if (MODE == 8) leaf_mfma_probe<2>(lb, xs, xdiag, 0, flag);
+    else if (MODE == 9) db_leaf_blk(lb, xs, xdiag, 0, flag);
     else {
       double v = lb[lane] + lb[lane + 64];
       xs[lane] = v;
@@ -221,7 +273,7 @@ int main() {
   hipMalloc(&A, 256 * 8); hipMalloc(&out, 512 * 8); hipMalloc(&t, 16);
   hipMemcpy(A, h, 256 * 8, hipMemcpyHostToDevice);
   const int reps = 200;
-  for (int m = 0; m < 7; ++m) {
+  for (int m = 0; m < 10; ++m) {
     for (int it = 0; it < 2; ++it) {
       if (m == 0) hipLaunchKernelGGL(k_leaf<0>, dim3(1), dim3(64), 0, 0, A, out, t, reps);
       if (m == 1) hipLaunchKernelGGL(k_leaf<1>, dim3(1), dim3(64), 0, 0, A, out, t, reps);
@@ -230,6 +282,9 @@ int main() {
       if (m == 4) hipLaunchKernelGGL(k_leaf<4>, dim3(1), dim3(64), 0, 0, A, out, t, reps);
       if (m == 5) hipLaunchKernelGGL(k_leaf<5>, dim3(1), dim3(64), 0, 0, A, out, t, reps);
       if (m == 6) hipLaunchKernelGGL(k_leaf<6>, dim3(1), dim3(64), 0, 0, A, out, t, reps);
+      if (m == 7) hipLaunchKernelGGL(k_leaf<7>, dim3(1), dim3(64), 0, 0, A, out, t, reps);
+      if (m == 8) hipLaunchKernelGGL(k_leaf<8>, dim3(1), dim3(64), 0, 0, A, out, t, reps);
+      if (m == 9) hipLaunchKernelGGL(k_leaf<9>, dim3(1), dim3(64), 0, 0, A, out, t, reps);
       hipDeviceSynchronize();
     }
     unsigned long long th[2];
