@@ -85,6 +85,12 @@ struct Fact {
   // workspace only)
   bool aug = false;
   double* Faug = nullptr;
+  // split-K scratch of the TRTRI / LAUUM launches with few tiles (k_gemm ksplit):
+  // SPLIT_SLOTS partial tiles and one counter per tile of a launch
+  double* part = nullptr;
+  int* tcnt = nullptr;
+  // B's diagonal tiles hold the full X_tt = L_tt^-1 (k_xasm ran after the last sweep)
+  bool xdone = false;
   int desc_base = 0;         // first slot of its descriptors in the device array
   Plan plan;
 };
@@ -361,7 +367,32 @@ int launch_gemm_range(gpe_ctx* c, const Launch& L, hipStream_t st = nullptr) {
 
 // tiles of a problem
 int prob_tiles(const GemmProb& p) {
-  return (p.flags & G_CLOWER) ? p.mt * (p.mt + 1) / 2 : p.mt * p.nt;
+  return ((p.flags & G_CLOWER) ? p.mt * (p.mt + 1) / 2 : p.mt * p.nt) * std::max(1, p.ksplit);
+}
+
+// Split K over workgroups for a launch with few tiles (small n, the TRTRI's first levels):
+// there each tile's K loop on one CU is the launch's latency, and the chip has 512
+// workgroup slots.  ks shares of at least 128 K each, at most SPLIT_SLOTS partials; beta = 0
+// problems only.  The launch then takes the implicit tile order (no list).
+constexpr int SPLIT_SLOTS = 512;
+void split_k(std::vector<GemmProb>& probs, double* part, int* tcnt) {
+  int T = 0, kmax = 0;
+  for (const GemmProb& p : probs) {
+    if (p.beta != 0.0 || p.ksplit > 1) return;
+    T += prob_tiles(p);
+    kmax = std::max(kmax, p.K);
+  }
+  if (T <= 0 || T >= 256) return;
+  const int ks = std::min({8, SPLIT_SLOTS / T, kmax / TILE});
+  if (ks < 2) return;
+  int off = 0;
+  for (GemmProb& p : probs) {
+    const int tl = prob_tiles(p);
+    p.ksplit = ks;
+    p.part = part + (size_t)off * ks * TILE * TILE;
+    p.tcnt = tcnt + off;
+    off += tl;
+  }
 }
 
 // Order the tiles of one launch: rows (problem, ti) sorted longest-first, greedily
@@ -450,7 +481,7 @@ void add_launch(Plan& pl, int kind, std::vector<GemmProb> probs, double flops) {
     p.ntiles = prob_tiles(p);
     t += p.ntiles;
     L.cdef = L.cdef || gemm_cdef(p);
-    listable = listable && p.mt <= 4096 && p.nt <= 4096;
+    listable = listable && p.mt <= 4096 && p.nt <= 4096 && p.ksplit <= 1;
     pl.probs.push_back(p);
   }
   L.tiles = t;
@@ -512,6 +543,7 @@ GemmProb mkprob(const double* A, long long lda, const double* B, long long ldb, 
   p.X = nullptr; p.ldx = 0; p.logdet = nullptr; p.diag_col0 = 0; p.flag = nullptr;
   p.Ld = nullptr; p.ldd = 0;
   p.pre0 = p.pre1 = p.post = nullptr; p.pre0_n = p.pre1_n = 0;
+  p.ksplit = 1; p.part = nullptr; p.tcnt = nullptr;
   p.cpost = nullptr;
   return p;
 }
@@ -549,11 +581,11 @@ int build_plan(gpe_ctx* c, Fact& F) {
   //             x 128) over columns j > start(g): part h holds column start(g)+h+1
   //             (factored next) plus a balanced share of the columns after g.
   // the diagonal tile of step t with K pending columns (from Lp): the pending update runs
-  // as three G_DQUAD workgroups (dquad, pushed before the tile; none for K = 0) and the
+  // as DQ_N G_DQUAD workgroups (dquad, pushed before the tile; none for K = 0) and the
   // G_DIAG workgroup waits for them, loads the updated tile and factors it
   int* cnt_dq = F.flags + 4 * NB;
   auto dquad = [&](int t, const double* Lp, int K, double alpha) {
-    GemmProb p = mkprob(Lp, ld, nullptr, 0, tile(A, t, t), ld, 3, 1, K, G_DQUAD, alpha, 1.0);
+    GemmProb p = mkprob(Lp, ld, nullptr, 0, tile(A, t, t), ld, DQ_N, 1, K, G_DQUAD, alpha, 1.0);
     p.post = cnt_dq + t;
     p.diag_col0 = t * TILE;
     return p;
@@ -564,7 +596,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
     GemmProb p = mkprob(nullptr, ld, nullptr, ld, tile(A, t, t), ld, 1, 1, 0, G_DIAG, 1.0, 1.0);
     if (K > 0) {
       p.pre0 = cnt_dq + t;
-      p.pre0_n = 3;
+      p.pre0_n = DQ_N;
     }
     p.X = tile(B, t, t);
     p.ldx = ld;
@@ -791,7 +823,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
       }
       // assemble: diag(gb) (after its quadrants), early, bulk; step 0's panels at grp_p0
       // (its first beside the diagonal tile), step h's chain at grp_p0 + h grp_stride
-      const size_t head = gi > 0 ? 4 : 1;   // step 0: quadrants (when K > 0) and diagonal tile
+      const size_t head = gi > 0 ? DQ_N + 1 : 1;   // step 0: quadrant blocks (when K > 0) and diagonal tile
       std::vector<unsigned> base(seg[0].begin(), seg[0].begin() + head);
       base.insert(base.end(), early.begin(), early.end());
       base.insert(base.end(), bulkc.begin(), bulkc.end());
@@ -873,6 +905,8 @@ int build_plan(gpe_ctx* c, Fact& F) {
       fb += (double)b * T * b * T * a * T;
     }
     if (pa.empty()) continue;
+    split_k(pa, F.part, F.tcnt);
+    split_k(pb, F.part, F.tcnt);
     pl.trtri.push_back((int)pl.launches.size());
     add_launch(pl, 1, pa, fa);
     pl.trtri.push_back((int)pl.launches.size());
@@ -882,8 +916,9 @@ int build_plan(gpe_ctx* c, Fact& F) {
   pl.lauum = (int)pl.launches.size();
   {
     const double N = (double)F.n_pad;
-    add_launch(pl, 2, {mkprob(B, ld, B, ld, A, ld, NB, NB, (int)F.n_pad, G_CLOWER | G_KBEG_TI, 1.0, 0.0)},
-               N * N * N / 3.0);
+    std::vector<GemmProb> lp = {mkprob(B, ld, B, ld, A, ld, NB, NB, (int)F.n_pad, G_CLOWER | G_KBEG_TI, 1.0, 0.0)};
+    split_k(lp, F.part, F.tcnt);
+    add_launch(pl, 2, lp, N * N * N / 3.0);
   }
   const int limit = (F.desc_base == 0) ? AUX_DESC_BASE : ADHOC_DESC_BASE - AUX_DESC_BASE;
   if ((int)pl.probs.size() > limit) return fail(c, GPE_ERR_UNSUPPORTED, "GEMM schedule too large");
@@ -928,6 +963,11 @@ int ensure_fact(gpe_ctx* c, Fact& F, long long n_pad) {
     CHK(dalloc(c, &F.logdet, (size_t)F.NB));
     CHK(dalloc(c, &F.flags, FACT_FLAG_INTS * (size_t)F.NB));
     CHK(dalloc(c, &F.tflags, 2));   // k_trsv_lower: row counter, list ticket
+    if (!F.part) {
+      CHK(dalloc(c, &F.part, (size_t)SPLIT_SLOTS * TILE * TILE));
+      CHK(dalloc(c, &F.tcnt, (size_t)SPLIT_SLOTS));
+      HIPCHK(c, hipMemset(F.tcnt, 0, SPLIT_SLOTS * sizeof(int)));
+    }
     if (F.aug) CHK(dalloc(c, &F.Faug, (size_t)n_pad * TILE));
     F.plan = Plan();
   }
@@ -988,6 +1028,7 @@ int potrf(gpe_ctx* c, Fact& F, bool with_aug = false) {
   const int NB = F.NB;
   // flags, the group schedule's counters and the launches' list tickets start at zero
   HIPCHK(c, hipMemsetAsync(F.flags, 0, FACT_FLAG_INTS * (size_t)NB * sizeof(int), c->stream));
+  F.xdone = false;   // the sweep leaves only X's diagonal 16 x 16 blocks (ensure_xdiag)
   const bool wa = with_aug && pl.aug;
   const bool grp = c->potrf_group &&
                    (c->potrf_mode == 1 || (c->potrf_mode == 0 && g_inflight[c->device & 63].load() <= 1));
@@ -1026,8 +1067,20 @@ int lauum(gpe_ctx* c, Fact& F) {
   return launch_gemm_range(c, F.plan.launches[F.plan.lauum]);
 }
 
+// the full diagonal-tile inverses X_tt in B (k_xasm) after a sweep: the TRTRI's leaves and
+// the forward substitution's D_t
+int ensure_xdiag(gpe_ctx* c, Fact& F) {
+  if (F.xdone) return GPE_OK;
+  hipLaunchKernelGGL(k_xasm, dim3(F.NB), dim3(256), DB_LDS_DOUBLES * sizeof(double), c->stream, F.A, F.B,
+                     (long long)F.n_pad);
+  HIPCHK(c, hipGetLastError());
+  F.xdone = true;
+  return GPE_OK;
+}
+
 int trtri(gpe_ctx* c, Fact& F) {
   CHK(build_plan(c, F));
+  CHK(ensure_xdiag(c, F));
   for (int li : F.plan.trtri) CHK(launch_gemm_range(c, F.plan.launches[li]));
   return GPE_OK;
 }
@@ -1222,6 +1275,7 @@ int ensure_linv(gpe_ctx* c) {
 // Y = L^-1 R (n_pad x P, column-major) from the Cholesky factor in F.A and the diagonal
 // inverses in F.B: k_trsv_lower, one launch per TS_PM columns
 int trsv_lower(gpe_ctx* c, Fact& F, const double* R, long long ldr, int P, double* Y, long long ldy) {
+  CHK(ensure_xdiag(c, F));
   for (int c0 = 0; c0 < P; c0 += TS_PM) {
     const int pc = std::min(TS_PM, P - c0);
     HIPCHK(c, hipMemsetAsync(F.tflags, 0, 2 * sizeof(int), c->stream));   // the row counter and ticket
@@ -1364,7 +1418,9 @@ gpe_ctx* gpe_create(int32_t device) {
          hipFuncSetAttribute((const void*)k_gemm<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
          hipFuncSetAttribute((const void*)k_gemm<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
          hipFuncSetAttribute((const void*)k_gemm<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
-         hipFuncSetAttribute((const void*)k_gemm<false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess;
+         hipFuncSetAttribute((const void*)k_gemm<false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_xasm, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)(DB_LDS_DOUBLES * sizeof(double))) == hipSuccess;
     if (!ok) c->err = "hipFuncSetAttribute(max dynamic LDS) failed";
   }
   if (!ok) {
@@ -1392,6 +1448,10 @@ void gpe_destroy(gpe_ctx* c) {
   if (c->dK32) hipFree(c->dK32);
   if (c->tr.flags) hipFree(c->tr.flags);
   if (c->aux.flags) hipFree(c->aux.flags);
+  for (Fact* F : {&c->tr, &c->aux}) {
+    if (F->part) hipFree(F->part);
+    if (F->tcnt) hipFree(F->tcnt);
+  }
   if (c->tr.tflags) hipFree(c->tr.tflags);
   if (c->tr.Faug) hipFree(c->tr.Faug);
   if (c->aux.tflags) hipFree(c->aux.tflags);

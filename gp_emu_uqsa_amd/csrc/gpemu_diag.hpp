@@ -429,9 +429,12 @@ __device__ __forceinline__ int db_blk(int bi, int bk) { return (bi * (bi + 1) / 
 // on_factored(): called by every thread once L and X's diagonal blocks are stored (only
 // with a good factor), before the rest of X is assembled -- the fused Cholesky's panel
 // tiles need no more than those (their block substitution, k_gemm G_PANEL).
+// assemble = false: return there; the rest of X is assembled later, off the Cholesky's
+// chain, for all diagonal tiles at once (k_xasm: it reads L and the stored leaf inverses).
 template <class OnFactored>
 __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long long ldl, double* Xg,
-                                                long long ldx, double* logdet_out, OnFactored on_factored) {
+                                                long long ldx, double* logdet_out, OnFactored on_factored,
+                                                bool assemble = true) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   double* xs = lb + 36 * 256;             // current leaf inverse, column-major 16 x 16
   double* xdiag = lb + DB_LDS_DOUBLES;    // 128 diagonal entries of X
@@ -547,6 +550,12 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
   DB_TN(3);
   for (int b = wave; b < 8; b += 4) db_put_block<2>(lb, db_blk(b, b), xg_at(b, b), ldx);
   on_factored();
+  if (!assemble) {
+    DB_T(3);
+    DB_T(0);
+    DB_TFLUSH;
+    return 0;
+  }
   db_xlevel<16>(lb);
   db_put_block<0>(lb, db_blk(2 * wave + 1, 2 * wave), xg_at(2 * wave + 1, 2 * wave), ldx);
   db_xlevel<32>(lb);

@@ -193,10 +193,9 @@ static __global__ void __launch_bounds__(256) k_pairs_wide(PairArgs a) {
 // the same launch released *flag) solved against the factored diagonal tile by block
 // substitution: L = (C - L L^T) L_tt^-T (panel_subst; Ld / X point at L_tt and at
 // L_tt^-1's diagonal 16 x 16 blocks).
-// G_DQUAD: the pending update of a G_DIAG tile split over three workgroups, one per
-// 64 x 64 quadrant of its lower half (tiles ti = 0, 1, 2: quadrants (0,0), (1,0), (1,1);
-// dq_update); each posts *post when stored, and the G_DIAG workgroup (K = 0) waits for
-// all three, then loads the updated tile.
+// G_DQUAD: the pending update of a G_DIAG tile split over DQ_N = 10 workgroups, one per
+// 32 x 32 block of its lower half (dq_update); each posts *post when stored, and the
+// G_DIAG workgroup (K = 0) waits for all of them, then loads the updated tile.
 // G_PHALF0 / G_PHALF1 (with G_PANEL): every panel tile is two workgroups, one per 64-row
 // half of its substitution.  The G_PHALF0 workgroup runs the tile's pending update, stores
 // it and posts *cpost, then substitutes rows 0-63; the G_PHALF1 workgroup (K = 0) waits
@@ -231,6 +230,15 @@ struct GemmProb {
   int* post;
   int pre0_n, pre1_n;
   int* cpost;         // G_PHALF0: counted once the tile's pending update is stored
+  // split K (plain instances, beta = 0, implicit tile order): ksplit workgroups per tile,
+  // each over a contiguous share of the K stages; each stores its partial 128 x 128 sum
+  // in part (slot tile * ksplit + kpart) and counts itself in tcnt[tile]; the last to
+  // arrive adds the ksplit partials in index order (deterministic) and stores C, then
+  // resets the counter.  For launches with fewer tiles than the chip has slots (small n,
+  // the TRTRI's small levels): each tile's K loop on one CU is the launch's latency.
+  int ksplit;
+  double* part;
+  int* tcnt;
 };
 
 // dev-tool per-tile timeline (-DGEMM_TTRACE build only, tools/hip/tile_probe.hip): per
@@ -769,97 +777,78 @@ __device__ unsigned long long gemm_trace[8 * 4096];
 #define GTRACE(P, slot) do {} while (0)
 #endif
 
-// One 64 x 64 quadrant (qr, qc) of a diagonal tile's pending update, C -= L_r L_c^T over K
-// (L_r / L_c: rows 64 qr / 64 qc of the tile row's pending columns, A = their top-left,
-// column-major, lda), by one workgroup: the diagonal tile's update is on the Cholesky's
-// critical chain, and on one CU its 128 x 128 x K product (4.2 MFLOP at K = 128, ~14 us at
-// one CU's fp64 MFMA rate, plus the cold C preload) was the step's second-longest link.
-// Three workgroups take the lower half's quadrants at once (1 MFLOP each at K = 128).
-// Waves 2 x 2, 32 x 32 each; K staged 16 deep through a 4-slot LDS ring ([k][m] images,
-// pitch 64, global_load_lds: one wave instruction = two k rows of 64 doubles), three
-// chunks in flight (the operands were just written by other CUs: L2 misses).
-// The quadrant's C is loaded before the first chunk and added after the K loop.
-// Diagonal quadrants skip their upper-right 32 x 32 (never read: only the tile's lower
-// half is factored).
-constexpr int DQ_P = 64;               // image pitch (doubles)
-constexpr int DQ_IMG = GK * DQ_P;      // one operand image, 1024 doubles
-constexpr int DQ_SLOT = 2 * DQ_IMG;    // A + B
-constexpr int DQ_RING = 4;             // 64 KB of the 72 KB staging space
-static_assert(DQ_RING * DQ_SLOT <= G_LDS_DOUBLES, "dq ring");
+// One 32 x 32 block (qr, qc) of a diagonal tile's lower half (DQ_N = 10 of them, ti =
+// qr (qr + 1) / 2 + qc) of its pending update, C -= L_r L_c^T over K (L_r / L_c: rows
+// 32 qr / 32 qc of the tile row's pending columns, A = their top-left, column-major,
+// lda), by one workgroup: the diagonal tile's update is on the Cholesky's critical chain,
+// and on one CU its 128 x 128 x K product (4.2 MFLOP at K = 128, ~14 us at one CU's fp64
+// MFMA rate, plus the cold C preload) was the chain step's second-longest link; ten
+// workgroups take 0.26 MFLOP each.  Waves 2 x 2, 16 x 16 each.  K staged 64 deep through
+// two LDS slots ([k][m] images, pitch 32, global_load_lds: one wave instruction = four k
+// rows of 32 doubles); at K = 128 (the width-1 steps) both chunks are requested at once.
+// The block's C is loaded before the first chunk and added after the K loop; diagonal
+// blocks skip their upper-right 16 x 16 (never read: only the tile's lower half is factored).
+constexpr int DQ_N = 10;
+constexpr int DQ_KC = 64;              // k per chunk
+constexpr int DQ_P = 32;               // image pitch (doubles)
+constexpr int DQ_IMG = DQ_KC * DQ_P;   // one operand image, 2048 doubles
+constexpr int DQ_SLOT = 2 * DQ_IMG;    // A + B: 32 KB
+static_assert(2 * DQ_SLOT <= G_LDS_DOUBLES, "dq slots");
 __device__ __forceinline__ void dq_stage(const double* La, const double* Lb, long long lda, int k0, double* lds,
                                          int slot, int lane) {
   const int wave = gemm_wave();   // the LDS targets (M0) are wave-uniform
   double* As = lds + slot * DQ_SLOT;
   double* Bs = As + DQ_IMG;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {   // wave instruction w = 2 wave + h: k rows 2w, 2w + 1
-    const int w = 2 * wave + h;
-    const long long off = 2 * (lane & 31) + (long long)(k0 + 2 * w + (lane >> 5)) * lda;
-    glds16(La + off, As + w * 2 * DQ_P);
-    glds16(Lb + off, Bs + w * 2 * DQ_P);
+  for (int h = 0; h < 4; ++h) {   // wave instruction w = 4 wave + h: k rows 4w .. 4w + 3
+    const int w = 4 * wave + h;
+    const long long off = 2 * (lane & 15) + (long long)(k0 + 4 * w + (lane >> 4)) * lda;
+    glds16(La + off, As + w * 4 * DQ_P);
+    glds16(Lb + off, Bs + w * 4 * DQ_P);
   }
 }
 
 template <class Prob>
 __device__ __forceinline__ void dq_update(const Prob& P, int quad, double* lds) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int qr = quad >= 1 ? 1 : 0, qc = quad == 2 ? 1 : 0;
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
-  const bool skip = qr == qc && wm < wn;   // upper-right 32 x 32 of a diagonal quadrant
-  const double* La = P.A + 64 * qr;
-  const double* Lb = P.A + 64 * qc;
-  double* Cq = P.C + 64 * qr + (long long)(64 * qc) * P.ldc;
-  const int nk = P.K / GK;
-  // this wave's C (2 x 2 blocks, 4 values each), in flight while the operands stream in
-  double cv[2][2][4];
+  int qr = 0;
+  while ((qr + 1) * (qr + 2) / 2 <= quad) ++qr;
+  const int qc = quad - qr * (qr + 1) / 2;
+  const int wm = (wave >> 1) * 16, wn = (wave & 1) * 16;
+  const bool skip = qr == qc && wm < wn;   // upper-right 16 x 16 of a diagonal block
+  const double* La = P.A + 32 * qr;
+  const double* Lb = P.A + 32 * qc;
+  double* Cq = P.C + 32 * qr + (long long)(32 * qc) * P.ldc;
+  const int nk = P.K / DQ_KC;   // K is a multiple of 128
+  double cv[4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        cv[i][j][r] = gld1(Cq + (wm + 16 * i + (lane & 15)) + (long long)(wn + 16 * j + mfma64_row(lane, r)) * P.ldc);
-  for (int c = 0; c < 3 && c < nk; ++c) dq_stage(La, Lb, P.lda, c * GK, lds, c, lane);
-  d4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int r = 0; r < 4; ++r) cv[r] = gld1(Cq + (wm + (lane & 15)) + (long long)(wn + mfma64_row(lane, r)) * P.ldc);
+  dq_stage(La, Lb, P.lda, 0, lds, 0, lane);
+  if (nk > 1) dq_stage(La, Lb, P.lda, DQ_KC, lds, 1, lane);
+  d4 acc = d4{0.0, 0.0, 0.0, 0.0};
   for (int c = 0; c < nk; ++c) {
-    // chunk c landed (4 loads per wave per chunk; the later chunks may stay in flight)
-    const int ahead = min(2, nk - 1 - c);
-    if (ahead == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    // chunk c landed (8 loads per wave per chunk; chunk c + 1 may stay in flight)
+    if (c + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();   // every wave's pieces of chunk c; every wave is done with chunk c - 1
-    if (c + 3 < nk) dq_stage(La, Lb, P.lda, (c + 3) * GK, lds, (c + 3) % DQ_RING, lane);
-    const double* As = lds + (c % DQ_RING) * DQ_SLOT;
+    __syncthreads();   // every wave's pieces of chunk c
+    const double* As = lds + (c & 1) * DQ_SLOT;
     const double* Bs = As + DQ_IMG;
     if (!skip) {
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
+      for (int ks = 0; ks < DQ_KC / 4; ++ks) {
         const int krow = 4 * ks + (lane >> 4);
-        double af[2], bf[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) af[i] = As[krow * DQ_P + wm + 16 * i + (lane & 15)];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) bf[j] = Bs[krow * DQ_P + wn + 16 * j + (lane & 15)];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(bf[j], af[i], acc[i][j], 0, 0, 0);
+        const double af = As[krow * DQ_P + wm + (lane & 15)];
+        const double bf = Bs[krow * DQ_P + wn + (lane & 15)];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(bf, af, acc, 0, 0, 0);
       }
     }
+    __syncthreads();   // every wave is done with slot c & 1
+    if (c + 2 < nk) dq_stage(La, Lb, P.lda, (c + 2) * DQ_KC, lds, c & 1, lane);
   }
   if (skip) return;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        gst1(Cq + (wm + 16 * i + (lane & 15)) + (long long)(wn + 16 * j + mfma64_row(lane, r)) * P.ldc,
-             P.beta * cv[i][j][r] + P.alpha * acc[i][j][r]);
+  for (int r = 0; r < 4; ++r)
+    gst1(Cq + (wm + (lane & 15)) + (long long)(wn + mfma64_row(lane, r)) * P.ldc, P.beta * cv[r] + P.alpha * acc[r]);
 }
 
 // Panel tile of the fused Cholesky by block substitution: P = C L^-T for a 128 x 128
@@ -1024,8 +1013,14 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
     p = lo;
   }
   const GemmProb P = probs[p];
+  int kpart = 0, tl = 0;   // split K: this workgroup's share and its tile's index in the problem
   if (!tiles) {
-    const int local = (int)pos - P.tile_begin;
+    int local = (int)pos - P.tile_begin;
+    if (!FUSED && P.ksplit > 1) {
+      kpart = local % P.ksplit;
+      local /= P.ksplit;
+      tl = local;
+    }
     if (P.flags & G_CLOWER) {
       tri_decode(local, ti, tj);
     } else if ((P.flags & G_KEND_TI) && nprob == 1) {
@@ -1048,6 +1043,12 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
   int kbeg = 0, kend = P.K;
   if (P.flags & G_KBEG_TI) kbeg = ti * TILE;
   if (P.flags & G_KEND_TI) kend = min(kend, (ti + 1) * TILE);
+  if (!FUSED && P.ksplit > 1) {   // this share of the tile's K stages
+    const int ns = max(0, kend - kbeg) / GK;
+    const int s0 = kpart * ns / P.ksplit, s1 = (kpart + 1) * ns / P.ksplit;
+    kend = kbeg + s1 * GK;
+    kbeg += s0 * GK;
+  }
 
   const int tid = threadIdx.x;
   if constexpr (FUSED) {
@@ -1174,7 +1175,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
           __syncthreads();
           if (tid == 0) { gemm_publish_flag(P.flag, 1); GTRACE(P, 2); }
         }
-      });
+      }, P.flag == nullptr);   // the single-GPU sweep (with flags) assembles X later (k_xasm)
       if (bad && tid == 0 && abort_flag) atomicCAS(abort_flag, 0, P.diag_col0 + bad);
       if (P.flag && bad) {   // (on_factored is not called for a bad factor)
         __syncthreads();
@@ -1222,6 +1223,44 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
       return;
     }
   }
+  if constexpr (!FUSED) {
+    if (P.ksplit > 1) {
+      // partial out (value-major: coalesced across the workgroup), count, and the last
+      // workgroup of the tile sums the partials in index order
+      const int ks = P.ksplit;
+      double* slot = P.part + ((long long)tl * ks + kpart) * (TILE * TILE);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) gst1(slot + ((i * 4 + j) * 4 + r) * 256 + tid, acc[i][j][r]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      int* last = reinterpret_cast<int*>(lds + G_LDS_LAUNCH_DOUBLES - 3);
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        *last = __hip_atomic_fetch_add(P.tcnt + tl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ks - 1;
+      }
+      __syncthreads();
+      if (!*last) return;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const double* p0 = P.part + (long long)tl * ks * (TILE * TILE);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int e = ((i * 4 + j) * 4 + r) * 256 + tid;
+            double sum = gld1(p0 + e);
+            for (int c = 1; c < ks; ++c) sum += gld1(p0 + (long long)c * (TILE * TILE) + e);
+            acc[i][j][r] = sum;
+          }
+      if (tid == 0) __hip_atomic_store(P.tcnt + tl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   gemm_store<!FUSED>(Cb, P.ldc, P.alpha, acc);
   if constexpr (FUSED) {
     if (P.post) gemm_post_count(P.post);
@@ -1231,6 +1270,34 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
   __syncthreads();
   TTRACE(3);
 #endif
+}
+
+// X_tt = L_tt^-1 for every diagonal tile t (blockIdx.x) of a factorisation, after the
+// fused Cholesky (whose diagonal workgroups store L and the eight 16 x 16 leaf inverses,
+// release the panel tiles and stop there: db_factor_invert(assemble = false)).  The
+// assembly (db_xlevel at 16, 32, 64) was ~12 us of each step's diagonal workgroup, which
+// in the width-1 steps outlived the panel substitution and held the launch open; here it
+// runs once for all tiles, off the chain.  X's strictly-upper blocks are already zero.
+static __global__ void __launch_bounds__(256) k_xasm(const double* __restrict__ A, double* __restrict__ B,
+                                                     long long ld) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const long long t0 = (long long)blockIdx.x * TILE * (ld + 1);
+  const double* L = A + t0;
+  double* X = B + t0;
+  for (int e = threadIdx.x; e < 36 * 256; e += 256) {
+    const int b = e >> 8, w = e & 255, bi = tri_row(b), bk = b - bi * (bi + 1) / 2;
+    const long long g = (bi * 16 + (w & 15)) + (long long)(bk * 16 + (w >> 4)) * ld;
+    lds[e] = gld1((bi == bk ? X : L) + g);   // leaf inverse (lower, stored with zeros above) / L block
+  }
+  __syncthreads();
+  db_xlevel<16>(lds);
+  db_xlevel<32>(lds);
+  db_xlevel<64>(lds);
+  const int wave = threadIdx.x >> 6;
+  for (int b = wave; b < 36; b += 4) {
+    const int bi = tri_row(b), bk = b - bi * (bi + 1) / 2;
+    if (bi != bk) db_put_block<0>(lds, b * 256, X + bi * 16 + (long long)(bk * 16) * ld, ld);
+  }
 }
 
 // ---------------------------------------------------------------------------
