@@ -18,10 +18,10 @@
 //             (k_gemm, tile list, K = 128 (ge-gb))
 //
 // Gradient (want_grad), same partition, no n x n collective, O(n^2 / P) memory:
-//   X = L^-1 by rows, right-looking: step k, owner(k) finishes its row
-//     X(k, 0:k) = Dinv_k R(k, 0:k)  (X(k,k) = Dinv_k kept from the sweep),
-//     broadcasts X(k, 0:k+1), every rank updates its rows i > k:
-//     R(i, 0:k+1) -= L(i,k) X(k, 0:k+1)                      (k_gemm)
+//   X = L^-1 by the single-GPU path's recursive TRTRI (block pairs, levels of doubling
+//     width), each level's two GEMMs over each rank's own tile rows: M^T = X11^T L21^T
+//     after an all-gather of X11, X21 = -X22 M after an all-gather of M (in column
+//     chunks that fit the slab; X(k,k) = Dinv_k kept from the sweep).
 //   A^-1 = X^T X = sum_r X_r^T X_r over each rank's rows.  The contraction
 //   <M, dA/dtheta> is linear in A^-1, so rank r contracts its own partial X_r^T X_r,
 //   formed slab by slab (a few tile rows of the lower triangle at a time, never the
@@ -32,8 +32,7 @@
 // all-gather) runs on a critical stream; the group's trailing update is split into
 // the next group's columns (queued first) and the rest, on the compute stream.  The
 // next group's chain waits only for the first part, so its collectives overlap the
-// rest of the update.  The panel buffer (and the TRTRI's group rows, organised the
-// same way by rows) is double-buffered by group parity.
+// rest of the update.  The panel buffer is double-buffered by group parity.
 //
 // Every logical rank owns all of its buffers (tile rows, Dinv, panel, all-gather
 // buffer, Gram, log-det, X rows, broadcast row, W, slab, sums).  The two transports
@@ -82,10 +81,11 @@ __global__ void __launch_bounds__(256) k_dist_kbuild(DistPairArgs a) {
   if (tj > gt) return;
   const int tid = threadIdx.x, r = tid & (TILE - 1);
   double* out = a.out + (long long)li * TILE + (long long)tj * TILE * a.ld;
-  if (gt == a.NB) {
+  if (gt >= a.NB) {   // augmented tile row u = gt - NB: [f H] columns 128 u .., transposed
+    const int pr = r + (gt - a.NB) * TILE;
     for (int c = tid >> 7; c < TILE; c += 2) {
       const int gj = tj * TILE + c;
-      const double v = (tj < a.NB && r < a.Pc) ? a.F[gj + (long long)r * a.ldF] : 0.0;
+      const double v = (tj < a.NB && pr < a.Pc) ? a.F[gj + (long long)pr * a.ldF] : 0.0;
       out[r + (long long)c * a.ld] = v;
     }
     return;
@@ -130,10 +130,11 @@ __global__ void __launch_bounds__(256) k_dist_kbuild_wide(DistPairArgs a) {
   if (tj > gt) return;
   const int tid = threadIdx.x, r = tid & (TILE - 1), h = tid >> 7;
   double* out = a.out + (long long)li * TILE + (long long)tj * TILE * a.ld;
-  if (gt == a.NB) {
+  if (gt >= a.NB) {   // augmented tile row u = gt - NB: [f H] columns 128 u .., transposed
+    const int pr = r + (gt - a.NB) * TILE;
     for (int c = h; c < TILE; c += 2) {
       const int gj = tj * TILE + c;
-      const double v = (tj < a.NB && r < a.Pc) ? a.F[gj + (long long)r * a.ldF] : 0.0;
+      const double v = (tj < a.NB && pr < a.Pc) ? a.F[gj + (long long)pr * a.ldF] : 0.0;
       out[r + (long long)c * a.ld] = v;
     }
     return;
@@ -207,13 +208,14 @@ __global__ void __launch_bounds__(256) k_dist_unpermute(const double* recv, long
   }
 }
 
-// Z = L^-1 [f H] (n_pad x Pc, column-major) out of the augmented tile row (local row li)
+// columns p0 .. p0+pc of Z = L^-1 [f H] (n_pad x Pc, column-major) out of an augmented
+// tile row (local row li)
 __global__ void __launch_bounds__(256) k_dist_take_z(const double* Aloc, long long ld, int li, long long np,
-                                                     int Pc, double* Z) {
+                                                     int p0, int pc, double* Z) {
   const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
   if (j >= np) return;
   const double* src = Aloc + (long long)li * TILE + j * ld;
-  for (int p = 0; p < Pc; ++p) Z[j + p * np] = src[p];
+  for (int p = 0; p < pc; ++p) Z[j + (p0 + p) * np] = src[p];
 }
 
 // rows of R2 (n_pad x Pc) at rank `rank`'s tile rows -> out (local rows, ld ldo)
@@ -232,6 +234,46 @@ __global__ void __launch_bounds__(256) k_dist_add(double* dst, const double* src
     dst[e] += src[e];
 }
 
+// Tile moves of the recursive TRTRI's gathers: dst tile (ti, tj) of a rows x cols block
+// <- src.  perm = 0: src tile (ti, tj).  perm = 1 (2): the block's tile rows (columns) are
+// the global tile rows g = g0 + ti (g0 + tj), which arrive by rank, in the all-gather
+// segment of g's owner (g mod P, seg doubles apart), as that rank's j-th such row:
+// src tile (j, tj) ((ti, j)) of that segment.
+struct MoveDesc {
+  const double* src;
+  double* dst;
+  long long lds, ldd, seg;
+  int rows, cols, tile_begin, perm, g0, P;
+};
+
+__global__ void __launch_bounds__(256) k_dist_move(const MoveDesc* __restrict__ d, int nd) {
+  int lo = 0, hi = nd - 1;   // last descriptor whose tile_begin <= blockIdx.x
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((int)blockIdx.x >= d[mid].tile_begin) lo = mid;
+    else hi = mid - 1;
+  }
+  const MoveDesc D = d[lo];
+  const int local = (int)blockIdx.x - D.tile_begin;
+  const int ti = local % D.rows, tj = local / D.rows;
+  int si = ti, sj = tj;
+  const double* s = D.src;
+  if (D.perm) {
+    const int g = D.g0 + (D.perm == 1 ? ti : tj), r = g % D.P;
+    const int first = D.g0 + (r - D.g0 % D.P + D.P) % D.P;   // the owner's first row >= g0
+    const int j = (g - first) / D.P;
+    s += (long long)r * D.seg;
+    (D.perm == 1 ? si : sj) = j;
+  }
+  s += (long long)si * TILE + (long long)sj * TILE * D.lds;
+  double* o = D.dst + (long long)ti * TILE + (long long)tj * TILE * D.ldd;
+  for (int e = threadIdx.x; e < TILE * TILE / 2; e += 256) {
+    const int i = (e & 63) * 2, c = e >> 6;
+    *reinterpret_cast<double2*>(o + i + (long long)c * D.ldd) =
+        *reinterpret_cast<const double2*>(s + i + (long long)c * D.lds);
+  }
+}
+
 struct Rank {              // one rank's buffers (one per process over RCCL, P in loopback)
   int rank = 0, nloc = 0;
   long long ld = 0;
@@ -244,15 +286,15 @@ struct Rank {              // one rank's buffers (one per process over RCCL, P i
   double* recv = nullptr;  // all-gather buffer, P segments of the largest panel
   double* gram = nullptr;  // Pc x Pc
   // gradient
-  double* X = nullptr;     // L^-1 rows, ld as A, NB*128 columns
-  double* xrow = nullptr;  // 128 x n_pad: X(k, 0:k+1), broadcast per step
-  double* xgrp = nullptr;  // 2 x wmax*128 x n_pad (ld wmax*128): a group's X rows (by group
-                           // parity), zero right of each row's diagonal tile within the group
+  double* X = nullptr;     // L^-1 rows, ld as A, NB*128 columns (zero above the diagonal)
+  double* g1 = nullptr;    // P > 1: a TRTRI chunk's gathered X11 blocks (global row order)
+  double* trecv = nullptr; // P > 1: the TRTRI's all-gather buffer (X11 rows, then M^T columns)
   double* dZ = nullptr;    // n_pad x Pc: L^-1 [f H] (broadcast)
   double* dR2 = nullptr;   // n_pad x Pc
   double* r2loc = nullptr; // local rows of R2, 128 columns (zero beyond Pc)
   double* wpart = nullptr; // n_pad x 128: [sqrt(c) alpha, W] (all-reduced)
   double* slab = nullptr;  // slab*128 x n_pad: tile rows of this rank's partial X_r^T X_r
+                           // (first, the TRTRI chunks' M^T blocks)
   double* csum = nullptr;  // d+3 contraction sums (all-reduced)
   size_t bytes = 0;        // device bytes held for this rank
 };
@@ -260,8 +302,17 @@ struct Rank {              // one rank's buffers (one per process over RCCL, P i
 struct DLaunch {           // one grouped k_gemm launch
   int first = 0, count = 0, tiles = 0;
   long long list = -1;
-  int kind = 0;            // 0 <false,false>, 1 <false,true>, 2 <true,true>
+  int kind = 0;            // 0 <false,false>, 1 <false,true>, 2 <true,true>, 3 <true,false>
   bool cdef = false;       // k_gemm's CDEF instance (gemm_cdef of some problem)
+};
+
+// one column chunk of one level of the recursive TRTRI (see ensure_grad)
+struct TriChunk {
+  DLaunch m, x;            // M^T = X11^T L21^T ; X21 = -X22 M
+  int pack0 = 0, npack = 0, pack_tiles = 0;   // P > 1: move descriptors and their tiles
+  int unp1 = 0, nunp1 = 0, unp1_tiles = 0;
+  int unp2 = 0, nunp2 = 0, unp2_tiles = 0;
+  size_t seg1 = 0, seg2 = 0;                  // all-gather segments (doubles)
 };
 
 struct SlabLaunch {        // one slab of a rank's partial of A^-1: GEMM + contraction
@@ -289,6 +340,7 @@ struct gpe_dist {
 
   long long n = 0, n_pad = 0;
   int d = 0, q = 0, NB = 0;
+  int NA = 1;              // augmented tile rows NB .. NB+NA-1: [f H]^T, 128 basis columns each
   bool has_r = false;
   // replicated inputs (one copy shared by the loopback ranks)
   double* dX = nullptr;    // n_pad x d raw
@@ -330,7 +382,9 @@ struct gpe_dist {
   int slab_rows = 1;                           // tile rows per slab of A^-1
   double* dT2 = nullptr;
   GemmProb* gprobs = nullptr;
-  std::vector<DLaunch> tri_p, tri_x, tri_un, tri_ur, wa_l;
+  std::vector<DLaunch> wa_l;
+  std::vector<TriChunk> tri;                   // the recursive TRTRI, level by level
+  MoveDesc* dmoves = nullptr;
   std::vector<std::vector<SlabLaunch>> slabs;  // per local rank
 };
 
@@ -384,7 +438,7 @@ int dalloc(gpe_dist* h, T** p, size_t count, size_t* acct = nullptr) {
 }
 
 void free_rank(Rank& R) {
-  double** bufs[] = {&R.A, &R.logdet, &R.dinv, &R.panel, &R.recv, &R.gram, &R.X, &R.xrow, &R.xgrp,
+  double** bufs[] = {&R.A, &R.logdet, &R.dinv, &R.panel, &R.recv, &R.gram, &R.X, &R.g1, &R.trecv,
                      &R.dZ, &R.dR2, &R.r2loc, &R.wpart, &R.slab, &R.csum};
   for (double** b : bufs) dfree(b);
   R.bytes = 0;
@@ -550,8 +604,8 @@ double* panel_of(const gpe_dist* h, const Rank& R, int k) {
 
 // every per-step GEMM descriptor and tile list, for the current n and partition
 int build_schedule(gpe_dist* h) {
-  const int NB = h->NB, P = h->P;
-  const long long ldp = (long long)(NB + 1) * TILE;
+  const int NB = h->NB, P = h->P, NT = NB + h->NA;
+  const long long ldp = (long long)NT * TILE;
   std::vector<GemmProb> probs;
   std::vector<unsigned> tiles;
   h->diag.assign(NB, DLaunch());
@@ -565,7 +619,7 @@ int build_schedule(gpe_dist* h) {
     const int Kp = (k - gb) * TILE;   // pending columns [gb, k)
     for (int r = 0; r < P; ++r) {
       li0[(size_t)k * P + r] = li0_of(k, P, r);
-      cnt[(size_t)k * P + r] = std::max(0, nloc_of(NB, P, r) - li0_of(k, P, r));
+      cnt[(size_t)k * P + r] = std::max(0, nloc_of(NT - 1, P, r) - li0_of(k, P, r));
       h->maxT[k] = std::max(h->maxT[k], cnt[(size_t)k * P + r]);
     }
     // diagonal tile: owner's local row k / P, column k, less the pending update
@@ -627,7 +681,7 @@ int build_schedule(gpe_dist* h) {
     if (k + 1 != ge) continue;
     const int ge2 = next_group_end(h, k);
     for (int part = 0; part < 2; ++part) {
-      const int j0 = part == 0 ? ge : ge2, j1 = part == 0 ? ge2 : NB + 1;   // columns [j0, j1)
+      const int j0 = part == 0 ? ge : ge2, j1 = part == 0 ? ge2 : NT;   // columns [j0, j1)
       DLaunch ul;
       ul.first = (int)probs.size();
       ul.list = (long long)tiles.size();
@@ -636,7 +690,7 @@ int build_schedule(gpe_dist* h) {
         const int a = li0_of(k, P, R.rank);
         if (a >= R.nloc) continue;
         GemmProb p = dprob(R.A + (long long)gb * TILE * R.ld, R.ld, panel_of(h, R, k), ldp, R.A, R.ld,
-                           R.nloc, NB + 1, (ge - gb) * TILE, 0, -1.0, 1.0);
+                           R.nloc, NT, (ge - gb) * TILE, 0, -1.0, 1.0);
         for (int li = a; li < R.nloc; ++li) {
           const int gt = li * P + R.rank;
           for (int j = j0; j < j1 && j <= gt; ++j)
@@ -676,6 +730,7 @@ int launch(gpe_dist* h, const DLaunch& L, const GemmProb* base = nullptr) {
     switch (L.kind) {
       case 1: hipLaunchKernelGGL((k_gemm<false, true, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
       case 2: hipLaunchKernelGGL((k_gemm<true, true, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
+      case 3: hipLaunchKernelGGL((k_gemm<true, false, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
       default:   // kind 0 launches may carry G_DIAG / G_PANEL problems
         hipLaunchKernelGGL((k_gemm<false, false, true, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
     }
@@ -683,6 +738,7 @@ int launch(gpe_dist* h, const DLaunch& L, const GemmProb* base = nullptr) {
     switch (L.kind) {
       case 1: hipLaunchKernelGGL((k_gemm<false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
       case 2: hipLaunchKernelGGL((k_gemm<true, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
+      case 3: hipLaunchKernelGGL((k_gemm<true, false>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
       default:   // kind 0 launches may carry G_DIAG / G_PANEL problems
         hipLaunchKernelGGL((k_gemm<false, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
     }
@@ -699,86 +755,161 @@ int ensure_grad(gpe_dist* h) {
   if (h->grad_ready) return GPE_OK;
   const int NB = h->NB, P = h->P, Pc = h->q + 1, d = h->d;
   const long long np = h->n_pad;
-  // slab of the A^-1 partial: as many tile rows as fit SLAB_DOUBLES
-  h->slab_rows = (int)std::max<long long>(1, std::min<long long>(NB, (long long)SLAB_DOUBLES / (TILE * np)));
+  // slab of the A^-1 partial (and the TRTRI's gathered blocks): as many tile rows as
+  // fit SLAB_DOUBLES, or GPEMU_DIST_SLAB_MB MiB (at least one tile row)
+  long long slab_doubles = (long long)SLAB_DOUBLES;
+  if (const char* e = std::getenv("GPEMU_DIST_SLAB_MB")) slab_doubles = std::max(1ll, std::atoll(e)) << 17;
+  h->slab_rows = (int)std::max<long long>(1, std::min<long long>(NB, slab_doubles / (TILE * np)));
   const long long lds = (long long)h->slab_rows * TILE;
   for (Rank& R : h->ranks) {
     R.nlx = R.rank <= NB - 1 ? (NB - 1 - R.rank) / P + 1 : 0;
     DCHK(dalloc(h, &R.X, (size_t)R.ld * NB * TILE, &R.bytes));
-    DCHK(dalloc(h, &R.xrow, (size_t)TILE * np, &R.bytes));
-    DCHK(dalloc(h, &R.xgrp, 2 * (size_t)h->wmax * TILE * np, &R.bytes));
     DCHK(dalloc(h, &R.dZ, (size_t)np * Pc, &R.bytes));
     DCHK(dalloc(h, &R.dR2, (size_t)np * Pc, &R.bytes));
-    DCHK(dalloc(h, &R.r2loc, (size_t)R.ld * TILE, &R.bytes));
-    DCHK_HIP(h, hipMemset(R.r2loc, 0, (size_t)R.ld * TILE * sizeof(double)));
-    DCHK(dalloc(h, &R.wpart, (size_t)np * TILE, &R.bytes));
+    DCHK(dalloc(h, &R.r2loc, (size_t)R.ld * h->NA * TILE, &R.bytes));
+    DCHK_HIP(h, hipMemset(R.r2loc, 0, (size_t)R.ld * h->NA * TILE * sizeof(double)));
+    DCHK(dalloc(h, &R.wpart, (size_t)np * h->NA * TILE, &R.bytes));
     DCHK(dalloc(h, &R.slab, (size_t)lds * np, &R.bytes));
     DCHK(dalloc(h, &R.csum, (size_t)d + 3, &R.bytes));
   }
   DCHK(dalloc(h, &h->dT2, (size_t)Pc * Pc, &h->shared_bytes));
   DCHK(dalloc(h, &h->cpart, (size_t)NB * (NB + 1) / 2 * (d + 3), &h->shared_bytes));
 
-  // Rows of X = L^-1 in the Cholesky's column groups [gb, ge): the owner of row k first
-  // applies the pending rows gb..k-1 of its group, R(k, 0:k) -= L(k, gb:k) X(gb:k, 0:k)
-  // (K = 128 (k-gb), the group's broadcast rows held in xgrp), then finishes
-  // X(k, 0:k) = Dinv_k R(k, 0:k); the step closing a group updates every rank's rows
-  // i >= ge with the whole group, R(i, 0:ge) -= L(i, gb:ge) X(gb:ge, 0:ge), K = 128 W.
+  // X = L^-1 by the recursive TRTRI of the single-GPU path (gpemu.hip build_plan), level
+  // by level (block pairs [t0, h), [h, t1) of s tile columns, s = 2, 4, ...; the
+  // diagonal tiles X(t,t) = Dinv_t were kept from the sweep), on the tile rows each rank
+  // owns:
+  //   M^T = X11^T L21^T  X11 = X(t0:h, t0:h) gathered from every rank, L21 the rank's
+  //                      rows of L(h:t1, t0:h): its columns of M^T (its rows of M)
+  //   X21 = -X22 M       M gathered; the rank's rows of X22 (finished a level earlier)
+  // in column chunks [c0, c0 + cw) of [t0, h), as wide as the gathered blocks fit the
+  // slab (X11's rows c0:h of the chunk's columns, M^T's chunk rows).  Two all-gathers
+  // per chunk; none at P = 1, where X11 is read in place and M^T lands in the slab.
   std::vector<GemmProb> probs;
-  const long long ldx = (long long)h->wmax * TILE;
-  const size_t xg_sz = (size_t)ldx * np;
-  auto xgrp_of = [&](const Rank& R, int k) { return R.xgrp + (size_t)(h->gid[k] & 1) * xg_sz; };
-  h->tri_p.assign(NB, DLaunch());
-  h->tri_x.assign(NB, DLaunch());
-  h->tri_un.assign(NB, DLaunch());
-  h->tri_ur.assign(NB, DLaunch());
-  for (int k = 0; k < NB; ++k) {
-    const int lk = k / P;
-    const int gb = h->gstart[k], ge = group_end(h, k), w = k - gb;
-    Rank* O = rank_slot(h, k % P);
-    if (O && k > 0) {
-      double* row = O->X + (long long)lk * TILE;
-      if (w > 0) {
-        GemmProb p = dprob(O->A + (long long)lk * TILE + (long long)gb * TILE * O->ld, O->ld, xgrp_of(*O, k), ldx,
-                           row, O->ld, 1, k, w * TILE, 0, -1.0, 1.0);
-        p.ntiles = k;
-        DLaunch L;
-        L.first = (int)probs.size(); L.count = 1; L.tiles = k; L.kind = 1;
-        L.cdef = gemm_cdef(p);
-        h->tri_p[k] = L;
-        probs.push_back(p);
-      }
-      // X(k, 0:k) = Dinv_k R(k, 0:k) with R(k, c) = -sum_{j<k} L(k,j) X(j,c), in place
-      // (each output tile reads only itself)
-      GemmProb p = dprob(row + (long long)k * TILE * O->ld, O->ld, row, O->ld, row, O->ld, 1, k, TILE, 0, 1.0, 0.0);
-      p.ntiles = k;
-      DLaunch L;
-      L.first = (int)probs.size(); L.count = 1; L.tiles = k; L.kind = 1;
-      h->tri_x[k] = L;
-      probs.push_back(p);
+  std::vector<MoveDesc> moves;
+  h->tri.clear();
+  const long long cap = lds * np, T2 = (long long)TILE * TILE;
+  struct Pair { int t0, h, t1; };
+  std::vector<std::pair<int, int>> lev;   // per level: {s, chunk width}
+  long long g1_need = 0, rv_need = 0;
+  for (int s = 2; s / 2 < NB; s *= 2) {
+    const int a = s / 2;
+    long long g1 = 0, s1 = 0, g2 = 0, s2 = 0;   // per unit of chunk width
+    for (int t0 = 0; t0 + a < NB; t0 += s) {
+      const int b = std::min(t0 + s, NB) - (t0 + a);
+      g1 += a; s1 += (a + P - 1) / P; g2 += b; s2 += (b + P - 1) / P;
     }
-    if (k + 1 != ge) continue;
-    // the group's rows applied to every rank's rows below it, in two launches: the
-    // rows of the next group (its chain waits for these only), then the rest
-    const int ge2 = next_group_end(h, k);
-    for (int part = 0; part < 2; ++part) {
-      const int r0 = part == 0 ? ge : ge2, r1 = part == 0 ? ge2 : NB;   // global tile rows [r0, r1)
-      DLaunch ul;
-      ul.first = (int)probs.size();
-      ul.kind = 1;
-      for (Rank& R : h->ranks) {
-        const int a = lstart_of(r0, P, R.rank), b = std::min(R.nlx, lstart_of(r1, P, R.rank)), c = b - a;
-        if (c <= 0) continue;
-        GemmProb p = dprob(R.A + (long long)a * TILE + (long long)gb * TILE * R.ld, R.ld, xgrp_of(R, k), ldx,
-                           R.X + (long long)a * TILE, R.ld, c, ge, (ge - gb) * TILE, 0, -1.0, 1.0);
-        p.tile_begin = ul.tiles;
-        p.ntiles = c * ge;
-        ul.tiles += p.ntiles;
-        ul.cdef = ul.cdef || gemm_cdef(p);
-        probs.push_back(p);
-        ++ul.count;
-      }
-      (part == 0 ? h->tri_un : h->tri_ur)[k] = ul;
+    int cc = a;
+    auto fits = [&](long long w) {
+      return g2 * w * T2 <= cap && (P == 1 || (g1 * w * T2 <= cap && P * s1 * w * T2 <= cap && P * s2 * w * T2 <= cap));
+    };
+    while (cc > 1 && !fits(cc)) cc = (cc + 1) / 2;
+    if (!fits(cc)) return dfail(h, GPE_ERR_UNSUPPORTED, "distributed TRTRI blocks exceed the slab");
+    lev.push_back({s, cc});
+    if (P > 1) {
+      g1_need = std::max(g1_need, g1 * cc * T2);
+      rv_need = std::max({rv_need, P * s1 * cc * T2, P * s2 * cc * T2});
     }
+  }
+  for (Rank& R : h->ranks) {
+    DCHK(dalloc(h, &R.g1, (size_t)g1_need, &R.bytes));
+    DCHK(dalloc(h, &R.trecv, (size_t)rv_need, &R.bytes));
+  }
+  for (const auto& lv : lev) {
+    const int s = lv.first, a = s / 2, cc = lv.second;
+    std::vector<Pair> pairs;
+    for (int t0 = 0; t0 + a < NB; t0 += s) pairs.push_back({t0, t0 + a, std::min(t0 + s, NB)});
+    for (int j0 = 0; j0 < a; j0 += cc) {
+      const int cw = std::min(cc, a - j0), rows1 = a - j0, mx1 = (rows1 + P - 1) / P;
+      TriChunk tc;
+      // per pair: offsets in the all-gather segments (o1, o2) and the gathered blocks (og1, og2)
+      std::vector<long long> o1, og1, o2, og2;
+      long long s1 = 0, gg1 = 0, s2 = 0, gg2 = 0;
+      for (const Pair& pr : pairs) {
+        const int b = pr.t1 - pr.h;
+        o1.push_back(s1 * T2); s1 += (long long)mx1 * cw;
+        og1.push_back(gg1 * T2); gg1 += (long long)rows1 * cw;
+        o2.push_back(s2 * T2); s2 += (long long)cw * ((b + P - 1) / P);
+        og2.push_back(gg2 * T2); gg2 += (long long)cw * b;
+      }
+      tc.seg1 = (size_t)(s1 * T2);
+      tc.seg2 = (size_t)(s2 * T2);
+      auto add_move = [&](MoveDesc m, int& tiles) {
+        if (m.rows <= 0 || m.cols <= 0) return;
+        m.tile_begin = tiles;
+        tiles += m.rows * m.cols;
+        moves.push_back(m);
+      };
+      if (P > 1) {   // the rank's rows c0:h of X11's chunk columns into its segment, then out by rows
+        tc.pack0 = (int)moves.size();
+        for (Rank& R : h->ranks)
+          for (size_t p = 0; p < pairs.size(); ++p) {
+            const int c0 = pairs[p].t0 + j0, ls = lstart_of(c0, P, R.rank);
+            const int nown = std::min(R.nlx, lstart_of(pairs[p].h, P, R.rank)) - ls;
+            add_move({R.X + (long long)ls * TILE + (long long)c0 * TILE * R.ld, R.trecv + R.rank * tc.seg1 + o1[p],
+                      R.ld, (long long)mx1 * TILE, 0, nown, cw, 0, 0, 0, P}, tc.pack_tiles);
+          }
+        tc.npack = (int)moves.size() - tc.pack0;
+        tc.unp1 = (int)moves.size();
+        for (Rank& R : h->ranks)
+          for (size_t p = 0; p < pairs.size(); ++p)
+            add_move({R.trecv + o1[p], R.g1 + og1[p], (long long)mx1 * TILE, (long long)rows1 * TILE,
+                      (long long)tc.seg1, rows1, cw, 0, 1, pairs[p].t0 + j0, P}, tc.unp1_tiles);
+        tc.nunp1 = (int)moves.size() - tc.unp1;
+      }
+      // M^T(c0:c0+cw, the rank's rows of h:t1) = X11(c0:h, c0:c0+cw)^T L21(rows, c0:h)^T
+      // (X11 triangular: K from the output's row tile, G_KBEG_TI)
+      tc.m.kind = 3;
+      tc.m.first = (int)probs.size();
+      for (Rank& R : h->ranks)
+        for (size_t p = 0; p < pairs.size(); ++p) {
+          const int c0 = pairs[p].t0 + j0, ls = lstart_of(pairs[p].h, P, R.rank);
+          const int n2 = std::min(R.nlx, lstart_of(pairs[p].t1, P, R.rank)) - ls;
+          if (n2 <= 0) continue;
+          const double* A = P == 1 ? R.X + (long long)c0 * TILE + (long long)c0 * TILE * R.ld : R.g1 + og1[p];
+          double* C = P == 1 ? R.slab + og2[p] : R.trecv + R.rank * tc.seg2 + o2[p];
+          GemmProb q = dprob(A, P == 1 ? R.ld : (long long)rows1 * TILE,
+                             R.A + (long long)ls * TILE + (long long)c0 * TILE * R.ld, R.ld, C, (long long)cw * TILE,
+                             cw, n2, rows1 * TILE, G_KBEG_TI, 1.0, 0.0);
+          q.tile_begin = tc.m.tiles;
+          q.ntiles = cw * n2;
+          tc.m.tiles += q.ntiles;
+          ++tc.m.count;
+          probs.push_back(q);
+        }
+      if (P > 1) {   // M^T's columns out of the segments, in global row order
+        tc.unp2 = (int)moves.size();
+        for (Rank& R : h->ranks)
+          for (size_t p = 0; p < pairs.size(); ++p)
+            add_move({R.trecv + o2[p], R.slab + og2[p], (long long)cw * TILE, (long long)cw * TILE,
+                      (long long)tc.seg2, cw, pairs[p].t1 - pairs[p].h, 0, 2, pairs[p].h, P}, tc.unp2_tiles);
+        tc.nunp2 = (int)moves.size() - tc.unp2;
+      }
+      // X21(i, c0:c0+cw) = -X22(i, h:i+1) M(h:i+1, c0:c0+cw) for each of the rank's rows i
+      tc.x.kind = 0;
+      tc.x.first = (int)probs.size();
+      for (Rank& R : h->ranks)
+        for (size_t p = 0; p < pairs.size(); ++p) {
+          const int c0 = pairs[p].t0 + j0, hh = pairs[p].h;
+          const int le = std::min(R.nlx, lstart_of(pairs[p].t1, P, R.rank));
+          for (int li = lstart_of(hh, P, R.rank); li < le; ++li) {
+            const int i = li * P + R.rank;
+            double* row = R.X + (long long)li * TILE;
+            GemmProb q = dprob(row + (long long)hh * TILE * R.ld, R.ld, R.slab + og2[p], (long long)cw * TILE,
+                               row + (long long)c0 * TILE * R.ld, R.ld, 1, cw, (i - hh + 1) * TILE, 0, -1.0, 0.0);
+            q.tile_begin = tc.x.tiles;
+            q.ntiles = cw;
+            tc.x.tiles += cw;
+            ++tc.x.count;
+            probs.push_back(q);
+          }
+        }
+      h->tri.push_back(tc);
+    }
+  }
+  if (!moves.empty()) {
+    DCHK(dalloc(h, &h->dmoves, moves.size(), &h->shared_bytes));
+    DCHK_HIP(h, hipMemcpy(h->dmoves, moves.data(), moves.size() * sizeof(MoveDesc), hipMemcpyHostToDevice));
   }
   h->wa_l.assign(h->ranks.size(), DLaunch());
   h->slabs.assign(h->ranks.size(), std::vector<SlabLaunch>());
@@ -793,10 +924,10 @@ int ensure_grad(gpe_dist* h) {
       // W(a) += X_r(:, a)^T R2_r over its rows >= a
       GemmProb p = dprob(R.X + (long long)ls * TILE + (long long)a * TILE * R.ld, R.ld,
                          R.r2loc + (long long)ls * TILE, R.ld, R.wpart + (long long)a * TILE, np,
-                         1, 1, K, 0, 1.0, 1.0);
+                         1, h->NA, K, 0, 1.0, 1.0);
       p.tile_begin = wl.tiles;
-      p.ntiles = 1;
-      ++wl.tiles;
+      p.ntiles = h->NA;
+      wl.tiles += h->NA;
       ++wl.count;
       wl.cdef = wl.cdef || gemm_cdef(p);
       probs.push_back(p);
@@ -831,28 +962,28 @@ int ensure_grad(gpe_dist* h) {
   return GPE_OK;
 }
 
-// TRTRI step k: owner applies its group's pending rows and finishes X(k, :), broadcast
-// into every rank's group rows (the group-closing updates are issued by trtri_all)
-int trtri_step(gpe_dist* h, int k) {
-  const int P = h->P, owner = k % P, lk = k / P;
-  const int gb = h->gstart[k], ge = group_end(h, k), w = k - gb;
-  DCHK(launch(h, h->tri_p[k], h->gprobs));
-  DCHK(launch(h, h->tri_x[k], h->gprobs));
-  if (k == h->NB - 1) return GPE_OK;   // no rows below
-  if (Rank* O = rank_slot(h, owner))
-    DCHK_HIP(h, hipMemcpy2DAsync(O->xrow, TILE * sizeof(double), O->X + (long long)lk * TILE, O->ld * sizeof(double),
-                                 TILE * sizeof(double), (size_t)(k + 1) * TILE, hipMemcpyDeviceToDevice, h->cs));
-  DCHK(coll_bcast(h, &Rank::xrow, 0, (size_t)(k + 1) * TILE * TILE, owner));
-  // X(k, 0:k+1) -> the group's row block w; zero its columns k+1 .. ge-1, which the
-  // group's later rows and the closing update read as X(k, c) = 0
-  const long long ldx = (long long)h->wmax * TILE;
-  for (Rank& R : h->ranks) {
-    double* blk = R.xgrp + (size_t)(h->gid[k] & 1) * ldx * h->n_pad + (long long)w * TILE;
-    DCHK_HIP(h, hipMemcpy2DAsync(blk, ldx * sizeof(double), R.xrow, TILE * sizeof(double), TILE * sizeof(double),
-                                 (size_t)(k + 1) * TILE, hipMemcpyDeviceToDevice, h->cs));
-    if (ge > k + 1)
-      DCHK_HIP(h, hipMemset2DAsync(blk + (long long)(k + 1) * TILE * ldx, ldx * sizeof(double), 0,
-                                   TILE * sizeof(double), (size_t)(ge - k - 1) * TILE, h->cs));
+int move_launch(gpe_dist* h, int first, int count, int tiles) {
+  if (count == 0 || tiles == 0) return GPE_OK;
+  hipLaunchKernelGGL(k_dist_move, dim3(tiles), dim3(256), 0, h->cs, h->dmoves + first, count);
+  DCHK_HIP(h, hipGetLastError());
+  return GPE_OK;
+}
+
+// the recursive TRTRI (ensure_grad), chunk by chunk on the compute stream
+int trtri_all(gpe_dist* h) {
+  h->cs = h->stream;
+  for (const TriChunk& tc : h->tri) {
+    if (h->P > 1) {
+      DCHK(move_launch(h, tc.pack0, tc.npack, tc.pack_tiles));
+      DCHK(coll_allgather(h, &Rank::trecv, tc.seg1));
+      DCHK(move_launch(h, tc.unp1, tc.nunp1, tc.unp1_tiles));
+    }
+    DCHK(launch(h, tc.m, h->gprobs));
+    if (h->P > 1) {
+      DCHK(coll_allgather(h, &Rank::trecv, tc.seg2));
+      DCHK(move_launch(h, tc.unp2, tc.nunp2, tc.unp2_tiles));
+    }
+    DCHK(launch(h, tc.x, h->gprobs));
   }
   return GPE_OK;
 }
@@ -873,7 +1004,7 @@ int kbuild(gpe_dist* h, int kernel, double nu, double s2, double rscale) {
     a.ld = R.ld; a.ldF = h->n_pad; a.d = h->d; a.n_valid = (int)h->n; a.NB = h->NB; a.nranks = h->P;
     a.rank = R.rank; a.nloc = R.nloc; a.Pc = h->q + 1;
     a.s2 = s2; a.coff = coff; a.cdiag = cdiag; a.rscale = rscale;
-    const dim3 grid((unsigned)(R.nloc * (h->NB + 1)));
+    const dim3 grid((unsigned)(R.nloc * (h->NB + h->NA)));
     if (h->d <= 4) hipLaunchKernelGGL(k_dist_kbuild<4>, grid, dim3(256), 0, h->stream, a);
     else if (h->d <= 8) hipLaunchKernelGGL(k_dist_kbuild<8>, grid, dim3(256), 0, h->stream, a);
     else if (h->d <= 10) hipLaunchKernelGGL(k_dist_kbuild<10>, grid, dim3(256), 0, h->stream, a);
@@ -898,7 +1029,7 @@ int step(gpe_dist* h, int k) {
                                    TILE, hipMemcpyDeviceToDevice, h->cs));
   }
   DCHK(launch(h, h->panel_l[k]));
-  const long long ldp = (long long)(h->NB + 1) * TILE;
+  const long long ldp = (long long)(h->NB + h->NA) * TILE;
   const long long pcol = (long long)(k - h->gstart[k]) * TILE * ldp;   // block of k in its group's panels
   const int T = h->maxT[k];
   if (T > 0) {
@@ -937,8 +1068,7 @@ int ensure_group_events(gpe_dist* h, size_t ng) {
 // (ev_next[g] releases the next chain), the rest behind them, overlapping the next
 // chain and its collectives.  The compute stream ends after every chain (it waited on
 // each ev_chain), so work queued on it afterwards follows the whole sweep.
-// tri = false: the Cholesky sweep (step); tri = true: the row TRTRI (trtri_step).
-int group_sweep(gpe_dist* h, bool tri) {
+int group_sweep(gpe_dist* h) {
   const int ng = (int)h->gs.size() - 1;
   DCHK(ensure_group_events(h, (size_t)ng));
   DCHK_HIP(h, hipEventRecord(h->ev_join, h->stream));
@@ -947,13 +1077,13 @@ int group_sweep(gpe_dist* h, bool tri) {
     const int gb = h->gs[g], ge = h->gs[g + 1];
     h->cs = h->crit;
     if (g > 0) DCHK_HIP(h, hipStreamWaitEvent(h->crit, h->ev_next[g - 1], 0));
-    for (int k = gb; k < ge; ++k) DCHK(tri ? trtri_step(h, k) : step(h, k));
+    for (int k = gb; k < ge; ++k) DCHK(step(h, k));
     DCHK_HIP(h, hipEventRecord(h->ev_chain[g], h->crit));
     h->cs = h->stream;
     DCHK_HIP(h, hipStreamWaitEvent(h->stream, h->ev_chain[g], 0));
-    DCHK(tri ? launch(h, h->tri_un[ge - 1], h->gprobs) : launch(h, h->upd_next[ge - 1]));
+    DCHK(launch(h, h->upd_next[ge - 1]));
     DCHK_HIP(h, hipEventRecord(h->ev_next[g], h->stream));
-    DCHK(tri ? launch(h, h->tri_ur[ge - 1], h->gprobs) : launch(h, h->upd_rest[ge - 1]));
+    DCHK(launch(h, h->upd_rest[ge - 1]));
   }
   h->cs = h->stream;
   return GPE_OK;
@@ -1059,6 +1189,7 @@ void gpe_dist_destroy(gpe_dist* h) {
   dfree(&h->dprobs);
   dfree(&h->dtiles);
   dfree(&h->gprobs);
+  dfree(&h->dmoves);
   if (h->hpin) (void)hipHostFree(h->hpin);
   for (hipEvent_t e : h->cev) (void)hipEventDestroy(e);
   if (h->e0) (void)hipEventDestroy(h->e0);
@@ -1076,8 +1207,7 @@ const char* gpe_dist_last_error(gpe_dist* h) { return h ? h->err.c_str() : "null
 int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double* X, const double* f,
                       const double* H, const double* r) {
   if (!h) return GPE_ERR_ARG;
-  // [f H]^T rides in ONE tile row under the matrix (tile row NB): at most 128 columns
-  if (q + 1 > TILE) return dfail(h, GPE_ERR_UNSUPPORTED, "the row-block path takes at most 127 basis functions");
+  // [f H]^T rides in the tile rows under the matrix (NB .. NB+NA-1), 128 columns each
   if (n <= 0 || d <= 0 || q < 0 || !X || !f || (q > 0 && !H))
     return dfail(h, GPE_ERR_ARG, "bad shapes");
   DCHK_HIP(h, hipSetDevice(h->device));
@@ -1088,7 +1218,8 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
   h->q = q;
   h->NB = (int)((n + TILE - 1) / TILE);
   h->n_pad = (long long)h->NB * TILE;
-  if (h->NB + 1 > 4095) return dfail(h, GPE_ERR_UNSUPPORTED, "n too large for the tile list");
+  h->NA = (q + 1 + TILE - 1) / TILE;
+  if (h->NB + h->NA > 4095) return dfail(h, GPE_ERR_UNSUPPORTED, "n too large for the tile list");
   const long long np = h->n_pad;
   const int Pc = q + 1;
   for (Rank& R : h->ranks) free_rank(R);
@@ -1098,6 +1229,7 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
   dfree(&h->cpart);
   dfree(&h->dT2);
   dfree(&h->gprobs);
+  dfree(&h->dmoves);
   DCHK(pinned(h, (size_t)np * std::max(d, Pc) + 16));
   // X (row-major, zero padded)
   DCHK(dalloc(h, &h->dX, (size_t)np * d, &h->shared_bytes));
@@ -1124,17 +1256,18 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
   DCHK(dalloc(h, &h->dinvdelta, (size_t)d, &h->shared_bytes));
   // local ranks and their sweep buffers
   build_groups(h);
-  h->panel_sz = (size_t)(h->NB + 1) * TILE * TILE * h->wmax;
-  h->T0 = nloc_of(h->NB, h->P, 0);
+  const int NT = h->NB + h->NA;
+  h->panel_sz = (size_t)NT * TILE * TILE * h->wmax;
+  h->T0 = nloc_of(NT - 1, h->P, 0);
   for (int rr = 0; rr < h->P; ++rr) {
     if (!h->loop && rr != h->rank) continue;
     Rank R;
     R.rank = rr;
-    R.nloc = nloc_of(h->NB, h->P, rr);
+    R.nloc = nloc_of(NT - 1, h->P, rr);
     R.ld = (long long)std::max(R.nloc, 1) * TILE;
     h->ranks.push_back(R);
     Rank& B = h->ranks.back();
-    DCHK(dalloc(h, &B.A, (size_t)B.ld * (size_t)(h->NB + 1) * TILE, &B.bytes));
+    DCHK(dalloc(h, &B.A, (size_t)B.ld * (size_t)NT * TILE, &B.bytes));
     DCHK(dalloc(h, &B.logdet, (size_t)h->NB + 1, &B.bytes));
     DCHK(dalloc(h, &B.dinv, (size_t)TILE * TILE, &B.bytes));
     DCHK(dalloc(h, &B.panel, 2 * h->panel_sz, &B.bytes));
@@ -1195,24 +1328,33 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
       DCHK_HIP(h, hipMemsetAsync(R.X, 0, (size_t)R.ld * NB * TILE * sizeof(double), h->stream));
   }
   DCHK(kbuild(h, kernel, nu, s2, rscale));
-  DCHK(group_sweep(h, false));
+  DCHK(group_sweep(h));
 
-  // Gram of L^-1 [f H] = -(tile (NB, NB)), and Z = L^-1 [f H], from the owner of tile row NB
-  const int ra = NB % P;
-  if (Rank* O = rank_slot(h, ra)) {
-    const double* t = O->A + (long long)(NB / P) * TILE + (long long)NB * TILE * O->ld;
-    DCHK_HIP(h, hipMemcpy2DAsync(O->gram, Pc * sizeof(double), t, O->ld * sizeof(double), Pc * sizeof(double),
-                                 Pc, hipMemcpyDeviceToDevice, h->stream));
-    if (h->grad_now) {
-      hipLaunchKernelGGL(k_dist_take_z, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, h->stream, O->A, O->ld,
-                         NB / P, np, Pc, O->dZ);
-      DCHK_HIP(h, hipGetLastError());
+  // Gram of L^-1 [f H] = -(the augmented rows' diagonal block; its lower tiles), and
+  // Z = L^-1 [f H], from the owners of the augmented tile rows: each places its rows of
+  // the Gram (the rest zero) for an all-reduce, and broadcasts its columns of Z
+  for (Rank& R : h->ranks) DCHK_HIP(h, hipMemsetAsync(R.gram, 0, (size_t)Pc * Pc * sizeof(double), h->stream));
+  for (int u = 0; u < h->NA; ++u) {
+    const int gt = NB + u, p0 = u * TILE, pc = std::min(Pc - p0, TILE);
+    if (Rank* O = rank_slot(h, gt % P)) {
+      const double* t = O->A + (long long)(gt / P) * TILE + (long long)NB * TILE * O->ld;
+      DCHK_HIP(h, hipMemcpy2DAsync(O->gram + p0, Pc * sizeof(double), t, O->ld * sizeof(double), pc * sizeof(double),
+                                   p0 + pc, hipMemcpyDeviceToDevice, h->stream));
+      if (h->grad_now) {
+        hipLaunchKernelGGL(k_dist_take_z, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, h->stream, O->A,
+                           O->ld, gt / P, np, p0, pc, O->dZ);
+        DCHK_HIP(h, hipGetLastError());
+      }
     }
   }
-  DCHK(coll_bcast(h, &Rank::gram, 0, (size_t)Pc * Pc, ra));
+  DCHK(coll_allreduce_sum(h, &Rank::gram, 0, (size_t)Pc * Pc));
   DCHK(coll_allreduce_sum(h, &Rank::logdet, 0, (size_t)NB + 1));
   DCHK(coll_info_max(h));
-  if (h->grad_now) DCHK(coll_bcast(h, &Rank::dZ, 0, (size_t)np * Pc, ra));
+  if (h->grad_now)
+    for (int u = 0; u < h->NA; ++u) {
+      const int p0 = u * TILE, pc = std::min(Pc - p0, TILE);
+      DCHK(coll_bcast(h, &Rank::dZ, (long long)p0 * np, (size_t)np * pc, (NB + u) % P));
+    }
   // host reads behind an event; the triangular inverse (independent of the host
   // algebra) is queued first so the GPU does not idle over the round trip
   double* hld = h->hpin;
@@ -1221,7 +1363,7 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
   DCHK_HIP(h, hipMemcpyAsync(hgram, R0.gram, (size_t)Pc * Pc * sizeof(double), hipMemcpyDeviceToHost, h->stream));
   DCHK_HIP(h, hipMemcpyAsync(hgram + Pc * Pc, h->dinfo, sizeof(int), hipMemcpyDeviceToHost, h->stream));
   DCHK_HIP(h, hipEventRecord(h->e1, h->stream));
-  if (h->grad_now) DCHK(group_sweep(h, true));
+  if (h->grad_now) DCHK(trtri_all(h));
   DCHK_HIP(h, hipEventSynchronize(h->e1));
   int info = 0;
   std::memcpy(&info, hgram + Pc * Pc, sizeof(int));
@@ -1238,8 +1380,8 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
   for (int k = 0; k < NB; ++k) logdetA += hld[k];
   logdetA *= 2.0;
   std::vector<double> G((size_t)Pc * Pc);
-  for (int i = 0; i < Pc; ++i)
-    for (int j = 0; j < Pc; ++j) G[(size_t)i * Pc + j] = -hgram[i + (size_t)j * Pc];
+  for (int i = 0; i < Pc; ++i)   // from the lower triangle (tiles above the diagonal are not formed)
+    for (int j = 0; j < Pc; ++j) G[(size_t)i * Pc + j] = -hgram[std::max(i, j) + (size_t)std::min(i, j) * Pc];
   SmallAlgebra sa = small_from_gram(G, Pc);
   if (!sa.ok) {
     (void)hipStreamSynchronize(h->stream);
@@ -1269,7 +1411,7 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
     DCHK_HIP(h, hipMemcpyAsync(h->dT2, h->hpin, T2.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
     for (size_t s = 0; s < h->ranks.size(); ++s) {
       Rank& R = h->ranks[s];
-      DCHK_HIP(h, hipMemsetAsync(R.wpart, 0, (size_t)np * TILE * sizeof(double), h->stream));
+      DCHK_HIP(h, hipMemsetAsync(R.wpart, 0, (size_t)np * h->NA * TILE * sizeof(double), h->stream));
       if (R.nlx == 0) continue;
       if (Pc <= SK_PMAX)
         hipLaunchKernelGGL(k_apply_small, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, h->stream, R.dZ, np, Pc,

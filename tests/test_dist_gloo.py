@@ -74,20 +74,21 @@ def _problem(n, q, seed=3):
     return A, F
 
 
-def _sched_worker(rank, world, port, n, q, W, out):
+def _sched_worker(rank, world, port, n, q, W, CW, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         A, F = _problem(n, q)
         nb = n // B
         Pc = q + 1
+        NA = -(-Pc // B)                                              # augmented tile rows
         gstart = [k - k % W for k in range(nb)]                      # column groups of width W
         gend = [min(gstart[k] + W, nb) for k in range(nb)]
-        # augmented matrix: tile row nb holds F^T (zero padded to B rows), (nb, nb) = 0
-        full = np.zeros(((nb + 1) * B, (nb + 1) * B))
+        # augmented matrix: tile rows nb .. nb+NA-1 hold F^T (zero padded), their block 0
+        full = np.zeros(((nb + NA) * B, (nb + NA) * B))
         full[:n, :n] = A
         full[n:n + Pc, :n] = F.T
-        mine = [t for t in range(nb + 1) if t % world == rank]
+        mine = [t for t in range(nb + NA) if t % world == rank]
         loc = {t: full[t * B:(t + 1) * B, :].copy() for t in mine}     # own tile rows
         logdet = np.zeros(nb + 1)
         gpanel = {}   # the group's gathered panel columns: gpanel[c][t] = L(t, c)
@@ -113,7 +114,7 @@ def _sched_worker(rank, world, port, n, q, W, out):
             Dinv = dinv.numpy()
             for t in rows:                                            # panel
                 loc[t][:, k * B:(k + 1) * B] = loc[t][:, k * B:(k + 1) * B] @ Dinv.T
-            maxT = max(len([t for t in range(nb + 1) if t % world == r and t > k]) for r in range(world))
+            maxT = max(len([t for t in range(nb + NA) if t % world == r and t > k]) for r in range(world))
             send = torch.zeros(maxT, B, B, dtype=torch.float64)
             for i, t in enumerate(rows):
                 send[i] = torch.from_numpy(loc[t][:, k * B:(k + 1) * B])
@@ -121,7 +122,7 @@ def _sched_worker(rank, world, port, n, q, W, out):
             dist.all_gather(recv, send)
             panel = {}
             for r in range(world):                                   # unpermute
-                rt = [t for t in range(nb + 1) if t % world == r and t > k]
+                rt = [t for t in range(nb + NA) if t % world == r and t > k]
                 for i, t in enumerate(rt):
                     panel[t] = recv[r][i].numpy()
             gpanel[k] = panel
@@ -132,54 +133,83 @@ def _sched_worker(rank, world, port, n, q, W, out):
                             loc[t][:, j * B:(j + 1) * B] -= loc[t][:, c * B:(c + 1) * B] @ gpanel[c][j].T
         ld = torch.from_numpy(logdet)
         dist.all_reduce(ld)
+        # -Gram: each owner of an augmented row places its rows (lower tiles), all-reduced
         g = torch.zeros(Pc, Pc, dtype=torch.float64)
-        if nb % world == rank:
-            g = torch.from_numpy(-loc[nb][:Pc, nb * B:nb * B + Pc].copy())
-        dist.broadcast(g, src=nb % world)
-        # gradient schedule: X = L^-1 by rows; R(t, :) accumulates -sum L(t,j) X(j, :)
-        # in the same column groups: the owner applies its group's earlier rows first, the
-        # step closing a group updates every rank's rows below it
+        for u in range(NA):
+            if (nb + u) in loc:
+                p0, pc = u * B, min(Pc - u * B, B)
+                g[p0:p0 + pc, :p0 + pc] = torch.from_numpy(-loc[nb + u][:pc, nb * B:nb * B + p0 + pc].copy())
+        dist.all_reduce(g)
+        G = g.numpy()
+        G = np.tril(G) + np.tril(G, -1).T
+        # gradient: X = L^-1 by the recursive TRTRI (gpemu_dist.hip ensure_grad): pairs
+        # [t0,h), [h,t1) of s tile columns, in column chunks of width <= CW: the own rows
+        # c0:h of X11's chunk columns packed by pair, all-gathered, unpermuted by owner;
+        # each rank's columns of M^T = X11^T L21^T, all-gathered, unpermuted; then
+        # X21 = -X22 M on its own rows
+        def unpermute_index(g, g0):
+            r = g % world
+            first = g0 + (r - g0 % world) % world
+            return r, (g - first) // world
+
         Xl = {t: np.zeros((B, nb * B)) for t in mine if t < nb}
-        xg = {}
-        for k in range(nb):
-            owner = k % world
-            gb, ge = gstart[k], gend[k]
-            if k == gb:
-                xg = {}
-            xrow = torch.zeros(B, (k + 1) * B, dtype=torch.float64)
-            if owner == rank:
-                for c in range(gb, k):
-                    Xl[k][:, :(c + 1) * B] -= loc[k][:, c * B:(c + 1) * B] @ xg[c]
-                Dinv = np.linalg.inv(loc[k][:, k * B:(k + 1) * B])
-                Xl[k][:, :k * B] = Dinv @ Xl[k][:, :k * B]
-                Xl[k][:, k * B:(k + 1) * B] = Dinv
-                xrow = torch.from_numpy(Xl[k][:, :(k + 1) * B].copy())
-            dist.broadcast(xrow, src=owner)
-            xg[k] = xrow.numpy()
-            if k + 1 == ge:
-                for t in Xl:
-                    if t >= ge:
-                        for c in range(gb, ge):
-                            Xl[t][:, :(c + 1) * B] -= loc[t][:, c * B:(c + 1) * B] @ xg[c]
+        for t in Xl:
+            Xl[t][:, t * B:(t + 1) * B] = np.linalg.inv(loc[t][:, t * B:(t + 1) * B])
+        s = 2
+        while s // 2 < nb:
+            a = s // 2
+            pairs = [(t0, t0 + a, min(t0 + s, nb)) for t0 in range(0, nb - a, s)]
+            for j0 in range(0, a, CW):
+                cw, rows1 = min(CW, a - j0), a - j0
+                mx1 = -(-rows1 // world)
+                send = torch.zeros(len(pairs), mx1, B, cw * B, dtype=torch.float64)
+                for p, (t0, h, t1) in enumerate(pairs):
+                    c0 = t0 + j0
+                    for j, t in enumerate([t for t in range(c0, h) if t % world == rank]):
+                        send[p, j] = torch.from_numpy(Xl[t][:, c0 * B:(c0 + cw) * B])
+                recv = [torch.zeros_like(send) for _ in range(world)]
+                dist.all_gather(recv, send)
+                mx2 = max(-(-(t1 - h) // world) for (_, h, t1) in pairs)
+                send2 = torch.zeros(len(pairs), mx2, cw * B, B, dtype=torch.float64)
+                for p, (t0, h, t1) in enumerate(pairs):
+                    c0 = t0 + j0
+                    G1 = np.zeros((rows1 * B, cw * B))
+                    for gr in range(c0, h):
+                        r, j = unpermute_index(gr, c0)
+                        G1[(gr - c0) * B:(gr - c0 + 1) * B] = recv[r][p, j].numpy()
+                    for j, i in enumerate([t for t in range(h, t1) if t % world == rank]):
+                        send2[p, j] = torch.from_numpy(G1.T @ loc[i][:, c0 * B:h * B].T)
+                recv2 = [torch.zeros_like(send2) for _ in range(world)]
+                dist.all_gather(recv2, send2)
+                for p, (t0, h, t1) in enumerate(pairs):
+                    c0 = t0 + j0
+                    G2 = np.zeros((cw * B, (t1 - h) * B))
+                    for gc in range(h, t1):
+                        r, j = unpermute_index(gc, h)
+                        G2[:, (gc - h) * B:(gc - h + 1) * B] = recv2[r][p, j].numpy()
+                    for i in [t for t in range(h, t1) if t % world == rank]:
+                        Xl[i][:, c0 * B:(c0 + cw) * B] = -(Xl[i][:, h * B:(i + 1) * B] @ G2[:, :(i - h + 1) * B].T)
+            s *= 2
         part = np.zeros((nb * B, nb * B))
         for xr in Xl.values():
             part += xr.T @ xr
         ainv = torch.from_numpy(part)
         dist.all_reduce(ainv)     # the library contracts each partial instead; the sum is A^-1
-        out[rank] = (2.0 * float(ld.sum()), g.numpy().tolist(), ainv.numpy().tolist())
+        out[rank] = (2.0 * float(ld.sum()), G.tolist(), ainv.numpy().tolist())
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,W", [(2, 1), (3, 1), (2, 3), (3, 4)])
-def test_schedule_model_matches_dense(world, W):
+@pytest.mark.parametrize("world,W,q,CW", [(2, 1, 3, 8), (3, 1, 11, 2), (2, 3, 19, 1), (3, 4, 3, 3)])
+def test_schedule_model_matches_dense(world, W, q, CW):
     """W: column-group width (1 = a trailing update per column; 3 and 4 leave a ragged
-    last group of the 7 tile columns)."""
-    n, q = 7 * B, 3
+    last group of the 7 tile columns); q + 1 > 8 spreads [f H]^T over 2-3 augmented tile
+    rows; CW: the TRTRI's column-chunk width (1 and 2 split its upper levels)."""
+    n = 7 * B
     port = _free_port()
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_sched_worker, args=(world, port, n, q, W, out), nprocs=world, join=True)
+        mp.spawn(_sched_worker, args=(world, port, n, q, W, CW, out), nprocs=world, join=True)
         res = dict(out)
     A, F = _problem(n, q)
     L = np.linalg.cholesky(A)

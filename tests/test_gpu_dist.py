@@ -154,6 +154,26 @@ def test_loopback_column_groups(ctx, monkeypatch, groups, P):
     assert ok, err
 
 
+@pytest.mark.parametrize("P", [1, 3])
+def test_loopback_gradient_chunked_trtri(ctx, monkeypatch, P):
+    """A one-tile-row slab (GPEMU_DIST_SLAB_MB=1) splits the recursive TRTRI's upper
+    levels into column chunks of 1-2 tiles (each with its own pair of all-gathers) and
+    the A^-1 partial into one-row slabs: value and gradient as the single-GPU path."""
+    monkeypatch.setenv("GPEMU_DIST_SLAB_MB", "1")
+    n, d = 3000, 4
+    X, f, H = orc.synthetic_problem(n, d, seed=11)
+    hp = _hp(d)
+    ctx.set_data(X, f, H)
+    ref, gref, _ = ctx.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=True)
+    dc = native.DistContext(0, P)
+    dc.set_data(X, f, H)
+    llh, g, _ = dc.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=True)
+    dc.close()
+    assert abs(llh - ref) <= 1e-10 * abs(ref), (llh, ref)
+    ok, err = _grad_ok(g, gref)
+    assert ok, (g, gref, err)
+
+
 @pytest.mark.parametrize("P", [2, 3])
 def test_loopback_rank_memory(P):
     """Each logical rank holds its own tile rows (of A and, after a gradient call, of

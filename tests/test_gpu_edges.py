@@ -55,9 +55,9 @@ def test_any_d_and_basis_width(ctx):
     151 basis columns, beyond the 128 the context's small buffers start at
     (GPE_MAX_DIMS / GPE_MAX_COLS, include/gpemu.h).  Value, gradient and sigma^2
     against the oracle (the value path without the augmented row, which holds 128
-    columns), then the kernel matrix at d = 129, and the row-block path (2 loopback
-    ranks) at d = 150 with 21 basis columns (it carries [f H]^T in one tile row: more
-    than 128 columns there is a loud error)."""
+    columns), then the kernel matrix at d = 129, and the row-block path (2 and 3 loopback
+    ranks) with all 151 basis columns: [f H]^T rides in two augmented tile rows there,
+    owned by different ranks."""
     n, d = 400, 150
     X, f, H = _wide_problem(n, d, seed=8)
     hp = np.concatenate([np.linspace(2.5, 4.0, d), [1e-2, 0.9]])
@@ -73,20 +73,17 @@ def test_any_d_and_basis_width(ctx):
     A = ctx.kernel_var(native.KERNEL_STD, np.full(129, 3.0), 1e-3, X2)
     Aref, _ = orc.kernel_var_ref(X2, np.full(129, 3.0), 1e-3, orc.STD, True)
     assert np.max(np.abs(A - Aref)) <= 1e-13
-    # the row-block path carries [f H]^T in one tile row: any d, at most 128 columns
-    H2 = H[:, :21]
-    ref2 = orc.objective_fast(X, f, H2, hp, orc.GP4ML, orc.STD, True)
-    dc = native.DistContext(0, 2)
-    try:
-        with pytest.raises(RuntimeError):
+    for P in (2, 3):
+        dc = native.DistContext(0, P)
+        try:
             dc.set_data(X, f, H)
-        dc.set_data(X, f, H2)
-        llh_d, g_d, _ = dc.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=True)
-    finally:
-        dc.close()
-    assert abs(llh_d - ref2[0]) <= 1e-10 * abs(ref2[0]), (llh_d, ref2[0])
-    scale2 = np.max(np.abs(ref2[1])) + 1.0
-    assert np.max(np.abs(g_d - ref2[1])) <= 1e-7 * scale2
+            llh_d, g_d, s2_d = dc.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=True)
+            v_d = dc.objective(native.GP4ML, native.KERNEL_STD, hp)[0]
+        finally:
+            dc.close()
+        assert abs(llh_d - ref[0]) <= 1e-10 * abs(ref[0]), (P, llh_d, ref[0])
+        assert v_d == llh_d
+        assert np.max(np.abs(g_d - ref[1])) <= 1e-7 * scale, (P, np.max(np.abs(g_d - ref[1])))
 
 
 def test_noise_sample_single_point(ctx):
