@@ -15,3 +15,6 @@ if [ -f gp_emu_uqsa_amd/libgpemu_trace.so ]; then
     GPEMU_LIB=gp_emu_uqsa_amd/libgpemu_trace.so timeout -k 10 120 python3 tools/chol_trace.py $n || exit 1
   done 2>&1 | tee gpurun_out/chol_trace_$TAG.log
 fi
+for P in 1 2; do
+  timeout -k 10 240 python3 tools/dist_objective.py --loopback $P --points 16384 --dims 10 --grad --check || exit 1
+done 2>&1 | tee gpurun_out/dist_$TAG.log
