@@ -376,6 +376,9 @@ int prob_tiles(const GemmProb& p) {
 // problems only.  The launch then takes the implicit tile order (no list).
 constexpr int SPLIT_SLOTS = 512;
 void split_k(std::vector<GemmProb>& probs, double* part, int* tcnt) {
+#ifdef GPE_NO_SPLITK   // dev A/B build (tools/ab_libs.sh)
+  return;
+#endif
   int T = 0, kmax = 0;
   for (const GemmProb& p : probs) {
     if (p.beta != 0.0 || p.ksplit > 1) return;
