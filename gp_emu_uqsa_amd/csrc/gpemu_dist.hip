@@ -799,12 +799,15 @@ int ensure_grad(gpe_dist* h) {
       const int b = std::min(t0 + s, NB) - (t0 + a);
       g1 += a; s1 += (a + P - 1) / P; g2 += b; s2 += (b + P - 1) / P;
     }
+    // (M^T's blocks live in the slab: g2 <= NB tiles always fits; the gathered X11 and the
+    // all-gather buffer are sized to the slab as well, except at width 1, where the
+    // segments' per-pair rounding to ceil(rows / P) may take them past it at small levels)
     int cc = a;
     auto fits = [&](long long w) {
       return g2 * w * T2 <= cap && (P == 1 || (g1 * w * T2 <= cap && P * s1 * w * T2 <= cap && P * s2 * w * T2 <= cap));
     };
     while (cc > 1 && !fits(cc)) cc = (cc + 1) / 2;
-    if (!fits(cc)) return dfail(h, GPE_ERR_UNSUPPORTED, "distributed TRTRI blocks exceed the slab");
+    if (g2 * cc * T2 > cap) return dfail(h, GPE_ERR_UNSUPPORTED, "distributed TRTRI blocks exceed the slab");
     lev.push_back({s, cc});
     if (P > 1) {
       g1_need = std::max(g1_need, g1 * cc * T2);
