@@ -1287,7 +1287,7 @@ static __global__ void __launch_bounds__(256) k_xasm(const double* __restrict__ 
   for (int e = threadIdx.x; e < 36 * 256; e += 256) {
     const int b = e >> 8, w = e & 255, bi = tri_row(b), bk = b - bi * (bi + 1) / 2;
     const long long g = (bi * 16 + (w & 15)) + (long long)(bk * 16 + (w >> 4)) * ld;
-    lds[e] = gld1((bi == bk ? X : L) + g);   // leaf inverse (lower, stored with zeros above) / L block
+    lds[b * 256 + db_e(w & 15, w >> 4)] = gld1((bi == bk ? X : L) + g);   // leaf inverse (zeros above) / L block
   }
   __syncthreads();
   db_xlevel<16>(lds);
