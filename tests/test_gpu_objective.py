@@ -97,9 +97,11 @@ def test_objective_value_only_matches(ctx, n, d):
     assert abs(a[0] - b[0]) <= 1e-12 * abs(a[0]), (a[0], b[0])
     ref = orc.objective_fast(X, f, H, hp, orc.GP4ML, orc.STD, True)[0]
     assert abs(b[0] - ref) <= 1e-10 * abs(ref), (b[0], ref)
+    # MUCM's value is a difference of O(n) terms ((n - q) log sigma^2 against log|A|; 36 out
+    # of terms near 10^3 at n = 3000, d = 40): 1e-11 of it is ~1e-13 of the terms
     m = ctx.objective(orc.MUCM, orc.STD, hp[:-1], want_grad=False)
     mg = ctx.objective(orc.MUCM, orc.STD, hp[:-1], want_grad=True)
-    assert abs(m[0] - mg[0]) <= 1e-12 * abs(mg[0]) and abs(m[2] - mg[2]) <= 1e-12 * mg[2]
+    assert abs(m[0] - mg[0]) <= 1e-11 * abs(mg[0]) and abs(m[2] - mg[2]) <= 1e-12 * mg[2]
 
 
 def test_value_only_not_pd(ctx):
