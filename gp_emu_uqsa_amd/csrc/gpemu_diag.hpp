@@ -5,8 +5,8 @@
 // of tile (k+1,k+1) then overlaps the rest of the update instead of following it.
 //
 // LDS: L in block-packed form -- the 36 lower 16x16 blocks (bi >= bk), block
-// bi*(bi+1)/2 + bk at 256*blk doubles, column-major inside the block -- exactly
-// 73,728 B, the GEMM's staging space; plus a 2 KB scratch for the current leaf
+// bi*(bi+1)/2 + bk at DB_BS*blk doubles, column-major inside the block with column j
+// shifted by j & 14 (db_e) -- 78,336 B; plus a 2 KB scratch for the current leaf
 // inverse.  After L is written out, X = L^-1 is assembled in place of it (X21
 // overwrites L21 once T = L21 X11 is in registers) and written out.
 //
@@ -23,8 +23,17 @@ namespace gpe {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-constexpr int DB_LDS_DOUBLES = 36 * 256 + 512;   // block-packed L + two leaf-inverse buffers
-constexpr int DB_EXTRA_DOUBLES = 128 + 10;       // X diagonal, reduction slots, flag, hand-offs
+// Element (i, j) of a 16 x 16 block in LDS: column-major with column j shifted by j & 14
+// doubles (block stride DB_BS).  The accumulator pattern of the MFMA code (lane ->
+// (lane >> 4 + 4 r, lane & 15)) then reads conflict-free and writes 3 LDS cycles per
+// 16-lane group instead of 16 (plain column-major: every lane of a ds_write_b64 group on
+// one bank, reads 8-way), the operand pattern (lane -> (lane & 15, 4 s + lane >> 4)) stays
+// conflict-free, and both stay affine in r and s (immediate offsets, no extra address
+// registers); pairs of rows stay 16-byte aligned.
+constexpr int DB_BS = 272;
+__host__ __device__ constexpr int db_e(int i, int j) { return i + 16 * j + (j & 14); }
+constexpr int DB_LDS_DOUBLES = 36 * DB_BS + 256;   // block-packed L + leaf-inverse scratch
+constexpr int DB_EXTRA_DOUBLES = 128 + 8;        // X diagonal, reduction slots, flag
 
 // dev-tool phase timing (tools/hip/db_bench.hip): -DDB_TIMING
 #ifdef DB_TIMING
@@ -51,16 +60,9 @@ __device__ __forceinline__ void db_gst2(double* p, double x, double y) {
 }
 __device__ __forceinline__ void db_gst1(double* p, double x) { *(__attribute__((address_space(1))) double*)(p) = x; }
 
-// Element (i, j) of a 16 x 16 block in LDS: column-major with the row index XOR'd by the
-// column.  Both access patterns of the MFMA code are then bank-conflict-free: operand reads
-// (lane -> (lane & 15, 4 s + lane >> 4)) and accumulator reads and writes (lane ->
-// (lane >> 4 + 4 r, lane & 15)); plain column-major puts the accumulator pattern's 16
-// lanes of a ds_write_b64 group on one bank (16-way) and its reads 8-way.
-__device__ __forceinline__ int db_e(int i, int j) { return (i ^ j) + 16 * j; }
-
 __device__ __forceinline__ int db_off(int i, int k) {   // i >= k
   const int bi = i >> 4, bk = k >> 4;
-  return (bi * (bi + 1) / 2 + bk) * 256 + db_e(i & 15, k & 15);
+  return (bi * (bi + 1) / 2 + bk) * DB_BS + db_e(i & 15, k & 15);
 }
 
 __device__ __forceinline__ double db_bcast(double v, int src) {
@@ -93,7 +95,7 @@ __device__ __forceinline__ double db_perm(double v, int src_lane) {
 __device__ __forceinline__ void db_leaf(double* lb, double* xs, double* xdiag, int jb, int* flag) {
   const int lane = threadIdx.x & 63;
   const int i = lane & 15, q = lane >> 4;
-  const int base = (jb * (jb + 1) / 2 + jb) * 256;
+  const int base = (jb * (jb + 1) / 2 + jb) * DB_BS;
   double a[4], xc[4];
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
@@ -155,7 +157,7 @@ __device__ __forceinline__ void db_leaf(double* lb, double* xs, double* xdiag, i
 __device__ __forceinline__ void db_leaf_mfma(double* lb, double* xs, double* xdiag, int jb, int* flag) {
   const int lane = threadIdx.x & 63;
   const int j = lane & 15, q = lane >> 4;
-  const int base = (jb * (jb + 1) / 2 + jb) * 256;
+  const int base = (jb * (jb + 1) / 2 + jb) * DB_BS;
   d4 acc, Y;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -209,7 +211,7 @@ __device__ __forceinline__ void db_leaf_mfma(double* lb, double* xs, double* xdi
 __device__ __forceinline__ void db_leaf_blk(double* lb, double* xs, double* xdiag, int jb, int* flag) {
   const int lane = threadIdx.x & 63;
   const int j = lane & 15, q = lane >> 4;
-  const int base = (jb * (jb + 1) / 2 + jb) * 256;
+  const int base = (jb * (jb + 1) / 2 + jb) * DB_BS;
   d4 acc, Y;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -291,23 +293,6 @@ __device__ __forceinline__ void db_leaf_blk(double* lb, double* xs, double* xdia
 #define DB_LEAF db_leaf_blk
 #endif
 
-// L(bo) = A(bo) X^T for the 16 x 16 block at LDS offset bo, X the leaf inverse at xp (one wave)
-__device__ __forceinline__ void db_panel_block(double* lb, int bo, const double* xp) {
-  const int lane = threadIdx.x & 63;
-  d4 acc = d4{0.0, 0.0, 0.0, 0.0};
-  double av[4], bv[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int k = 4 * s + (lane >> 4);
-    av[s] = lb[bo + db_e(lane & 15, k)];          // A(m, k)
-    bv[s] = xp[db_e(lane & 15, k)];               // X^T(k, n) = X(n, k)
-  }
-#pragma unroll
-  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) lb[bo + db_e((lane >> 4) + 4 * r, lane & 15)] = acc[r];
-}
-
 // A(po) -= L(pa) L(pb)^T for 16 x 16 blocks at LDS offsets pa, pb, po (one wave)
 __device__ __forceinline__ void db_syrk_block(double* lb, int pa, int pb, int po) {
   const int lane = threadIdx.x & 63;
@@ -368,7 +353,7 @@ __device__ __forceinline__ void db_xlevel(double* lb) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // diagonal blocks hold X in their lower part only
   auto xop = [&](int bi, int bk, int r, int c) -> double {
-    const int off = (bi * (bi + 1) / 2 + bk) * 256 + db_e(r, c);
+    const int off = (bi * (bi + 1) / 2 + bk) * DB_BS + db_e(r, c);
     return (bi > bk || r >= c) ? lb[off] : 0.0;
   };
   constexpr int ITEMS = NINST * NBH;   // 4 for every level
@@ -387,7 +372,7 @@ __device__ __forceinline__ void db_xlevel(double* lb) {
       for (int s = 0; s < 4; ++s) {
         const int k = 4 * s + (lane >> 4);
         const int bi = ob2 + ib, bk = ob + kb;
-        av[s] = lb[(bi * (bi + 1) / 2 + bk) * 256 + db_e(lane & 15, k)];   // L21(m, k)
+        av[s] = lb[(bi * (bi + 1) / 2 + bk) * DB_BS + db_e(lane & 15, k)];   // L21(m, k)
         bv[s] = xop(ob + kb, ob + cb, k, lane & 15);                          // X11(k, n)
       }
 #pragma unroll
@@ -409,14 +394,13 @@ __device__ __forceinline__ void db_xlevel(double* lb) {
     const int bi = ob2 + ib, bk = ob + cb;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      lb[(bi * (bi + 1) / 2 + bk) * 256 + db_e((lane >> 4) + 4 * r, lane & 15)] = -acc[r];
+      lb[(bi * (bi + 1) / 2 + bk) * DB_BS + db_e((lane >> 4) + 4 * r, lane & 15)] = -acc[r];
   }
   __syncthreads();
 }
 
 // One wave stores 16 x 16 block (at lb[off], db_e layout) to G (its top-left element):
-// lane = 8 columns x 8 row pairs per 16-byte store (rows r, r+1 of column c sit in one
-// aligned pair, swapped when c is odd).  MODE 0: whole block; 1: lower
+// lane = 8 columns x 8 row pairs per 16-byte store.  MODE 0: whole block; 1: lower
 // part with the diagonal only (L's diagonal blocks, whose upper part holds X^T);
 // 2: lower part and zeros above (X's diagonal blocks).
 template <int MODE>
@@ -426,8 +410,7 @@ __device__ __forceinline__ void db_put_block(const double* lb, int off, double* 
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int c = (lane >> 3) + 8 * h;
-    double2 v = *reinterpret_cast<const double2*>(lb + off + ((r ^ c) & ~1) + c * 16);
-    if (c & 1) v = double2{v.y, v.x};
+    double2 v = *reinterpret_cast<const double2*>(lb + off + db_e(r, c));
     double* gp = G + r + (long long)c * ld;
     if (MODE == 1) {
       if (r >= c) db_gst2(gp, v.x, v.y);
@@ -442,9 +425,9 @@ __device__ __forceinline__ void db_put_block(const double* lb, int off, double* 
   }
 }
 
-__device__ __forceinline__ int db_blk(int bi, int bk) { return (bi * (bi + 1) / 2 + bk) * 256; }
+__device__ __forceinline__ int db_blk(int bi, int bk) { return (bi * (bi + 1) / 2 + bk) * DB_BS; }
 
-// Factor + invert the tile held block-packed in lb[0 .. 36*256).  Writes L (lower)
+// Factor + invert the tile held block-packed in lb[0 .. 36*DB_BS).  Writes L (lower)
 // to Lg, X = L^-1 (full tile, zero upper) to Xg, returns 0 or the 1-based column
 // of the first bad pivot; *logdet_out (thread 0) = sum log L_jj.
 // LDS: lb[0, DB_LDS_DOUBLES) plus DB_EXTRA_DOUBLES after it.
@@ -462,18 +445,13 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
                                                 long long ldx, double* logdet_out, OnFactored on_factored,
                                                 bool assemble = true) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  double* xs = lb + 36 * 256;             // leaf inverses X_jb, by parity of jb: 2 x 16 x 16 (db_e)
+  double* xs = lb + 36 * DB_BS;           // current leaf inverse, 16 x 16 (db_e)
   double* xdiag = lb + DB_LDS_DOUBLES;    // 128 diagonal entries of X
   double* red = xdiag + 128;              // 4
   int* flag = reinterpret_cast<int*>(red + 4);
-  int* hand = reinterpret_cast<int*>(red + 5);   // [0] L(r, r-1) stored (r), [1] waves 1-3 met (3 per round)
   auto lg_at = [&](int bi, int bk) { return Lg + bi * 16 + (long long)(bk * 16) * ldl; };
   auto xg_at = [&](int bi, int bk) { return Xg + bi * 16 + (long long)(bk * 16) * ldx; };
-  if (tid == 0) {
-    *flag = 0;
-    hand[0] = 0;
-    hand[1] = 0;
-  }
+  if (tid == 0) *flag = 0;
   DB_TDECL;
   __syncthreads();
   DB_TN(0);
@@ -494,49 +472,58 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
   }
   __syncthreads();
   DB_T(1);
-  // Round r = 1 .. 7 (column jb = r - 1 done, leaf r next), one barrier per round:
-  //   wave 0:    L(r, jb) = A(r, jb) X_jb^T (published to waves 1-3), the diagonal block's
-  //              update A(r, r) -= L(r, jb) L(r, jb)^T, leaf r (factor + inverse, X_r into
-  //              the other inverse buffer)
-  //   waves 1-3: the rest of column jb's panel, L(ib, jb) = A(ib, jb) X_jb^T, ib > r; then
-  //              (with each other and wave 0's L(r, jb)) the trailing update by column jb,
-  //              A(ib, kb) -= L(ib, jb) L(kb, jb)^T, r <= kb <= ib except (r, r); column jb
-  //              of L out.
-  // The panel rides beside the leaf instead of in a phase of its own between two barriers.
-  for (int r = 1; r < 8; ++r) {
+  for (int jb = 0; jb < 8; ++jb) {
     if (*flag) return *flag;
-    const int jb = r - 1;
-    const double* xp = xs + (jb & 1) * 256;
+    DB_TN(2);
+    // ---- panel: L(ib,jb) = A(ib,jb) X_jb^T, one 16x16 block per wave
+    for (int ib = jb + 1 + wave; ib < 8; ib += 4) {
+      const int bo = db_blk(ib, jb);
+      d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+      double av[4], bv[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int k = 4 * s + (lane >> 4);
+        av[s] = lb[bo + db_e(lane & 15, k)];          // A(ib,jb)(m, k)
+        bv[s] = xs[db_e(lane & 15, k)];               // X^T(k, n) = X(n, k)
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lb[bo + db_e((lane >> 4) + 4 * r, lane & 15)] = acc[r];
+    }
+    __syncthreads();
+    DB_T(2);
+    if (jb == 7) break;
+    // ---- wave 0: update diagonal block jb+1 and factor it (look-ahead);
+    //      waves 1-3: the rest of the trailing update A(ib,kb) -= L(ib,jb) L(kb,jb)^T,
+    //      then column block jb of L out
     DB_TN(1);
     if (wave == 0) {
+      const int p1 = db_blk(jb + 1, jb);
       DB_TN(6);
-      const int p1 = db_blk(r, jb);
-      db_panel_block(lb, p1, xp);
-      if (lane == 0) __hip_atomic_store(&hand[0], r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      db_syrk_block(lb, p1, p1, db_blk(r, r));
+      db_syrk_block(lb, p1, p1, db_blk(jb + 1, jb + 1));
       DB_T(6);
       DB_TN(5);
-      DB_LEAF(lb, xs + (r & 1) * 256, xdiag, r, flag);
+      DB_LEAF(lb, xs, xdiag, jb + 1, flag);
       DB_T(5);
     } else {
       DB_TN(7);
-      for (int ib = r + wave; ib < 8; ib += 3) db_panel_block(lb, db_blk(ib, jb), xp);
-      if (lane == 0) __hip_atomic_fetch_add(&hand[1], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      while (__hip_atomic_load(&hand[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 3 * r ||
-             __hip_atomic_load(&hand[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < r)
-        __builtin_amdgcn_s_sleep(1);
-      const int m = 8 - r, cnt = m * (m + 1) / 2;
+      const int m = 7 - jb, cnt = m * (m + 1) / 2;
+#ifdef DB_NO_UPDATE
+      if (cnt < 0)   // dev probe: the leaf without the concurrent update (wrong results)
+#endif
       // blocks b = wave, wave + 3, ... (b = 0, the diagonal block, is wave 0's), two at a
-      // time (each LDS round trip paid once per pair)
+      // time (one at a time, the update's LDS round trips held wave 0's leaf at twice its
+      // stand-alone time: factor 78.7 -> 73.4 us with pairs, tools/hip/db_bench.hip)
       for (int b = wave; b < cnt; b += 6) {
         int rr = 0;
         while ((rr + 1) * (rr + 2) / 2 <= b) ++rr;
-        const int ib = r + rr, kb = r + (b - rr * (rr + 1) / 2);
+        const int ib = jb + 1 + rr, kb = jb + 1 + (b - rr * (rr + 1) / 2);
         const int b1 = b + 3;
         const bool has1 = b1 < cnt;
         int r1 = rr;
         while ((r1 + 1) * (r1 + 2) / 2 <= b1) ++r1;
-        const int ib1 = r + r1, kb1 = r + (b1 - r1 * (r1 + 1) / 2);
+        const int ib1 = jb + 1 + r1, kb1 = jb + 1 + (b1 - r1 * (r1 + 1) / 2);
         db_syrk_pair(lb, db_blk(ib, jb), db_blk(kb, jb), db_blk(ib, kb),
                      has1 ? db_blk(ib1, jb) : 0, has1 ? db_blk(kb1, jb) : 0, has1 ? db_blk(ib1, kb1) : 0, has1);
       }
@@ -549,7 +536,6 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
     __syncthreads();
     DB_T(1);
   }
-  if (*flag) return *flag;
   DB_TN(4);
   // ---- last diagonal block of L out, log-determinant
   if (wave == 1) db_put_block<1>(lb, db_blk(7, 7), lg_at(7, 7), ldl);
