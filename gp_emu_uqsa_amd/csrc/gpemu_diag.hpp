@@ -32,7 +32,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // registers); pairs of rows stay 16-byte aligned.
 constexpr int DB_BS = 272;
 __host__ __device__ constexpr int db_e(int i, int j) { return i + 16 * j + (j & 14); }
-constexpr int DB_LDS_DOUBLES = 36 * DB_BS + 256;   // block-packed L + leaf-inverse scratch
+constexpr int DB_LDS_DOUBLES = 37 * DB_BS;   // block-packed L + leaf-inverse scratch (same layout)
 constexpr int DB_EXTRA_DOUBLES = 128 + 8;        // X diagonal, reduction slots, flag
 
 // dev-tool phase timing (tools/hip/db_bench.hip): -DDB_TIMING
