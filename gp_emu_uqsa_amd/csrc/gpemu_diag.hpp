@@ -5,8 +5,8 @@
 // of tile (k+1,k+1) then overlaps the rest of the update instead of following it.
 //
 // LDS: L in block-packed form -- the 36 lower 16x16 blocks (bi >= bk), block
-// bi*(bi+1)/2 + bk at 256*blk doubles, column-major inside the block -- exactly
-// 73,728 B, the GEMM's staging space; plus a 2 KB scratch for the current leaf
+// bi*(bi+1)/2 + bk at DB_BS*blk doubles, column-major inside the block with column j
+// shifted by j & 14 (db_e) -- 78,336 B; plus a 2 KB scratch for the current leaf
 // inverse.  After L is written out, X = L^-1 is assembled in place of it (X21
 // overwrites L21 once T = L21 X11 is in registers) and written out.
 //
@@ -23,7 +23,16 @@ namespace gpe {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-constexpr int DB_LDS_DOUBLES = 36 * 256 + 256;   // block-packed L + leaf-inverse scratch
+// Element (i, j) of a 16 x 16 block in LDS: column-major with column j shifted by j & 14
+// doubles (block stride DB_BS).  The accumulator pattern of the MFMA code (lane ->
+// (lane >> 4 + 4 r, lane & 15)) then reads conflict-free and writes 3 LDS cycles per
+// 16-lane group instead of 16 (plain column-major: every lane of a ds_write_b64 group on
+// one bank, reads 8-way), the operand pattern (lane -> (lane & 15, 4 s + lane >> 4)) stays
+// conflict-free, and both stay affine in r and s (immediate offsets, no extra address
+// registers); pairs of rows stay 16-byte aligned.
+constexpr int DB_BS = 272;
+__host__ __device__ constexpr int db_e(int i, int j) { return i + 16 * j + (j & 14); }
+constexpr int DB_LDS_DOUBLES = 37 * DB_BS;   // block-packed L + leaf-inverse scratch (same layout)
 constexpr int DB_EXTRA_DOUBLES = 128 + 8;        // X diagonal, reduction slots, flag
 
 // dev-tool phase timing (tools/hip/db_bench.hip): -DDB_TIMING
@@ -53,7 +62,7 @@ __device__ __forceinline__ void db_gst1(double* p, double x) { *(__attribute__((
 
 __device__ __forceinline__ int db_off(int i, int k) {   // i >= k
   const int bi = i >> 4, bk = k >> 4;
-  return (bi * (bi + 1) / 2 + bk) * 256 + (i & 15) + (k & 15) * 16;
+  return (bi * (bi + 1) / 2 + bk) * DB_BS + db_e(i & 15, k & 15);
 }
 
 __device__ __forceinline__ double db_bcast(double v, int src) {
@@ -86,12 +95,12 @@ __device__ __forceinline__ double db_perm(double v, int src_lane) {
 __device__ __forceinline__ void db_leaf(double* lb, double* xs, double* xdiag, int jb, int* flag) {
   const int lane = threadIdx.x & 63;
   const int i = lane & 15, q = lane >> 4;
-  const int base = (jb * (jb + 1) / 2 + jb) * 256;
+  const int base = (jb * (jb + 1) / 2 + jb) * DB_BS;
   double a[4], xc[4];
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
     const int k = 4 * kk + q;
-    a[kk] = (k <= i) ? lb[base + i + k * 16] : 0.0;
+    a[kk] = (k <= i) ? lb[base + db_e(i, k)] : 0.0;
     xc[kk] = (k == i) ? 1.0 : 0.0;
   }
   int bad = 0;
@@ -125,8 +134,8 @@ __device__ __forceinline__ void db_leaf(double* lb, double* xs, double* xdiag, i
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
     const int k = 4 * kk + q;
-    lb[base + i + k * 16] = (k <= i) ? a[kk] : xc[kk];   // L lower / X(k,i) at (i,k) upper
-    xs[k + i * 16] = xc[kk];                             // X(k, i), zero for k < i
+    lb[base + db_e(i, k)] = (k <= i) ? a[kk] : xc[kk];   // L lower / X(k,i) at (i,k) upper
+    xs[db_e(k, i)] = xc[kk];                             // X(k, i), zero for k < i
     if (k == i) xdiag[jb * 16 + i] = xc[kk];
   }
 }
@@ -148,12 +157,12 @@ __device__ __forceinline__ void db_leaf(double* lb, double* xs, double* xdiag, i
 __device__ __forceinline__ void db_leaf_mfma(double* lb, double* xs, double* xdiag, int jb, int* flag) {
   const int lane = threadIdx.x & 63;
   const int j = lane & 15, q = lane >> 4;
-  const int base = (jb * (jb + 1) / 2 + jb) * 256;
+  const int base = (jb * (jb + 1) / 2 + jb) * DB_BS;
   d4 acc, Y;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = q + 4 * r;   // this register's row
-    acc[r] = (i >= j) ? lb[base + i + 16 * j] : lb[base + j + 16 * i];
+    acc[r] = (i >= j) ? lb[base + db_e(i, j)] : lb[base + db_e(j, i)];
     Y[r] = (i == j) ? 1.0 : 0.0;
   }
   int bad = 0;
@@ -181,8 +190,8 @@ __device__ __forceinline__ void db_leaf_mfma(double* lb, double* xs, double* xdi
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int c = q + 4 * r;   // this register's row of acc / Y: L(j, c) or X(c, j)
-    lb[base + j + 16 * c] = (j >= c) ? acc[r] : Y[r];   // L lower / X(c, j) at (j, c), upper
-    xs[c + 16 * j] = Y[r];                              // X(c, j), zero for j > c
+    lb[base + db_e(j, c)] = (j >= c) ? acc[r] : Y[r];   // L lower / X(c, j) at (j, c), upper
+    xs[db_e(c, j)] = Y[r];                              // X(c, j), zero for j > c
     if (j == c) xdiag[jb * 16 + c] = Y[r];
   }
 }
@@ -202,12 +211,12 @@ __device__ __forceinline__ void db_leaf_mfma(double* lb, double* xs, double* xdi
 __device__ __forceinline__ void db_leaf_blk(double* lb, double* xs, double* xdiag, int jb, int* flag) {
   const int lane = threadIdx.x & 63;
   const int j = lane & 15, q = lane >> 4;
-  const int base = (jb * (jb + 1) / 2 + jb) * 256;
+  const int base = (jb * (jb + 1) / 2 + jb) * DB_BS;
   d4 acc, Y;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = q + 4 * r;   // this register's row
-    acc[r] = (i >= j) ? lb[base + i + 16 * j] : lb[base + j + 16 * i];
+    acc[r] = (i >= j) ? lb[base + db_e(i, j)] : lb[base + db_e(j, i)];
     Y[r] = (i == j) ? 1.0 : 0.0;
   }
   int bad = 0;
@@ -268,8 +277,8 @@ __device__ __forceinline__ void db_leaf_blk(double* lb, double* xs, double* xdia
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int c = q + 4 * r;   // this register's row of acc / Y: L(j, c) or X(c, j)
-    lb[base + j + 16 * c] = (j >= c) ? acc[r] : Y[r];   // L lower / X(c, j) at (j, c), upper
-    xs[c + 16 * j] = Y[r];                              // X(c, j), zero for j > c
+    lb[base + db_e(j, c)] = (j >= c) ? acc[r] : Y[r];   // L lower / X(c, j) at (j, c), upper
+    xs[db_e(c, j)] = Y[r];                              // X(c, j), zero for j > c
     if (j == c) xdiag[jb * 16 + c] = Y[r];
   }
 }
@@ -292,13 +301,13 @@ __device__ __forceinline__ void db_syrk_block(double* lb, int pa, int pb, int po
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int k = 4 * s + (lane >> 4);
-    av[s] = lb[pa + (lane & 15) + k * 16];
-    bv[s] = lb[pb + (lane & 15) + k * 16];        // L(kb,jb)^T(k, n) = L(kb,jb)(n, k)
+    av[s] = lb[pa + db_e(lane & 15, k)];
+    bv[s] = lb[pb + db_e(lane & 15, k)];          // L(kb,jb)^T(k, n) = L(kb,jb)(n, k)
   }
 #pragma unroll
   for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
 #pragma unroll
-  for (int r = 0; r < 4; ++r) lb[po + ((lane >> 4) + 4 * r) + (lane & 15) * 16] -= acc[r];
+  for (int r = 0; r < 4; ++r) lb[po + db_e((lane >> 4) + 4 * r, lane & 15)] -= acc[r];
 }
 
 // Two independent blocks of the trailing update at once (the second only if has1): both
@@ -311,17 +320,17 @@ __device__ __forceinline__ void db_syrk_pair(double* lb, int pa0, int pb0, int p
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int k = 4 * s + (lane >> 4);
-    av0[s] = lb[pa0 + (lane & 15) + k * 16];
-    bv0[s] = lb[pb0 + (lane & 15) + k * 16];
+    av0[s] = lb[pa0 + db_e(lane & 15, k)];
+    bv0[s] = lb[pb0 + db_e(lane & 15, k)];
     if (has1) {
-      av1[s] = lb[pa1 + (lane & 15) + k * 16];
-      bv1[s] = lb[pb1 + (lane & 15) + k * 16];
+      av1[s] = lb[pa1 + db_e(lane & 15, k)];
+      bv1[s] = lb[pb1 + db_e(lane & 15, k)];
     }
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    c0[r] = lb[po0 + ((lane >> 4) + 4 * r) + (lane & 15) * 16];
-    if (has1) c1[r] = lb[po1 + ((lane >> 4) + 4 * r) + (lane & 15) * 16];
+    c0[r] = lb[po0 + db_e((lane >> 4) + 4 * r, lane & 15)];
+    if (has1) c1[r] = lb[po1 + db_e((lane >> 4) + 4 * r, lane & 15)];
   }
   d4 acc0 = d4{0.0, 0.0, 0.0, 0.0}, acc1 = acc0;
 #pragma unroll
@@ -331,8 +340,8 @@ __device__ __forceinline__ void db_syrk_pair(double* lb, int pa0, int pb0, int p
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    lb[po0 + ((lane >> 4) + 4 * r) + (lane & 15) * 16] = c0[r] - acc0[r];
-    if (has1) lb[po1 + ((lane >> 4) + 4 * r) + (lane & 15) * 16] = c1[r] - acc1[r];
+    lb[po0 + db_e((lane >> 4) + 4 * r, lane & 15)] = c0[r] - acc0[r];
+    if (has1) lb[po1 + db_e((lane >> 4) + 4 * r, lane & 15)] = c1[r] - acc1[r];
   }
 }
 
@@ -344,7 +353,7 @@ __device__ __forceinline__ void db_xlevel(double* lb) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // diagonal blocks hold X in their lower part only
   auto xop = [&](int bi, int bk, int r, int c) -> double {
-    const int off = (bi * (bi + 1) / 2 + bk) * 256 + r + c * 16;
+    const int off = (bi * (bi + 1) / 2 + bk) * DB_BS + db_e(r, c);
     return (bi > bk || r >= c) ? lb[off] : 0.0;
   };
   constexpr int ITEMS = NINST * NBH;   // 4 for every level
@@ -363,7 +372,7 @@ __device__ __forceinline__ void db_xlevel(double* lb) {
       for (int s = 0; s < 4; ++s) {
         const int k = 4 * s + (lane >> 4);
         const int bi = ob2 + ib, bk = ob + kb;
-        av[s] = lb[(bi * (bi + 1) / 2 + bk) * 256 + (lane & 15) + k * 16];   // L21(m, k)
+        av[s] = lb[(bi * (bi + 1) / 2 + bk) * DB_BS + db_e(lane & 15, k)];   // L21(m, k)
         bv[s] = xop(ob + kb, ob + cb, k, lane & 15);                          // X11(k, n)
       }
 #pragma unroll
@@ -385,12 +394,12 @@ __device__ __forceinline__ void db_xlevel(double* lb) {
     const int bi = ob2 + ib, bk = ob + cb;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      lb[(bi * (bi + 1) / 2 + bk) * 256 + ((lane >> 4) + 4 * r) + (lane & 15) * 16] = -acc[r];
+      lb[(bi * (bi + 1) / 2 + bk) * DB_BS + db_e((lane >> 4) + 4 * r, lane & 15)] = -acc[r];
   }
   __syncthreads();
 }
 
-// One wave stores 16 x 16 block (column-major at lb[off]) to G (its top-left element):
+// One wave stores 16 x 16 block (at lb[off], db_e layout) to G (its top-left element):
 // lane = 8 columns x 8 row pairs per 16-byte store.  MODE 0: whole block; 1: lower
 // part with the diagonal only (L's diagonal blocks, whose upper part holds X^T);
 // 2: lower part and zeros above (X's diagonal blocks).
@@ -401,7 +410,7 @@ __device__ __forceinline__ void db_put_block(const double* lb, int off, double* 
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int c = (lane >> 3) + 8 * h;
-    double2 v = *reinterpret_cast<const double2*>(lb + off + r + c * 16);
+    double2 v = *reinterpret_cast<const double2*>(lb + off + db_e(r, c));
     double* gp = G + r + (long long)c * ld;
     if (MODE == 1) {
       if (r >= c) db_gst2(gp, v.x, v.y);
@@ -416,9 +425,9 @@ __device__ __forceinline__ void db_put_block(const double* lb, int off, double* 
   }
 }
 
-__device__ __forceinline__ int db_blk(int bi, int bk) { return (bi * (bi + 1) / 2 + bk) * 256; }
+__device__ __forceinline__ int db_blk(int bi, int bk) { return (bi * (bi + 1) / 2 + bk) * DB_BS; }
 
-// Factor + invert the tile held block-packed in lb[0 .. 36*256).  Writes L (lower)
+// Factor + invert the tile held block-packed in lb[0 .. 36*DB_BS).  Writes L (lower)
 // to Lg, X = L^-1 (full tile, zero upper) to Xg, returns 0 or the 1-based column
 // of the first bad pivot; *logdet_out (thread 0) = sum log L_jj.
 // LDS: lb[0, DB_LDS_DOUBLES) plus DB_EXTRA_DOUBLES after it.
@@ -436,7 +445,7 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
                                                 long long ldx, double* logdet_out, OnFactored on_factored,
                                                 bool assemble = true) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  double* xs = lb + 36 * 256;             // current leaf inverse, column-major 16 x 16
+  double* xs = lb + 36 * DB_BS;           // current leaf inverse, 16 x 16 (db_e)
   double* xdiag = lb + DB_LDS_DOUBLES;    // 128 diagonal entries of X
   double* red = xdiag + 128;              // 4
   int* flag = reinterpret_cast<int*>(red + 4);
@@ -474,13 +483,13 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int k = 4 * s + (lane >> 4);
-        av[s] = lb[bo + (lane & 15) + k * 16];        // A(ib,jb)(m, k)
-        bv[s] = xs[(lane & 15) + k * 16];             // X^T(k, n) = X(n, k)
+        av[s] = lb[bo + db_e(lane & 15, k)];          // A(ib,jb)(m, k)
+        bv[s] = xs[db_e(lane & 15, k)];               // X^T(k, n) = X(n, k)
       }
 #pragma unroll
       for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) lb[bo + ((lane >> 4) + 4 * r) + (lane & 15) * 16] = acc[r];
+      for (int r = 0; r < 4; ++r) lb[bo + db_e((lane >> 4) + 4 * r, lane & 15)] = acc[r];
     }
     __syncthreads();
     DB_T(2);
@@ -541,8 +550,8 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
     const int base = db_blk(jb, jb);
     for (int e = t; e < 256; e += 32) {
       const int i = e & 15, c = e >> 4;
-      if (i > c) lb[base + i + c * 16] = lb[base + c + i * 16];
-      else if (i == c) lb[base + i + c * 16] = xdiag[jb * 16 + i];
+      if (i > c) lb[base + db_e(i, c)] = lb[base + db_e(c, i)];
+      else if (i == c) lb[base + db_e(i, c)] = xdiag[jb * 16 + i];
     }
   }
   __syncthreads();

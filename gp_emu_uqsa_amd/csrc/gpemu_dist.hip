@@ -46,6 +46,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <map>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -302,7 +303,8 @@ struct Rank {              // one rank's buffers (one per process over RCCL, P i
 struct DLaunch {           // one grouped k_gemm launch
   int first = 0, count = 0, tiles = 0;
   long long list = -1;
-  int kind = 0;            // 0 <false,false>, 1 <false,true>, 2 <true,true>, 3 <true,false>
+  int kind = 0;            // 0 <false,false> (the fused instance: G_DIAG problems), 1 <false,true>,
+                           // 2 <true,true>, 3 <true,false>, 4 <false,false> (plain)
   bool cdef = false;       // k_gemm's CDEF instance (gemm_cdef of some problem)
 };
 
@@ -382,6 +384,7 @@ struct gpe_dist {
   int slab_rows = 1;                           // tile rows per slab of A^-1
   double* dT2 = nullptr;
   GemmProb* gprobs = nullptr;
+  unsigned* gtiles = nullptr;                  // tile lists of the gradient launches
   std::vector<DLaunch> wa_l;
   std::vector<TriChunk> tri;                   // the recursive TRTRI, level by level
   MoveDesc* dmoves = nullptr;
@@ -602,6 +605,62 @@ double* panel_of(const gpe_dist* h, const Rank& R, int k) {
   return R.panel + (size_t)(h->gid[k] & 1) * h->panel_sz;
 }
 
+// XCD-aware order of a launch's tiles (as gpemu.hip order_tiles): rows (problem, ti) -- one
+// A panel each -- longest tiles first, greedily packed into 8 bins of equal work, the bins
+// interleaved tile by tile.  Under round-robin dispatch each row's tiles then run on one
+// XCD and its A panel stays in that XCD's L2: in implicit order (ti fastest) every XCD
+// streams every panel, and a K = 8192 TRTRI level ran 2.7x over its MFMA time.
+std::vector<unsigned> xcd_order(const GemmProb* probs, const std::vector<unsigned>& tiles) {
+  struct Row { double w = 0.0, tw = 0.0; std::vector<unsigned> t; };
+  std::map<std::pair<int, int>, Row> rows;
+  for (unsigned code : tiles) {
+    const int p = (int)(code >> 24), ti = (int)((code >> 12) & 0xfff);
+    const GemmProb& P = probs[p];
+    int kb = 0, ke = P.K;
+    if (P.flags & G_KBEG_TI) kb = ti * TILE;
+    if (P.flags & G_KEND_TI) ke = std::min(ke, (ti + 1) * TILE);
+    Row& r = rows[{p, ti}];
+    r.tw = (double)std::max(ke - kb, 0) + 2.0 * GK;   // + fixed per-tile cost
+    r.w += r.tw;
+    r.t.push_back(code);
+  }
+  std::vector<const Row*> order;
+  for (const auto& kv : rows) order.push_back(&kv.second);
+  std::stable_sort(order.begin(), order.end(), [](const Row* a, const Row* b) { return a->tw > b->tw; });
+  constexpr int NX = 8;
+  std::vector<std::vector<unsigned>> bins(NX);
+  std::vector<double> load(NX, 0.0);
+  for (const Row* r : order) {
+    const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    load[x] += r->w;
+    bins[x].insert(bins[x].end(), r->t.begin(), r->t.end());
+  }
+  std::vector<unsigned> out;
+  size_t longest = 0;
+  for (auto& b : bins) longest = std::max(longest, b.size());
+  for (size_t j = 0; j < longest; ++j)
+    for (int x = 0; x < NX; ++x)
+      if (j < bins[x].size()) out.push_back(bins[x][j]);
+  return out;
+}
+
+// every tile of a plain launch's problems, XCD-ordered, appended to tiles as L's list
+// (launches of more than 256 problems, which the list code cannot name, keep the
+// implicit order)
+void list_launch(DLaunch& L, const std::vector<GemmProb>& probs, std::vector<unsigned>& tiles) {
+  if (L.count == 0 || L.count > 256) return;
+  std::vector<unsigned> all;
+  for (int p = 0; p < L.count; ++p) {
+    const GemmProb& P = probs[L.first + p];
+    for (int tj = 0; tj < P.nt; ++tj)
+      for (int ti = 0; ti < P.mt; ++ti)
+        if (!(P.flags & G_CLOWER) || tj <= ti) all.push_back(((unsigned)p << 24) | ((unsigned)ti << 12) | (unsigned)tj);
+  }
+  const std::vector<unsigned> ord = xcd_order(probs.data() + L.first, all);
+  L.list = (long long)tiles.size();
+  tiles.insert(tiles.end(), ord.begin(), ord.end());
+}
+
 // every per-step GEMM descriptor and tile list, for the current n and partition
 int build_schedule(gpe_dist* h) {
   const int NB = h->NB, P = h->P, NT = NB + h->NA;
@@ -674,6 +733,7 @@ int build_schedule(gpe_dist* h) {
       probs.push_back(p);
       ++pl.count;
     }
+    pl.kind = 4;
     h->panel_l[k] = pl;
     // the step closing a group: trailing update of each local rank's rows by the
     // whole group, columns ge <= j <= i, K = 128 (ge - gb), in two launches: the next
@@ -703,6 +763,12 @@ int build_schedule(gpe_dist* h) {
       }
       ul.tiles = (int)(tiles.size() - ul.list);
       if (ul.tiles == 0) ul.count = 0;
+      if (ul.tiles > 0) {   // (at most 256 problems: one per local rank)
+        const std::vector<unsigned> mine(tiles.begin() + ul.list, tiles.end());
+        const std::vector<unsigned> ord = xcd_order(probs.data() + ul.first, mine);
+        std::copy(ord.begin(), ord.end(), tiles.begin() + ul.list);
+      }
+      ul.kind = 4;
       (part == 0 ? h->upd_next : h->upd_rest)[k] = ul;
     }
   }
@@ -719,11 +785,12 @@ int build_schedule(gpe_dist* h) {
   return GPE_OK;
 }
 
-int launch(gpe_dist* h, const DLaunch& L, const GemmProb* base = nullptr) {
+// the sweep's launches (dprobs / dtiles), or the gradient's (gprobs / gtiles) with grad
+int launch(gpe_dist* h, const DLaunch& L, bool grad = false) {
   if (L.count == 0 || L.tiles == 0) return GPE_OK;
   const size_t lds = G_LDS_LAUNCH_DOUBLES * sizeof(double);
-  const unsigned* tl = L.list >= 0 ? h->dtiles + L.list : nullptr;
-  const GemmProb* pr = (base ? base : h->dprobs) + L.first;
+  const unsigned* tl = L.list >= 0 ? (grad ? h->gtiles : h->dtiles) + L.list : nullptr;
+  const GemmProb* pr = (grad ? h->gprobs : h->dprobs) + L.first;
   const dim3 g(L.tiles);
   const dim3 b(256);
   if (L.cdef) {
@@ -731,6 +798,7 @@ int launch(gpe_dist* h, const DLaunch& L, const GemmProb* base = nullptr) {
       case 1: hipLaunchKernelGGL((k_gemm<false, true, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
       case 2: hipLaunchKernelGGL((k_gemm<true, true, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
       case 3: hipLaunchKernelGGL((k_gemm<true, false, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
+      case 4: hipLaunchKernelGGL((k_gemm<false, false, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
       default:   // kind 0 launches may carry G_DIAG / G_PANEL problems
         hipLaunchKernelGGL((k_gemm<false, false, true, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
     }
@@ -739,6 +807,7 @@ int launch(gpe_dist* h, const DLaunch& L, const GemmProb* base = nullptr) {
       case 1: hipLaunchKernelGGL((k_gemm<false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
       case 2: hipLaunchKernelGGL((k_gemm<true, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
       case 3: hipLaunchKernelGGL((k_gemm<true, false>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
+      case 4: hipLaunchKernelGGL((k_gemm<false, false>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
       default:   // kind 0 launches may carry G_DIAG / G_PANEL problems
         hipLaunchKernelGGL((k_gemm<false, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
     }
@@ -889,7 +958,7 @@ int ensure_grad(gpe_dist* h) {
         tc.nunp2 = (int)moves.size() - tc.unp2;
       }
       // X21(i, c0:c0+cw) = -X22(i, h:i+1) M(h:i+1, c0:c0+cw) for each of the rank's rows i
-      tc.x.kind = 0;
+      tc.x.kind = 4;
       tc.x.first = (int)probs.size();
       for (Rank& R : h->ranks)
         for (size_t p = 0; p < pairs.size(); ++p) {
@@ -909,6 +978,11 @@ int ensure_grad(gpe_dist* h) {
         }
       h->tri.push_back(tc);
     }
+  }
+  std::vector<unsigned> gt;
+  for (TriChunk& tc : h->tri) {
+    list_launch(tc.m, probs, gt);
+    list_launch(tc.x, probs, gt);
   }
   if (!moves.empty()) {
     DCHK(dalloc(h, &h->dmoves, moves.size(), &h->shared_bytes));
@@ -958,7 +1032,13 @@ int ensure_grad(gpe_dist* h) {
       h->slabs[s].push_back(sl);
     }
   }
+  for (DLaunch& L : h->wa_l) list_launch(L, probs, gt);
+  for (auto& v : h->slabs)
+    for (SlabLaunch& sl : v) list_launch(sl.gemm, probs, gt);
   if ((int)probs.size() > DIST_DESC_MAX) return dfail(h, GPE_ERR_UNSUPPORTED, "distributed gradient schedule too large");
+  DCHK(dalloc(h, &h->gtiles, std::max<size_t>(gt.size(), 1), &h->shared_bytes));
+  if (!gt.empty())
+    DCHK_HIP(h, hipMemcpy(h->gtiles, gt.data(), gt.size() * sizeof(unsigned), hipMemcpyHostToDevice));
   DCHK(dalloc(h, &h->gprobs, probs.size(), &h->shared_bytes));
   DCHK_HIP(h, hipMemcpy(h->gprobs, probs.data(), probs.size() * sizeof(GemmProb), hipMemcpyHostToDevice));
   h->grad_ready = true;
@@ -981,12 +1061,12 @@ int trtri_all(gpe_dist* h) {
       DCHK(coll_allgather(h, &Rank::trecv, tc.seg1));
       DCHK(move_launch(h, tc.unp1, tc.nunp1, tc.unp1_tiles));
     }
-    DCHK(launch(h, tc.m, h->gprobs));
+    DCHK(launch(h, tc.m, true));
     if (h->P > 1) {
       DCHK(coll_allgather(h, &Rank::trecv, tc.seg2));
       DCHK(move_launch(h, tc.unp2, tc.nunp2, tc.unp2_tiles));
     }
-    DCHK(launch(h, tc.x, h->gprobs));
+    DCHK(launch(h, tc.x, true));
   }
   return GPE_OK;
 }
@@ -1192,6 +1272,7 @@ void gpe_dist_destroy(gpe_dist* h) {
   dfree(&h->dprobs);
   dfree(&h->dtiles);
   dfree(&h->gprobs);
+  dfree(&h->gtiles);
   dfree(&h->dmoves);
   if (h->hpin) (void)hipHostFree(h->hpin);
   for (hipEvent_t e : h->cev) (void)hipEventDestroy(e);
@@ -1232,6 +1313,7 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
   dfree(&h->cpart);
   dfree(&h->dT2);
   dfree(&h->gprobs);
+  dfree(&h->gtiles);
   dfree(&h->dmoves);
   DCHK(pinned(h, (size_t)np * std::max(d, Pc) + 16));
   // X (row-major, zero padded)
@@ -1427,7 +1509,7 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
       hipLaunchKernelGGL(k_dist_rows, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, h->stream, R.dR2, np, Pc,
                          P, R.rank, R.nlx, R.r2loc, R.ld);
       DCHK_HIP(h, hipGetLastError());
-      DCHK(launch(h, h->wa_l[s], h->gprobs));
+      DCHK(launch(h, h->wa_l[s], true));
     }
     DCHK(coll_allreduce_sum(h, &Rank::wpart, 0, (size_t)np * Pc));
     // each rank: its partial of A^-1 slab by slab, each slab contracted at once
@@ -1441,7 +1523,7 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
       if (R.nlx == 0) continue;
       const int q1 = R.rank == 0 ? Pc : 0;   // the -W W^T term once
       for (const SlabLaunch& sl : h->slabs[s]) {
-        DCHK(launch(h, sl.gemm, h->gprobs));
+        DCHK(launch(h, sl.gemm, true));
         const int b0 = sl.a0 * (sl.a0 + 1) / 2, b1 = sl.a1 * (sl.a1 + 1) / 2;
         contract_launch(h, R.slab, lds, (long long)sl.a0 * TILE, b0, b1 - b0, R.wpart, q1, rdiag);
         DCHK_HIP(h, hipGetLastError());

@@ -906,7 +906,8 @@ __host__ __device__ constexpr int tri_row(int b) {   // bi of packed lower block
   return bi;
 }
 
-// LDS: L(jb,kb) (kb < jb) and X_jb, block-packed (db_blk) -- 72 KB, the staging space;
+// LDS: L(jb,kb) (kb < jb) and X_jb, block-packed (256 doubles a block, plain column-major:
+// this code reads only the operand pattern) -- 72 KB, the staging space;
 // every thread's 18 16-byte pieces are loaded together (one round trip), then stored.
 template <class Prob>
 __device__ __forceinline__ void panel_subst(const PanelAddr& pa, const double* Ld, long long ldd,
@@ -945,7 +946,7 @@ __device__ __forceinline__ void panel_subst(const PanelAddr& pa, const double* L
     // the step's A operands first, in one batch (row block jb of L, then X_jb): a read
     // beside each product would put an LDS round trip in front of every MFMA
     double av[8][4], xv[4];
-    const double* arow = lb + db_blk(jb, 0) + ao;   // blocks (jb, 0 .. jb) are contiguous
+    const double* arow = lb + (jb * (jb + 1) / 2) * 256 + ao;   // blocks (jb, 0 .. jb) are contiguous
 #pragma unroll
     for (int kb = 0; kb < jb; ++kb)
 #pragma unroll
@@ -1287,7 +1288,7 @@ static __global__ void __launch_bounds__(256) k_xasm(const double* __restrict__ 
   for (int e = threadIdx.x; e < 36 * 256; e += 256) {
     const int b = e >> 8, w = e & 255, bi = tri_row(b), bk = b - bi * (bi + 1) / 2;
     const long long g = (bi * 16 + (w & 15)) + (long long)(bk * 16 + (w >> 4)) * ld;
-    lds[e] = gld1((bi == bk ? X : L) + g);   // leaf inverse (lower, stored with zeros above) / L block
+    lds[b * DB_BS + db_e(w & 15, w >> 4)] = gld1((bi == bk ? X : L) + g);   // leaf inverse (zeros above) / L block
   }
   __syncthreads();
   db_xlevel<16>(lds);
@@ -1296,7 +1297,7 @@ static __global__ void __launch_bounds__(256) k_xasm(const double* __restrict__ 
   const int wave = threadIdx.x >> 6;
   for (int b = wave; b < 36; b += 4) {
     const int bi = tri_row(b), bk = b - bi * (bi + 1) / 2;
-    if (bi != bk) db_put_block<0>(lds, b * 256, X + bi * 16 + (long long)(bk * 16) * ld, ld);
+    if (bi != bk) db_put_block<0>(lds, b * DB_BS, X + bi * 16 + (long long)(bk * 16) * ld, ld);
   }
 }
 

@@ -23,7 +23,7 @@ __device__ __forceinline__ void db_leaf_sc(double* lb, double* xs, double* xdiag
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     double a = 0.0;
-    if (frow && k <= i) a = lb[base + i + k * 16];
+    if (frow && k <= i) a = lb[base + db_e(i, k)];
     if (xcol && k == i) a = 1.0;
     v[k] = a;
   }
@@ -45,12 +45,12 @@ __device__ __forceinline__ void db_leaf_sc(double* lb, double* xs, double* xdiag
   if (frow) {
 #pragma unroll
     for (int k = 0; k < 16; ++k)
-      if (k <= i) lb[base + i + k * 16] = v[k];          // L lower
+      if (k <= i) lb[base + db_e(i, k)] = v[k];          // L lower
   } else if (xcol) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      if (k > i) lb[base + i + k * 16] = v[k];           // X(k, c) at (c, k), upper
-      xs[k + i * 16] = v[k];                             // X(k, c), zero for k < c
+      if (k > i) lb[base + db_e(i, k)] = v[k];           // X(k, c) at (c, k), upper
+      xs[db_e(k, i)] = v[k];                             // X(k, c), zero for k < c
     }
     xdiag[jb * 16 + i] = v[i];
   }
@@ -70,7 +70,7 @@ __device__ __forceinline__ void leaf_sc2(double* lb, double* xs, double* xdiag, 
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     double a = 0.0;
-    if (frow && k <= i) a = lb[base + i + k * 16];
+    if (frow && k <= i) a = lb[base + db_e(i, k)];
     if (xcol && k == i) a = 1.0;
     v[k] = a;
   }
@@ -106,12 +106,12 @@ __device__ __forceinline__ void leaf_sc2(double* lb, double* xs, double* xdiag, 
   if (frow) {
 #pragma unroll
     for (int k = 0; k < 16; ++k)
-      if (k <= i) lb[base + i + k * 16] = v[k];
+      if (k <= i) lb[base + db_e(i, k)] = v[k];
   } else if (xcol) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      if (k > i) lb[base + i + k * 16] = v[k];
-      xs[k + i * 16] = v[k];
+      if (k > i) lb[base + db_e(i, k)] = v[k];
+      xs[db_e(k, i)] = v[k];
     }
     xdiag[jb * 16 + i] = v[i];
   }
@@ -129,7 +129,7 @@ __device__ __forceinline__ void leaf_lds(double* lb, double* xs, double* xdiag, 
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     double a = 0.0;
-    if (frow && k <= i) a = lb[base + i + k * 16];
+    if (frow && k <= i) a = lb[base + db_e(i, k)];
     if (xcol && k == i) a = 1.0;
     v[k] = a;
   }
@@ -164,12 +164,12 @@ __device__ __forceinline__ void leaf_lds(double* lb, double* xs, double* xdiag, 
   if (frow) {
 #pragma unroll
     for (int k = 0; k < 16; ++k)
-      if (k <= i) lb[base + i + k * 16] = v[k];
+      if (k <= i) lb[base + db_e(i, k)] = v[k];
   } else if (xcol) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      if (k > i) lb[base + i + k * 16] = v[k];
-      xs[k + i * 16] = v[k];
+      if (k > i) lb[base + db_e(i, k)] = v[k];
+      xs[db_e(k, i)] = v[k];
     }
     xdiag[jb * 16 + i] = v[i];
   }
@@ -187,7 +187,7 @@ __device__ __forceinline__ void leaf_mfma_probe(double* lb, double* xs, double* 
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = q + 4 * r;
-    acc[r] = (i >= j) ? lb[base + i + 16 * j] : lb[base + j + 16 * i];
+    acc[r] = (i >= j) ? lb[base + db_e(i, j)] : lb[base + db_e(j, i)];
     Y[r] = (i == j) ? 1.0 : 0.0;
   }
   int bad = 0;
@@ -216,8 +216,8 @@ __device__ __forceinline__ void leaf_mfma_probe(double* lb, double* xs, double* 
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int c = q + 4 * r;
-    lb[base + j + 16 * c] = (j >= c) ? acc[r] : Y[r];
-    xs[c + 16 * j] = Y[r];
+    lb[base + db_e(j, c)] = (j >= c) ? acc[r] : Y[r];
+    xs[db_e(c, j)] = Y[r];
     if (j == c) xdiag[jb * 16 + c] = Y[r];
   }
 }
@@ -237,7 +237,7 @@ __global__ void __launch_bounds__(64) k_leaf(const double* A, double* out, unsig
   if (lane == 0) *flag = 0;
   unsigned long long acc = 0, accs = 0;
   for (int r = 0; r < reps; ++r) {
-    for (int e = lane; e < 256; e += 64) lb[e] = A[e];     // block (0,0), column-major
+    for (int e = lane; e < 256; e += 64) lb[db_e(e & 15, e >> 4)] = A[e];     // block (0,0)
     __syncthreads();
     const unsigned long long t0 = wall_clock64();
     const unsigned long long s0 = clock64();
@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(64) k_leaf(const double* A, double* out, unsig
     acc += t1 - t0;
     accs += s1 - s0;
   }
-  for (int e = lane; e < 256; e += 64) out[e] = lb[e], out[256 + e] = xs[e];
+  for (int e = lane; e < 256; e += 64) out[e] = lb[db_e(e & 15, e >> 4)], out[256 + e] = xs[db_e(e & 15, e >> 4)];
   if (lane == 0) t[0] = acc, t[1] = accs;
 }
 
