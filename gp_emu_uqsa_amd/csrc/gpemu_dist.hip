@@ -384,6 +384,8 @@ struct gpe_dist {
   int slab_rows = 1;                           // tile rows per slab of A^-1
   double* dT2 = nullptr;
   GemmProb* gprobs = nullptr;
+  double* wsplit = nullptr;                    // split-K partials of the W launch
+  int* wcnt = nullptr;                         // its per-tile arrival counters
   unsigned* gtiles = nullptr;                  // tile lists of the gradient launches
   std::vector<DLaunch> wa_l;
   std::vector<TriChunk> tri;                   // the recursive TRTRI, level by level
@@ -600,8 +602,11 @@ int next_group_end(const gpe_dist* h, int k) {
   return g + 2 < (int)h->gs.size() ? h->gs[g + 2] : h->NB;
 }
 
-// the panel buffer of step k's group (double-buffered by group parity)
+// the panel buffer of step k's group (double-buffered by group parity); with one rank the
+// gathered panels would be the rank's own columns in the same layout: its tile rows
+int gather_panels(const gpe_dist* h) { return h->P > 1; }
 double* panel_of(const gpe_dist* h, const Rank& R, int k) {
+  if (!gather_panels(h)) return R.A + (long long)h->gstart[k] * TILE * R.ld;
   return R.panel + (size_t)(h->gid[k] & 1) * h->panel_sz;
 }
 
@@ -827,6 +832,9 @@ int ensure_grad(gpe_dist* h) {
   // slab of the A^-1 partial (and the TRTRI's gathered blocks): as many tile rows as
   // fit SLAB_DOUBLES, or GPEMU_DIST_SLAB_MB MiB (at least one tile row)
   long long slab_doubles = (long long)SLAB_DOUBLES;
+  // the whole lower triangle's tile rows in one slab when they take at most 4x that
+  // (n <= 16384: the partial then forms in one launch, as the single-GPU LAUUM)
+  if ((long long)NB * TILE * np <= 4 * (long long)SLAB_DOUBLES) slab_doubles = (long long)NB * TILE * np;
   if (const char* e = std::getenv("GPEMU_DIST_SLAB_MB")) slab_doubles = std::max(1ll, std::atoll(e)) << 17;
   h->slab_rows = (int)std::max<long long>(1, std::min<long long>(NB, slab_doubles / (TILE * np)));
   const long long lds = (long long)h->slab_rows * TILE;
@@ -988,6 +996,14 @@ int ensure_grad(gpe_dist* h) {
     DCHK(dalloc(h, &h->dmoves, moves.size(), &h->shared_bytes));
     DCHK_HIP(h, hipMemcpy(h->dmoves, moves.data(), moves.size() * sizeof(MoveDesc), hipMemcpyHostToDevice));
   }
+  {   // the W launch's split-K scratch (shared by the local ranks' launches, stream-ordered)
+    const int ntw = NB * h->NA, ks = std::max(1, std::min(8, 512 / std::max(ntw, 1)));
+    if (ks > 1) {
+      DCHK(dalloc(h, &h->wsplit, (size_t)ntw * ks * TILE * TILE, &h->shared_bytes));
+      DCHK(dalloc(h, &h->wcnt, (size_t)ntw, &h->shared_bytes));
+      DCHK_HIP(h, hipMemset(h->wcnt, 0, (size_t)ntw * sizeof(int)));
+    }
+  }
   h->wa_l.assign(h->ranks.size(), DLaunch());
   h->slabs.assign(h->ranks.size(), std::vector<SlabLaunch>());
   for (size_t s = 0; s < h->ranks.size(); ++s) {
@@ -995,20 +1011,29 @@ int ensure_grad(gpe_dist* h) {
     DLaunch wl;
     wl.kind = 2;
     wl.first = (int)probs.size();
+    // W(a) = X_r(:, a)^T R2_r over its rows >= a: one tile row of W per a, K up to n -- a
+    // launch of NB tiles, so K is split over up to 8 workgroups per tile (last-arriver
+    // reduction in index order, as the single-GPU split_k)
+    const int ntw = (R.nlx > 0 ? NB : 0) * h->NA;
+    const int ks = ntw > 0 ? std::max(1, std::min(8, 512 / ntw)) : 1;
     for (int a = 0; a < NB; ++a) {
       const int ls = lstart_of(a, P, R.rank), K = (R.nlx - ls) * TILE;
       if (K <= 0) continue;
-      // W(a) += X_r(:, a)^T R2_r over its rows >= a
       GemmProb p = dprob(R.X + (long long)ls * TILE + (long long)a * TILE * R.ld, R.ld,
                          R.r2loc + (long long)ls * TILE, R.ld, R.wpart + (long long)a * TILE, np,
-                         1, h->NA, K, 0, 1.0, 1.0);
-      p.tile_begin = wl.tiles;
-      p.ntiles = h->NA;
+                         1, h->NA, K, 0, 1.0, 0.0);
+      if (ks > 1) {
+        p.ksplit = ks;
+        p.part = h->wsplit + (size_t)wl.tiles * ks * TILE * TILE;
+        p.tcnt = h->wcnt + wl.tiles;
+      }
+      p.tile_begin = wl.tiles * ks;
+      p.ntiles = h->NA * ks;
       wl.tiles += h->NA;
       ++wl.count;
-      wl.cdef = wl.cdef || gemm_cdef(p);
       probs.push_back(p);
     }
+    wl.tiles *= ks;
     h->wa_l[s] = wl;
     // partial of A^-1 by slabs of tile rows [a0, a1): P_r(a, 0:a+1) = X_r(:, a)^T X_r(:, 0:a+1)
     // over its rows >= a (K = 0 writes zeros), into slab row a - a0
@@ -1032,7 +1057,6 @@ int ensure_grad(gpe_dist* h) {
       h->slabs[s].push_back(sl);
     }
   }
-  for (DLaunch& L : h->wa_l) list_launch(L, probs, gt);
   for (auto& v : h->slabs)
     for (SlabLaunch& sl : v) list_launch(sl.gemm, probs, gt);
   if ((int)probs.size() > DIST_DESC_MAX) return dfail(h, GPE_ERR_UNSUPPORTED, "distributed gradient schedule too large");
@@ -1115,7 +1139,7 @@ int step(gpe_dist* h, int k) {
   const long long ldp = (long long)(h->NB + h->NA) * TILE;
   const long long pcol = (long long)(k - h->gstart[k]) * TILE * ldp;   // block of k in its group's panels
   const int T = h->maxT[k];
-  if (T > 0) {
+  if (T > 0 && gather_panels(h)) {
     const size_t seg = (size_t)T * TILE * TILE;
     for (Rank& R : h->ranks) {
       const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
@@ -1274,6 +1298,8 @@ void gpe_dist_destroy(gpe_dist* h) {
   dfree(&h->gprobs);
   dfree(&h->gtiles);
   dfree(&h->dmoves);
+  dfree(&h->wsplit);
+  dfree(&h->wcnt);
   if (h->hpin) (void)hipHostFree(h->hpin);
   for (hipEvent_t e : h->cev) (void)hipEventDestroy(e);
   if (h->e0) (void)hipEventDestroy(h->e0);
@@ -1315,6 +1341,8 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
   dfree(&h->gprobs);
   dfree(&h->gtiles);
   dfree(&h->dmoves);
+  dfree(&h->wsplit);
+  dfree(&h->wcnt);
   DCHK(pinned(h, (size_t)np * std::max(d, Pc) + 16));
   // X (row-major, zero padded)
   DCHK(dalloc(h, &h->dX, (size_t)np * d, &h->shared_bytes));
@@ -1355,8 +1383,10 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
     DCHK(dalloc(h, &B.A, (size_t)B.ld * (size_t)NT * TILE, &B.bytes));
     DCHK(dalloc(h, &B.logdet, (size_t)h->NB + 1, &B.bytes));
     DCHK(dalloc(h, &B.dinv, (size_t)TILE * TILE, &B.bytes));
-    DCHK(dalloc(h, &B.panel, 2 * h->panel_sz, &B.bytes));
-    DCHK(dalloc(h, &B.recv, (size_t)h->P * h->T0 * TILE * TILE, &B.bytes));
+    if (gather_panels(h)) {
+      DCHK(dalloc(h, &B.panel, 2 * h->panel_sz, &B.bytes));
+      DCHK(dalloc(h, &B.recv, (size_t)h->P * h->T0 * TILE * TILE, &B.bytes));
+    }
     DCHK(dalloc(h, &B.gram, (size_t)Pc * Pc, &B.bytes));
   }
   DCHK(build_schedule(h));
