@@ -372,7 +372,7 @@ int prob_tiles(const GemmProb& p) {
 
 // Split K over workgroups for a launch with few tiles (small n, the TRTRI's first levels):
 // there each tile's K loop on one CU is the launch's latency, and the chip has 512
-// workgroup slots.  ks shares of at least 128 K each, at most SPLIT_SLOTS partials; beta = 0
+// workgroup slots.  ks shares of at least 64 K each, at most SPLIT_SLOTS partials; beta = 0
 // problems only.  The launch then takes the implicit tile order (no list).
 constexpr int SPLIT_SLOTS = 512;
 void split_k(std::vector<GemmProb>& probs, double* part, int* tcnt) {
@@ -386,7 +386,9 @@ void split_k(std::vector<GemmProb>& probs, double* part, int* tcnt) {
     kmax = std::max(kmax, p.K);
   }
   if (T <= 0 || T >= 256) return;
-  const int ks = std::min({8, SPLIT_SLOTS / T, kmax / TILE});
+  // shares of at least 64 of K (4 stages): one 128 x 128 x 128 tile is ~16 us of fp64
+  // MFMA on one CU, the first TRTRI level's whole launch
+  const int ks = std::min({8, SPLIT_SLOTS / T, kmax / 64});
   if (ks < 2) return;
   int off = 0;
   for (GemmProb& p : probs) {

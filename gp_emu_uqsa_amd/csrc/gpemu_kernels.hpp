@@ -1248,17 +1248,31 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
       if (!*last) return;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       const double* p0 = P.part + (long long)tl * ks * (TILE * TILE);
+      // partial by partial, each one's 64 loads issued together (a load-add chain per
+      // element put ~ks x 64 dependent load latencies in front of the store: a 4-way split
+      // of a 16-tile TRTRI level took 70 us)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int e = ((i * 4 + j) * 4 + r) * 256 + tid;
-            double sum = gld1(p0 + e);
-            for (int c = 1; c < ks; ++c) sum += gld1(p0 + (long long)c * (TILE * TILE) + e);
-            acc[i][j][r] = sum;
-          }
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = gld1(p0 + ((i * 4 + j) * 4 + r) * 256 + tid);
+      for (int c = 1; c < ks; ++c) {
+        const double* pc = p0 + (long long)c * (TILE * TILE);
+        double t[4][4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t[i][j][r] = gld1(pc + ((i * 4 + j) * 4 + r) * 256 + tid);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[i][j][r] += t[i][j][r];
+      }
       if (tid == 0) __hip_atomic_store(P.tcnt + tl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
