@@ -1099,7 +1099,12 @@ int skinny(gpe_ctx* c, bool transposed, const double* M, long long ldm, int ntr,
                  Y + (long long)c0 * ldy, ldy));
     return GPE_OK;
   }
-  const int nch = lower ? (std::max(ntr, nit) + SK_CH - 1) / SK_CH : (ntr + SK_CH - 1) / SK_CH;
+  // k chunks of chk tiles: SK_CH, or fewer when the launch has few output tiles (small n:
+  // 8 row tiles with one chunk each left 8 workgroups walking all of K, ~35 us at n = 1024)
+  const int kext = lower ? std::max(ntr, nit) : ntr;
+  const int want = (256 + nit - 1) / nit;   // chunks per output tile for ~256 workgroups
+  const int chk = std::max(1, std::min(SK_CH, (kext + want - 1) / want));
+  const int nch = (kext + chk - 1) / chk;
   const long long rows = (long long)nit * TILE;
   const size_t need = (size_t)nch * rows * P;
   if (need > c->skp_cap) {
@@ -1111,6 +1116,7 @@ int skinny(gpe_ctx* c, bool transposed, const double* M, long long ldm, int ntr,
   a.M = M; a.ldm = ldm; a.R = R; a.ldr = ldr; a.part = c->dskp; a.ldp = rows;
   a.pstride = rows * P; a.P = P; a.ntr = ntr; a.lower = lower ? 1 : 0; a.nit = nit;
   a.abort_flag = c->dinfo;
+  a.chk = chk;
   dim3 grid(nit * nch);
   const bool p16 = P <= 16;
   if (!transposed) {
@@ -1126,7 +1132,7 @@ int skinny(gpe_ctx* c, bool transposed, const double* M, long long ldm, int ntr,
   // partial layout is [ch][p][rows]; reduce into Y (ld = ldy >= rows)
   if (ldy != rows) return fail(c, GPE_ERR_STATE, "skinny: output ld mismatch");
   hipLaunchKernelGGL(k_reduce_chunks, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
-                     c->dskp, (long long)(rows * P), Y, rows, P, (int)rows, ntr, mode, c->dinfo);
+                     c->dskp, (long long)(rows * P), Y, rows, P, (int)rows, ntr, mode, c->dinfo, chk);
   HIPCHK(c, hipGetLastError());
   return GPE_OK;
 }
@@ -2004,6 +2010,7 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
       SkinnyArgs a;
       a.M = c->dW1; a.ldm = np; a.R = c->dWa + (long long)c0 * np; a.ldr = np; a.part = c->dskp; a.ldp = mp;
       a.pstride = mp * pc; a.P = pc; a.ntr = c->NB; a.lower = 0; a.nit = mt; a.abort_flag = nullptr;
+      a.chk = SK_CH;
       dim3 grid(mt * nch);
       if (pc <= 16) {
         hipLaunchKernelGGL((k_skinny_mfma<16, true>), grid, dim3(256), 0, c->stream, a);
@@ -2014,7 +2021,7 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
       const long long tot = mp * pc;
       hipLaunchKernelGGL(k_reduce_chunks, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
                          c->dskp, (long long)(mp * pc), dY + (long long)c0 * mp, mp, pc, (int)mp, c->NB, 2,
-                         nullptr);
+                         nullptr, SK_CH);
       HIPCHK(c, hipGetLastError());
     }
     // V = L^-1 K*   (np x mp), X lower-triangular -> kend = (ti+1)*128

@@ -1527,6 +1527,7 @@ struct SkinnyArgs {
   int lower;           // 1: M lower-triangular by tiles
   int nit;             // output tiles
   const int* abort_flag;
+  int chk;             // k tiles per chunk (<= SK_CH; fewer for launches of few output tiles)
 };
 
 // ---------------------------------------------------------------------------
@@ -1742,14 +1743,14 @@ static __global__ void __launch_bounds__(256) k_skinny_mfma(SkinnyArgs a) {
   int kt0, kt1;
   if (TR) {
     const int kbase = a.lower ? it : 0;
-    kt0 = kbase + ch * SK_CH;
+    kt0 = kbase + ch * a.chk;
     if (kt0 >= a.ntr) return;
-    kt1 = min(kt0 + SK_CH, a.ntr);
+    kt1 = min(kt0 + a.chk, a.ntr);
   } else {
     const int kend = a.lower ? it + 1 : a.ntr;
-    kt0 = ch * SK_CH;
+    kt0 = ch * a.chk;
     if (kt0 >= kend) return;
-    kt1 = min(kt0 + SK_CH, kend);
+    kt1 = min(kt0 + a.chk, kend);
   }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int P = a.P;
@@ -1801,16 +1802,16 @@ static __global__ void __launch_bounds__(256) k_skinny_mfma(SkinnyArgs a) {
 // nch(i) for the n-kernel (lower): ceil((it+1)/CH); t-kernel lower: ceil((ntr-it)/CH)
 static __global__ void k_reduce_chunks(const double* part, long long pstride, double* out,
                                 long long ldp, int P, int nrows, int ntr, int mode,
-                                const int* abort_flag) {
+                                const int* abort_flag, int chk) {
   if (abort_flag && *abort_flag) return;
   long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (long long)nrows * P) return;
   int i = (int)(e % nrows), p = (int)(e / nrows);
   int it = i / TILE;
   int nch;
-  if (mode == 0) nch = (it + SK_CH) / SK_CH;                 // lower, n-kernel
-  else if (mode == 1) nch = (ntr - it + SK_CH - 1) / SK_CH;  // lower, t-kernel
-  else nch = (ntr + SK_CH - 1) / SK_CH;                      // full
+  if (mode == 0) nch = (it + chk) / chk;                 // lower, n-kernel
+  else if (mode == 1) nch = (ntr - it + chk - 1) / chk;  // lower, t-kernel
+  else nch = (ntr + chk - 1) / chk;                      // full
   double s = 0.0;
   for (int ch = 0; ch < nch; ++ch) s += part[ch * pstride + i + (long long)p * ldp];
   out[i + (long long)p * ldp] = s;
