@@ -1,0 +1,15 @@
+# round-4 A/B (dev tool): the diagonal factor as a separate (noinline) device function
+# against the head: phases, two-try bench, chain trace, small n; alternating, twice
+mkdir -p gpurun_out
+for rep in 1 2; do
+  for L in libgpemu.so libgpemu_ni.so; do
+    echo "== $L rep $rep"
+    for n in 16384 4096; do GPEMU_LIB=gp_emu_uqsa_amd/$L timeout -k 10 120 python3 tools/quick_time.py $n 10 || exit 1; done
+    GPEMU_LIB=gp_emu_uqsa_amd/$L timeout -k 10 200 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline \
+      --no-other-configs --no-profile 2>/dev/null | tail -1 | cut -c1-200 || exit 1
+  done
+done > gpurun_out/ab_r04l.log 2>&1
+for L in libgpemu_trace.so libgpemu_ni_trace.so; do
+  echo "== $L"; GPEMU_LIB=gp_emu_uqsa_amd/$L timeout -k 10 120 python3 tools/chol_trace.py 4096 || exit 1
+done > gpurun_out/chol_ab_r04l.log 2>&1
+GPEMU_LIB=gp_emu_uqsa_amd/libgpemu_ni.so timeout -k 10 120 python3 tools/small_n_time.py > gpurun_out/small_n_r04l_ni.log 2>&1
