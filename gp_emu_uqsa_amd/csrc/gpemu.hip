@@ -305,18 +305,22 @@ int launch_pairs(gpe_ctx* c, const PairArgs& a, int nblocks) {
   int dm = 32;
   for (int w : widths)
     if (a.d <= w) { dm = w; break; }
-  const dim3 g(nblocks), b(256);
+  // launches of few tiles (small n) split each tile's columns over up to 4 workgroups
+  // (same values: every entry is computed as before, by another workgroup)
+  PairArgs a2 = a;
+  while (a2.csplit < 4 && nblocks * a2.csplit * 2 <= 512) a2.csplit *= 2;
+  const dim3 g(nblocks * a2.csplit), b(256);
   switch (dm) {
-    case 2: hipLaunchKernelGGL(k_pairs<2>, g, b, 0, c->stream, a); break;
-    case 4: hipLaunchKernelGGL(k_pairs<4>, g, b, 0, c->stream, a); break;
-    case 6: hipLaunchKernelGGL(k_pairs<6>, g, b, 0, c->stream, a); break;
-    case 8: hipLaunchKernelGGL(k_pairs<8>, g, b, 0, c->stream, a); break;
-    case 10: hipLaunchKernelGGL(k_pairs<10>, g, b, 0, c->stream, a); break;
-    case 12: hipLaunchKernelGGL(k_pairs<12>, g, b, 0, c->stream, a); break;
-    case 16: hipLaunchKernelGGL(k_pairs<16>, g, b, 0, c->stream, a); break;
-    case 20: hipLaunchKernelGGL(k_pairs<20>, g, b, 0, c->stream, a); break;
-    case 24: hipLaunchKernelGGL(k_pairs<24>, g, b, 0, c->stream, a); break;
-    default: hipLaunchKernelGGL(k_pairs<32>, g, b, 0, c->stream, a); break;
+    case 2: hipLaunchKernelGGL(k_pairs<2>, g, b, 0, c->stream, a2); break;
+    case 4: hipLaunchKernelGGL(k_pairs<4>, g, b, 0, c->stream, a2); break;
+    case 6: hipLaunchKernelGGL(k_pairs<6>, g, b, 0, c->stream, a2); break;
+    case 8: hipLaunchKernelGGL(k_pairs<8>, g, b, 0, c->stream, a2); break;
+    case 10: hipLaunchKernelGGL(k_pairs<10>, g, b, 0, c->stream, a2); break;
+    case 12: hipLaunchKernelGGL(k_pairs<12>, g, b, 0, c->stream, a2); break;
+    case 16: hipLaunchKernelGGL(k_pairs<16>, g, b, 0, c->stream, a2); break;
+    case 20: hipLaunchKernelGGL(k_pairs<20>, g, b, 0, c->stream, a2); break;
+    case 24: hipLaunchKernelGGL(k_pairs<24>, g, b, 0, c->stream, a2); break;
+    default: hipLaunchKernelGGL(k_pairs<32>, g, b, 0, c->stream, a2); break;
   }
   HIPCHK(c, hipGetLastError());
   return GPE_OK;

@@ -49,6 +49,7 @@ struct PairArgs {
   const double* r;
   const double* fcol = nullptr;
   double fscale = 0.0;
+  int csplit = 1;     // k_pairs: workgroups per tile, each a contiguous share of its columns
 };
 
 __device__ inline void tri_decode(int e, int& ti, int& tj) {
@@ -67,8 +68,9 @@ template <int DMAX>
 static __global__ void __launch_bounds__(256) k_pairs(PairArgs a) {
   __shared__ double xs_col[TILE * DMAX];
   int ti, tj;
-  if (a.mode & 1) tri_decode(blockIdx.x, ti, tj);
-  else { ti = blockIdx.x % a.mt; tj = blockIdx.x / a.mt; }
+  const int part = (int)blockIdx.x % a.csplit, blk = (int)blockIdx.x / a.csplit;
+  if (a.mode & 1) tri_decode(blk, ti, tj);
+  else { ti = blk % a.mt; tj = blk / a.mt; }
   const int tid = threadIdx.x;
   const int d = a.d;
   for (int e = tid; e < TILE * DMAX; e += 256) {
@@ -89,7 +91,8 @@ static __global__ void __launch_bounds__(256) k_pairs(PairArgs a) {
   if (train && a.r && ti == tj && !row_pad) vdiag += a.rscale * a.r[gi];
   const double fi = a.fcol ? a.fcol[gi] : 0.0;
   double* out = a.out + gi;
-  for (int c = (tid >> 7); c < TILE; c += 2) {
+  const int cw = TILE / a.csplit, cend = (part + 1) * cw;
+  for (int c = part * cw + (tid >> 7); c < cend; c += 2) {
     const int gj = tj * TILE + c;
     double s = 0.0;
 #pragma unroll
