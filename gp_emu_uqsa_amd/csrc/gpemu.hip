@@ -1526,7 +1526,7 @@ int gpe_set_data(gpe_ctx* c, int64_t n, int32_t d, int32_t q, const double* X, c
     CHK(dalloc(c, &c->dZ, (size_t)n_pad * cols));
     CHK(dalloc(c, &c->dR2, (size_t)n_pad * cols));
     CHK(dalloc(c, &c->dWa, (size_t)n_pad * cols));
-    const size_t cp = (size_t)c->NB * (c->NB + 1) / 2 * (d + 3);
+    const size_t cp = (size_t)c->NB * (c->NB + 1) / 2 * (d + 3) * 4;   // (up to 4 per tile: k_contract csplit)
     CHK(dalloc(c, &c->dcpart, cp));
     c->cpart_cap = cp;
   }
@@ -1662,19 +1662,23 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
     const double* rdiag = (gp4ml && kernel == GPE_KERNEL_STD && c->has_r) ? c->dr : nullptr;
     const int nblk = c->NB * (c->NB + 1) / 2;
     const int bucket = std::max(d, P);
+    int cs = 1;   // few tiles (small n): each tile's columns over up to 4 workgroups
+    if (!(d > 32 || P > 33))
+      while (cs < 4 && nblk * cs * 2 <= 512) cs *= 2;
+    const dim3 gc(nblk * cs);
     if (d > 32 || P > 33) {   // any d and q: staged through LDS in chunks of 32
       hipLaunchKernelGGL(k_contract_wide, dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
     } else if (d == 10 && P <= 13) {   // the headline configuration: no padded dimensions
-      hipLaunchKernelGGL((k_contract<10, 13>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
+      hipLaunchKernelGGL((k_contract<10, 13>), gc, dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag, cs);
     } else if (bucket <= 8) {
-      hipLaunchKernelGGL((k_contract<8, 9>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
+      hipLaunchKernelGGL((k_contract<8, 9>), gc, dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag, cs);
     } else if (bucket <= 16) {
-      hipLaunchKernelGGL((k_contract<16, 17>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
+      hipLaunchKernelGGL((k_contract<16, 17>), gc, dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag, cs);
     } else {
-      hipLaunchKernelGGL((k_contract<32, 33>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
+      hipLaunchKernelGGL((k_contract<32, 33>), gc, dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag, cs);
     }
     HIPCHK(c, hipGetLastError());
-    hipLaunchKernelGGL(k_reduce_rows, dim3(d + 3), dim3(256), 0, c->stream, c->dcpart, nblk, d + 3, c->dcsum);
+    hipLaunchKernelGGL(k_reduce_rows, dim3(d + 3), dim3(256), 0, c->stream, c->dcpart, nblk * cs, d + 3, c->dcsum);
     HIPCHK(c, hipGetLastError());
     ev_rec(c, 7);
     HIPCHK(c, hipMemcpyAsync(c->hpin, c->dcsum, (d + 3) * sizeof(double), hipMemcpyDeviceToHost, c->stream));

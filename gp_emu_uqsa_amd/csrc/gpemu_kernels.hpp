@@ -1945,13 +1945,17 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
                                                   const double* Wa, long long ldw, int q1,
                                                   int n_valid, double* part,
                                                   const int* abort_flag, int blk0 = 0,
-                                                  long long row0 = 0, const double* rdiag = nullptr) {
+                                                  long long row0 = 0, const double* rdiag = nullptr,
+                                                  int csplit = 1) {
   __shared__ double xs[TILE * DMAX];
   __shared__ double ws[TILE * QMAX];
   __shared__ double red[4 * (DMAX + 3)];
   if (abort_flag && *abort_flag) return;
   int ti, tj;
-  const int blk = blk0 + (int)blockIdx.x;
+  // csplit workgroups per tile (launches of few tiles), each a contiguous share of its
+  // columns with a partial of its own: part row blk * csplit + share
+  const int share = (int)blockIdx.x % csplit;
+  const int blk = blk0 + (int)blockIdx.x / csplit;
   tri_decode(blk, ti, tj);
   const int tid = threadIdx.x;
   // zero-padded to DMAX / QMAX: the padded terms are exact no-ops (fma(-0, 0, m) = m,
@@ -1979,9 +1983,10 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
   __syncthreads();
   if (gi < n_valid) {
     const double* acol = Ainv + (gi - row0) + (long long)tj * TILE * lda;
-    const int cend = min((ti == tj) ? r + 1 : TILE, n_valid - tj * TILE);
+    const int cw = TILE / csplit, cbeg = share * cw;
+    const int cend = min(min((ti == tj) ? r + 1 : TILE, n_valid - tj * TILE), cbeg + cw);
     // columns c = (tid >> 7) + 2u, four loads in flight ahead of the arithmetic
-    for (int c0 = (tid >> 7); c0 < cend; c0 += 8) {
+    for (int c0 = cbeg + (tid >> 7); c0 < cend; c0 += 8) {
       double mv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -2033,7 +2038,7 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
   if (tid < nv) {
     const double s = (red[tid] + red[(DMAX + 3) + tid]) +
                      (red[2 * (DMAX + 3) + tid] + red[3 * (DMAX + 3) + tid]);
-    part[(long long)blk * nv + tid] = s;
+    part[((long long)blk * csplit + share) * nv + tid] = s;
   }
 }
 
