@@ -798,10 +798,8 @@ int build_plan(gpe_ctx* c, Fact& F) {
           // row t of the group's panels is all the pending update reads: the previous step's
           // first panel tile (row t; the rest of that row was done before it started), not
           // all of that step's panels, which the quadrants waited for until round 4
-          if (h >= 1) {   // (step 0's inputs come from the previous launch)
-            dq.pre0 = cnt_first + t - 1;
-            dq.pre0_n = 2;
-          }
+          dq.pre0 = cnt_first + t - 1;
+          dq.pre0_n = 2;
           fp.push_back(dq);
           codes((int)fp.size() - 1, seg[h]);
         }
