@@ -554,7 +554,6 @@ GemmProb mkprob(const double* A, long long lda, const double* B, long long ldb, 
   p.pre0 = p.pre1 = p.post = nullptr; p.pre0_n = p.pre1_n = 0;
   p.ksplit = 1; p.part = nullptr; p.tcnt = nullptr;
   p.cpost = nullptr;
-  p.post_first = nullptr;
   return p;
 }
 
