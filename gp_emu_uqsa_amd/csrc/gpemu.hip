@@ -68,7 +68,7 @@ struct Plan {
 // panel counters, the list tickets of the Cholesky launches (one per column step), the
 // diagonal tiles' quadrant counters (G_DQUAD) and the panel tiles' stored-update counters
 // (G_PHALF0)
-constexpr int FACT_FLAG_INTS = 7;
+constexpr int FACT_FLAG_INTS = 6;
 
 // A factorisation workspace: two n_pad x n_pad buffers and their GEMM schedule.
 struct Fact {
@@ -746,7 +746,6 @@ int build_plan(gpe_ctx* c, Fact& F) {
     gidx.assign(NB, -1);
     int* cnt_col = F.flags + NB;
     int* cnt_pan = F.flags + 2 * NB;
-    int* cnt_first = F.flags + 6 * NB;   // both halves of step t's first panel tile (row t+1)
     for (int gi = 0; gi + 1 < (int)gs.size(); ++gi) {
       const int gb = gs[gi], ge = gs[gi + 1], W1 = ge - gb;
       if (W1 < 2) {
@@ -794,11 +793,6 @@ int build_plan(gpe_ctx* c, Fact& F) {
         if (K) {   // the step's hand-offs gate its diagonal tile's quadrants
           GemmProb dq = dquad(t, tile(A, t, p0), K, al);
           wire(dq);
-          // row t of the group's panels is all the pending update reads: the previous step's
-          // first panel tile (row t; the rest of that row was done before it started), not
-          // all of that step's panels, which the quadrants waited for until round 4
-          dq.pre0 = cnt_first + t - 1;
-          dq.pre0_n = 2;
           fp.push_back(dq);
           codes((int)fp.size() - 1, seg[h]);
         }
@@ -813,7 +807,6 @@ int build_plan(gpe_ctx* c, Fact& F) {
           GemmProb q = panelprob(t, K ? tile(A, t + 1, p0) : nullptr, K ? tile(A, t, p0) : nullptr, K, al);
           wire(q);
           q.post = cnt_pan + t;
-          if (h + 1 < W1) q.post_first = cnt_first + t;
           fp.push_back(q);
           codes((int)fp.size() - 1, seg[h]);
           fl += 2.0 * m * T * T * K + (double)m * T * T * T;
@@ -885,7 +878,6 @@ int build_plan(gpe_ctx* c, Fact& F) {
           const GemmProb& q = fp[order[i] >> 24];
           if (q.post) last_post[q.post] = i;
           if (q.cpost) last_post[q.cpost] = i;
-          if (q.post_first) last_post[q.post_first] = i;
           if (q.flags & G_DIAG) diag_at[q.flag] = i;
         }
         for (size_t i = 0; i < order.size(); ++i) {

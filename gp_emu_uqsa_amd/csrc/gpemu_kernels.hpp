@@ -233,8 +233,6 @@ struct GemmProb {
   int* post;
   int pre0_n, pre1_n;
   int* cpost;         // G_PHALF0: counted once the tile's pending update is stored
-  int* post_first;    // G_PANEL: also counted by the problem's first tile (the next diagonal
-                      // tile's row: the next step's pending update waits for it alone)
   // split K (plain instances, beta = 0, implicit tile order): ksplit workgroups per tile,
   // each over a contiguous share of the K stages; each stores its partial 128 x 128 sum
   // in part (slot tile * ksplit + kpart) and counts itself in tcnt[tile]; the last to
@@ -1221,7 +1219,6 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
       panel_subst(pa, P.Ld, P.ldd, P.X, P.ldx, lds, pt, P, ti);
       if (h0 && ti == 0) GTRACE(P, 7);
       if (P.post) gemm_post_count(P.post);
-      if (P.post_first && ti == 0) gemm_post_count(P.post_first);
 #ifdef GEMM_TTRACE
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
