@@ -441,7 +441,7 @@ __device__ __forceinline__ int db_blk(int bi, int bk) { return (bi * (bi + 1) / 
 // assemble = false: return there; the rest of X is assembled later, off the Cholesky's
 // chain, for all diagonal tiles at once (k_xasm: it reads L and the stored leaf inverses).
 template <class OnFactored>
-__device__ __attribute__((noinline)) int db_factor_invert(double* lb, double* Lg, long long ldl, double* Xg,
+__device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long long ldl, double* Xg,
                                                 long long ldx, double* logdet_out, OnFactored on_factored,
                                                 bool assemble = true) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
