@@ -305,18 +305,22 @@ int launch_pairs(gpe_ctx* c, const PairArgs& a, int nblocks) {
   int dm = 32;
   for (int w : widths)
     if (a.d <= w) { dm = w; break; }
-  const dim3 g(nblocks), b(256);
+  // launches of few tiles (small n) split each tile's columns over up to 4 workgroups
+  // (same values: every entry is computed as before, by another workgroup)
+  PairArgs a2 = a;
+  while (a2.csplit < 4 && nblocks * a2.csplit * 2 <= 512) a2.csplit *= 2;
+  const dim3 g(nblocks * a2.csplit), b(256);
   switch (dm) {
-    case 2: hipLaunchKernelGGL(k_pairs<2>, g, b, 0, c->stream, a); break;
-    case 4: hipLaunchKernelGGL(k_pairs<4>, g, b, 0, c->stream, a); break;
-    case 6: hipLaunchKernelGGL(k_pairs<6>, g, b, 0, c->stream, a); break;
-    case 8: hipLaunchKernelGGL(k_pairs<8>, g, b, 0, c->stream, a); break;
-    case 10: hipLaunchKernelGGL(k_pairs<10>, g, b, 0, c->stream, a); break;
-    case 12: hipLaunchKernelGGL(k_pairs<12>, g, b, 0, c->stream, a); break;
-    case 16: hipLaunchKernelGGL(k_pairs<16>, g, b, 0, c->stream, a); break;
-    case 20: hipLaunchKernelGGL(k_pairs<20>, g, b, 0, c->stream, a); break;
-    case 24: hipLaunchKernelGGL(k_pairs<24>, g, b, 0, c->stream, a); break;
-    default: hipLaunchKernelGGL(k_pairs<32>, g, b, 0, c->stream, a); break;
+    case 2: hipLaunchKernelGGL(k_pairs<2>, g, b, 0, c->stream, a2); break;
+    case 4: hipLaunchKernelGGL(k_pairs<4>, g, b, 0, c->stream, a2); break;
+    case 6: hipLaunchKernelGGL(k_pairs<6>, g, b, 0, c->stream, a2); break;
+    case 8: hipLaunchKernelGGL(k_pairs<8>, g, b, 0, c->stream, a2); break;
+    case 10: hipLaunchKernelGGL(k_pairs<10>, g, b, 0, c->stream, a2); break;
+    case 12: hipLaunchKernelGGL(k_pairs<12>, g, b, 0, c->stream, a2); break;
+    case 16: hipLaunchKernelGGL(k_pairs<16>, g, b, 0, c->stream, a2); break;
+    case 20: hipLaunchKernelGGL(k_pairs<20>, g, b, 0, c->stream, a2); break;
+    case 24: hipLaunchKernelGGL(k_pairs<24>, g, b, 0, c->stream, a2); break;
+    default: hipLaunchKernelGGL(k_pairs<32>, g, b, 0, c->stream, a2); break;
   }
   HIPCHK(c, hipGetLastError());
   return GPE_OK;
@@ -1514,7 +1518,7 @@ int gpe_set_data(gpe_ctx* c, int64_t n, int32_t d, int32_t q, const double* X, c
     CHK(dalloc(c, &c->dZ, (size_t)n_pad * cols));
     CHK(dalloc(c, &c->dR2, (size_t)n_pad * cols));
     CHK(dalloc(c, &c->dWa, (size_t)n_pad * cols));
-    const size_t cp = (size_t)c->NB * (c->NB + 1) / 2 * (d + 3);
+    const size_t cp = (size_t)c->NB * (c->NB + 1) / 2 * (d + 3) * 4;   // (up to 4 per tile: k_contract csplit)
     CHK(dalloc(c, &c->dcpart, cp));
     c->cpart_cap = cp;
   }
@@ -1650,19 +1654,23 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
     const double* rdiag = (gp4ml && kernel == GPE_KERNEL_STD && c->has_r) ? c->dr : nullptr;
     const int nblk = c->NB * (c->NB + 1) / 2;
     const int bucket = std::max(d, P);
+    int cs = 1;   // few tiles (small n): each tile's columns over up to 4 workgroups
+    if (!(d > 32 || P > 33))
+      while (cs < 4 && nblk * cs * 2 <= 512) cs *= 2;
+    const dim3 gc(nblk * cs);
     if (d > 32 || P > 33) {   // any d and q: staged through LDS in chunks of 32
       hipLaunchKernelGGL(k_contract_wide, dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
     } else if (d == 10 && P <= 13) {   // the headline configuration: no padded dimensions
-      hipLaunchKernelGGL((k_contract<10, 13>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
+      hipLaunchKernelGGL((k_contract<10, 13>), gc, dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag, cs);
     } else if (bucket <= 8) {
-      hipLaunchKernelGGL((k_contract<8, 9>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
+      hipLaunchKernelGGL((k_contract<8, 9>), gc, dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag, cs);
     } else if (bucket <= 16) {
-      hipLaunchKernelGGL((k_contract<16, 17>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
+      hipLaunchKernelGGL((k_contract<16, 17>), gc, dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag, cs);
     } else {
-      hipLaunchKernelGGL((k_contract<32, 33>), dim3(nblk), dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag);
+      hipLaunchKernelGGL((k_contract<32, 33>), gc, dim3(256), 0, c->stream, c->tr.A, np, c->dXw, d, c->dWa, np, P, (int)c->n, c->dcpart, c->dinfo, 0, 0ll, rdiag, cs);
     }
     HIPCHK(c, hipGetLastError());
-    hipLaunchKernelGGL(k_reduce_rows, dim3(d + 3), dim3(256), 0, c->stream, c->dcpart, nblk, d + 3, c->dcsum);
+    hipLaunchKernelGGL(k_reduce_rows, dim3(d + 3), dim3(256), 0, c->stream, c->dcpart, nblk * cs, d + 3, c->dcsum);
     HIPCHK(c, hipGetLastError());
     ev_rec(c, 7);
     HIPCHK(c, hipMemcpyAsync(c->hpin, c->dcsum, (d + 3) * sizeof(double), hipMemcpyDeviceToHost, c->stream));

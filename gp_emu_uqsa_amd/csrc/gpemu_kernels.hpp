@@ -49,6 +49,7 @@ struct PairArgs {
   const double* r;
   const double* fcol = nullptr;
   double fscale = 0.0;
+  int csplit = 1;     // k_pairs: workgroups per tile, each a contiguous share of its columns
 };
 
 __device__ inline void tri_decode(int e, int& ti, int& tj) {
@@ -67,8 +68,9 @@ template <int DMAX>
 static __global__ void __launch_bounds__(256) k_pairs(PairArgs a) {
   __shared__ double xs_col[TILE * DMAX];
   int ti, tj;
-  if (a.mode & 1) tri_decode(blockIdx.x, ti, tj);
-  else { ti = blockIdx.x % a.mt; tj = blockIdx.x / a.mt; }
+  const int part = (int)blockIdx.x % a.csplit, blk = (int)blockIdx.x / a.csplit;
+  if (a.mode & 1) tri_decode(blk, ti, tj);
+  else { ti = blk % a.mt; tj = blk / a.mt; }
   const int tid = threadIdx.x;
   const int d = a.d;
   for (int e = tid; e < TILE * DMAX; e += 256) {
@@ -89,7 +91,8 @@ static __global__ void __launch_bounds__(256) k_pairs(PairArgs a) {
   if (train && a.r && ti == tj && !row_pad) vdiag += a.rscale * a.r[gi];
   const double fi = a.fcol ? a.fcol[gi] : 0.0;
   double* out = a.out + gi;
-  for (int c = (tid >> 7); c < TILE; c += 2) {
+  const int cw = TILE / a.csplit, cend = (part + 1) * cw;
+  for (int c = part * cw + (tid >> 7); c < cend; c += 2) {
     const int gj = tj * TILE + c;
     double s = 0.0;
 #pragma unroll
@@ -1939,13 +1942,17 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
                                                   const double* Wa, long long ldw, int q1,
                                                   int n_valid, double* part,
                                                   const int* abort_flag, int blk0 = 0,
-                                                  long long row0 = 0, const double* rdiag = nullptr) {
+                                                  long long row0 = 0, const double* rdiag = nullptr,
+                                                  int csplit = 1) {
   __shared__ double xs[TILE * DMAX];
   __shared__ double ws[TILE * QMAX];
   __shared__ double red[4 * (DMAX + 3)];
   if (abort_flag && *abort_flag) return;
   int ti, tj;
-  const int blk = blk0 + (int)blockIdx.x;
+  // csplit workgroups per tile (launches of few tiles), each a contiguous share of its
+  // columns with a partial of its own: part row blk * csplit + share
+  const int share = (int)blockIdx.x % csplit;
+  const int blk = blk0 + (int)blockIdx.x / csplit;
   tri_decode(blk, ti, tj);
   const int tid = threadIdx.x;
   // zero-padded to DMAX / QMAX: the padded terms are exact no-ops (fma(-0, 0, m) = m,
@@ -1973,9 +1980,10 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
   __syncthreads();
   if (gi < n_valid) {
     const double* acol = Ainv + (gi - row0) + (long long)tj * TILE * lda;
-    const int cend = min((ti == tj) ? r + 1 : TILE, n_valid - tj * TILE);
+    const int cw = TILE / csplit, cbeg = share * cw;
+    const int cend = min(min((ti == tj) ? r + 1 : TILE, n_valid - tj * TILE), cbeg + cw);
     // columns c = (tid >> 7) + 2u, four loads in flight ahead of the arithmetic
-    for (int c0 = (tid >> 7); c0 < cend; c0 += 8) {
+    for (int c0 = cbeg + (tid >> 7); c0 < cend; c0 += 8) {
       double mv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -2027,7 +2035,7 @@ static __global__ void __launch_bounds__(256) k_contract(const double* Ainv, lon
   if (tid < nv) {
     const double s = (red[tid] + red[(DMAX + 3) + tid]) +
                      (red[2 * (DMAX + 3) + tid] + red[3 * (DMAX + 3) + tid]);
-    part[(long long)blk * nv + tid] = s;
+    part[((long long)blk * csplit + share) * nv + tid] = s;
   }
 }
 

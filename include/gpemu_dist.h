@@ -11,15 +11,17 @@
  * its tile rows of the lower triangle.  Per column step the owner factors the
  * diagonal tile in-kernel, RCCL broadcasts its inverse (128 KB), every rank forms
  * its panel tiles, RCCL all-gathers the panel column, and every rank applies the
- * trailing update to its own rows.  [f H] is carried as one extra tile row under
- * the matrix, so L^-1 [f H] and its Gram matrix fall out of the same sweep.
+ * trailing update to its own rows.  [f H] is carried as ceil((q+1)/128) extra tile
+ * rows under the matrix (dealt like the others), so L^-1 [f H] and its Gram matrix
+ * fall out of the same sweep.
  *
- * Gradient: X = L^-1 is formed by rows with the same partition (per step the
- * owner finishes X(k, :) and RCCL broadcasts it; every rank updates its own rows);
- * each rank then forms its partial X_r^T X_r of A^-1 slab by slab (a few tile rows
- * at a time, so per-rank memory stays O(n^2 / P)) and contracts it locally, so the
- * only other collectives are an all-reduce of the n x (q+1) matrix
- * [sqrt(c) alpha, W] and of the d+2 contraction sums.
+ * Gradient: X = L^-1 by the recursive TRTRI on the same partition: per level of
+ * block pairs, RCCL all-gathers the rows of X11 and, after each rank's columns of
+ * (L21 X11)^T, those columns; every rank then finishes its rows of X21 = -X22 L21 X11.
+ * Each rank forms its partial X_r^T X_r of A^-1 slab by slab (so per-rank memory
+ * stays O(n^2 / P)) and contracts it locally, so the only other collectives are an
+ * all-reduce of the n x (q+1) matrix [sqrt(c) alpha, W] and of the d+3 contraction
+ * sums.
  *
  * Processes: one per GPU.  Rank 0 calls gpe_dist_unique_id, the host shares the
  * 128 bytes (by default through the job's native file rendezvous,
@@ -27,7 +29,7 @@
  * alternative, distributed.share_unique_id), every rank calls gpe_dist_create with it.  unique_id == NULL selects the in-process
  * loopback transport: all P logical ranks live in this process on one GPU, each
  * with its own buffers, running the same partition, schedule and device code
- * (pack, all-gather buffer, unpermute, broadcast rows, all-reduced partials);
+ * (pack, all-gather buffers, unpermute, all-reduced partials);
  * only the collective calls become device copies (used to test P = 2..8 on one
  * GPU).
  *
@@ -67,7 +69,7 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
                        double* grad_out, double* sigma2_out);
 
 /* Partition map (pure functions, no GPU): owner rank of tile row t and the number
- * of tile rows (including the augmented [f H] row) rank `rank` stores. */
+ * of tile rows (including one augmented [f H] row: q + 1 <= 128) rank `rank` stores. */
 int32_t gpe_dist_owner(int32_t nranks, int32_t tile_row);
 int32_t gpe_dist_local_rows(int64_t n, int32_t nranks, int32_t rank);
 
