@@ -193,8 +193,11 @@ struct gpe_ctx {
   int potrf_mode = 0;
   int grp_p0 = 512, grp_stride = 896;
   // column-group widths of the fused Cholesky: {width, min remaining columns}, first
-  // match wins, else 1 (GPEMU_POTRF_W="4:64,2:32" style)
-  std::vector<std::pair<int, int>> potrf_groups = {{4, 80}, {2, 40}};
+  // match wins, else 1 (GPEMU_POTRF_W="4:64,2:32" style).  Round 4 (a shorter chain per
+  // step): 4 while more than 48 columns remain, then 2 while more than 24 -- at n = 16384
+  // the two-try bench 14.70 / 14.72 -> 14.78 / 14.81 evals/s and the Cholesky 28.4 -> 28.1 ms
+  // against round 3's {4, 80}, {2, 40} (profiles/group_width_ab_r04.log)
+  std::vector<std::pair<int, int>> potrf_groups = {{4, 48}, {2, 24}};
   // the fused Cholesky on the context's high-priority stream (default 1; 0: on the
   // context stream, GPEMU_CHOL_PRIO=0)
   int chol_prio = 1;
