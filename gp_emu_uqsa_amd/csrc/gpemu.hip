@@ -424,7 +424,7 @@ std::vector<unsigned> order_tiles(const std::vector<GemmProb>& probs) {
     for (int ti = 0; ti < P.mt; ++ti) {
       int kb = 0, ke = P.K;
       if (P.flags & G_KBEG_TI) kb = ti * TILE;
-      if (P.flags & G_KEND_TI) ke = std::min(ke, (ti + 1) * TILE);
+      if (P.flags & G_KEND_TI) ke = std::min(ke, (ti * P.kti_mul + P.kti_off + 1) * TILE);
       const double wt = (double)std::max(ke - kb, 0) + 2.0 * GK;   // + fixed per-tile cost
       Row r{p, ti, 0.0, {}};
       const int tjmax = (P.flags & G_CLOWER) ? ti : P.nt - 1;
@@ -557,6 +557,7 @@ GemmProb mkprob(const double* A, long long lda, const double* B, long long ldb, 
   p.pre0 = p.pre1 = p.post = nullptr; p.pre0_n = p.pre1_n = 0;
   p.ksplit = 1; p.part = nullptr; p.tcnt = nullptr;
   p.cpost = nullptr;
+  p.kti_mul = 1; p.kti_off = 0;
   return p;
 }
 

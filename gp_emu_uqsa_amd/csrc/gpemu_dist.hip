@@ -467,6 +467,7 @@ GemmProb dprob(const double* A, long long lda, const double* B, long long ldb, d
   p.lda = lda; p.ldb = ldb; p.ldc = ldc;
   p.mt = mt; p.nt = nt; p.K = K; p.flags = flags;
   p.alpha = alpha; p.beta = beta;
+  p.kti_mul = 1;
   return p;
 }
 
@@ -623,7 +624,7 @@ std::vector<unsigned> xcd_order(const GemmProb* probs, const std::vector<unsigne
     const GemmProb& P = probs[p];
     int kb = 0, ke = P.K;
     if (P.flags & G_KBEG_TI) kb = ti * TILE;
-    if (P.flags & G_KEND_TI) ke = std::min(ke, (ti + 1) * TILE);
+    if (P.flags & G_KEND_TI) ke = std::min(ke, (ti * P.kti_mul + P.kti_off + 1) * TILE);
     Row& r = rows[{p, ti}];
     r.tw = (double)std::max(ke - kb, 0) + 2.0 * GK;   // + fixed per-tile cost
     r.w += r.tw;
@@ -832,9 +833,11 @@ int ensure_grad(gpe_dist* h) {
   // slab of the A^-1 partial (and the TRTRI's gathered blocks): as many tile rows as
   // fit SLAB_DOUBLES, or GPEMU_DIST_SLAB_MB MiB (at least one tile row)
   long long slab_doubles = (long long)SLAB_DOUBLES;
-  // the whole lower triangle's tile rows in one slab when they take at most 4x that
-  // (n <= 16384: the partial then forms in one launch, as the single-GPU LAUUM)
-  if ((long long)NB * TILE * np <= 4 * (long long)SLAB_DOUBLES) slab_doubles = (long long)NB * TILE * np;
+  // when the whole lower triangle's tile rows take at most 4x that (n <= 16384), a slab
+  // of 1/P of them (at P = 1 the partial then forms in one launch, as the single-GPU
+  // LAUUM; per-rank memory stays O(n^2 / P): at P >= 4 the slab is the default)
+  const long long whole = (long long)NB * TILE * np;
+  if (whole <= 4 * (long long)SLAB_DOUBLES) slab_doubles = std::max(slab_doubles, whole / P);
   if (const char* e = std::getenv("GPEMU_DIST_SLAB_MB")) slab_doubles = std::max(1ll, std::atoll(e)) << 17;
   h->slab_rows = (int)std::max<long long>(1, std::min<long long>(NB, slab_doubles / (TILE * np)));
   const long long lds = (long long)h->slab_rows * TILE;
@@ -965,24 +968,28 @@ int ensure_grad(gpe_dist* h) {
                       (long long)tc.seg2, cw, pairs[p].t1 - pairs[p].h, 0, 2, pairs[p].h, P}, tc.unp2_tiles);
         tc.nunp2 = (int)moves.size() - tc.unp2;
       }
-      // X21(i, c0:c0+cw) = -X22(i, h:i+1) M(h:i+1, c0:c0+cw) for each of the rank's rows i
+      // X21(i, c0:c0+cw) = -X22(i, h:i+1) M(h:i+1, c0:c0+cw) for the rank's rows i of
+      // [h, t1): one problem per pair, local row ti = global row (ls + ti) P + rank with K
+      // up to its diagonal (G_KEND_TI with kti_mul = P)
       tc.x.kind = 4;
       tc.x.first = (int)probs.size();
       for (Rank& R : h->ranks)
         for (size_t p = 0; p < pairs.size(); ++p) {
           const int c0 = pairs[p].t0 + j0, hh = pairs[p].h;
+          const int ls = lstart_of(hh, P, R.rank);
           const int le = std::min(R.nlx, lstart_of(pairs[p].t1, P, R.rank));
-          for (int li = lstart_of(hh, P, R.rank); li < le; ++li) {
-            const int i = li * P + R.rank;
-            double* row = R.X + (long long)li * TILE;
-            GemmProb q = dprob(row + (long long)hh * TILE * R.ld, R.ld, R.slab + og2[p], (long long)cw * TILE,
-                               row + (long long)c0 * TILE * R.ld, R.ld, 1, cw, (i - hh + 1) * TILE, 0, -1.0, 0.0);
-            q.tile_begin = tc.x.tiles;
-            q.ntiles = cw;
-            tc.x.tiles += cw;
-            ++tc.x.count;
-            probs.push_back(q);
-          }
+          if (le <= ls) continue;
+          double* row = R.X + (long long)ls * TILE;
+          GemmProb q = dprob(row + (long long)hh * TILE * R.ld, R.ld, R.slab + og2[p], (long long)cw * TILE,
+                             row + (long long)c0 * TILE * R.ld, R.ld, le - ls, cw, (pairs[p].t1 - hh) * TILE,
+                             G_KEND_TI, -1.0, 0.0);
+          q.kti_mul = P;
+          q.kti_off = ls * P + R.rank - hh;
+          q.tile_begin = tc.x.tiles;
+          q.ntiles = (le - ls) * cw;
+          tc.x.tiles += q.ntiles;
+          ++tc.x.count;
+          probs.push_back(q);
         }
       h->tri.push_back(tc);
     }
@@ -1233,10 +1240,11 @@ int32_t gpe_dist_owner(int32_t nranks, int32_t tile_row) {
   return tile_row % nranks;
 }
 
-int32_t gpe_dist_local_rows(int64_t n, int32_t nranks, int32_t rank) {
-  if (n <= 0 || nranks <= 0 || rank < 0 || rank >= nranks) return -1;
+int32_t gpe_dist_local_rows(int64_t n, int32_t q, int32_t nranks, int32_t rank) {
+  if (n <= 0 || q < 0 || nranks <= 0 || rank < 0 || rank >= nranks) return -1;
   const int NB = (int)((n + TILE - 1) / TILE);
-  return nloc_of(NB, nranks, rank);
+  const int NA = (q + 1 + TILE - 1) / TILE;   // augmented [f H]^T tile rows (set_data)
+  return nloc_of(NB + NA - 1, nranks, rank);
 }
 
 gpe_dist* gpe_dist_create(int32_t device, int32_t nranks, int32_t rank, const uint8_t* unique_id) {

@@ -242,6 +242,9 @@ struct GemmProb {
   int ksplit;
   double* part;
   int* tcnt;
+  // G_KEND_TI: row tile ti's K ends at (ti kti_mul + kti_off + 1) x 128 (1, 0: the
+  // triangle's own rows; the row-block TRTRI: a rank's rows ti of a cyclic partition)
+  int kti_mul, kti_off;
 };
 
 // dev-tool per-tile timeline (-DGEMM_TTRACE build only, tools/hip/tile_probe.hip): per
@@ -1046,7 +1049,7 @@ static __global__ void __launch_bounds__(256, 2) k_gemm(const GemmProb* __restri
   }
   int kbeg = 0, kend = P.K;
   if (P.flags & G_KBEG_TI) kbeg = ti * TILE;
-  if (P.flags & G_KEND_TI) kend = min(kend, (ti + 1) * TILE);
+  if (P.flags & G_KEND_TI) kend = min(kend, (ti * P.kti_mul + P.kti_off + 1) * TILE);
   if (!FUSED && P.ksplit > 1) {   // this share of the tile's K stages
     const int ns = max(0, kend - kbeg) / GK;
     const int s0 = kpart * ns / P.ksplit, s1 = (kpart + 1) * ns / P.ksplit;

@@ -64,12 +64,14 @@ def dist_context(device: int | None = None, group=None) -> native.DistContext:
     return native.DistContext(device, world, rank, uid)
 
 
-def partition(n: int, nranks: int):
-    """Tile rows per rank: {rank: [global tile rows]} including the augmented row
-    (index ceil(n/128)), dealt cyclically -- the map libgpemu.so uses."""
+def partition(n: int, nranks: int, q: int = 0):
+    """Tile rows per rank: {rank: [global tile rows]} including the ceil((q+1)/128)
+    augmented [f H]^T rows (indices ceil(n/128) ...), dealt cyclically -- the map
+    libgpemu.so uses."""
     nb = (n + 127) // 128
+    na = (q + 1 + 127) // 128
     rows = {r: [] for r in range(nranks)}
-    for t in range(nb + 1):
+    for t in range(nb + na):
         rows[native.dist_owner(nranks, t)].append(t)
     return rows
 

@@ -74,7 +74,7 @@ SIGNATURES = {
     "gpe_dist_objective": (_ct.c_int, [_VP, _ct.c_int32, _ct.c_int32, _D, _ct.c_int32, _ct.c_double,
                                        _ct.c_int32, _D, _D, _D]),
     "gpe_dist_owner": (_ct.c_int32, [_ct.c_int32, _ct.c_int32]),
-    "gpe_dist_local_rows": (_ct.c_int32, [_ct.c_int64, _ct.c_int32, _ct.c_int32]),
+    "gpe_dist_local_rows": (_ct.c_int32, [_ct.c_int64, _ct.c_int32, _ct.c_int32, _ct.c_int32]),
     "gpe_dist_times": (_ct.c_int, [_VP, _D, _D]),
     "gpe_dist_rank_bytes": (_ct.c_int, [_VP, _ct.c_int32, _ct.POINTER(_ct.c_int64)]),
 }
@@ -583,6 +583,7 @@ def dist_owner(nranks: int, tile_row: int) -> int:
     return int(load_library().gpe_dist_owner(int(nranks), int(tile_row)))
 
 
-def dist_local_rows(n: int, nranks: int, rank: int) -> int:
-    """Tile rows (incl. the augmented [f H] row) rank `rank` stores (pure; no GPU)."""
-    return int(load_library().gpe_dist_local_rows(int(n), int(nranks), int(rank)))
+def dist_local_rows(n: int, nranks: int, rank: int, q: int = 0) -> int:
+    """Tile rows rank `rank` stores for n points and q basis columns, including its
+    share of the ceil((q+1)/128) augmented [f H]^T rows (pure; no GPU)."""
+    return int(load_library().gpe_dist_local_rows(int(n), int(q), int(nranks), int(rank)))

@@ -30,10 +30,11 @@
 extern "C" {
 #endif
 
-#define GPE_ABI_VERSION 8   /* 3: gpe_dist_objective gained want_grad / grad_out; 4: sensitivity;
+#define GPE_ABI_VERSION 9   /* 3: gpe_dist_objective gained want_grad / grad_out; 4: sensitivity;
                                 5: gpe_noise_sample (noise_fit); 6: gpe_kernel_grad;
                                 7: gpe_lhc_maximin; 8: gpe_dist_rank_bytes,
-                                gpe_device_synchronize, gpe_build_id */
+                                gpe_device_synchronize, gpe_build_id;
+                                9: gpe_dist_local_rows takes the basis width q */
 
 enum gpe_status {
     GPE_OK = 0,

@@ -62,16 +62,18 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
 /* Objective (and gradient when want_grad != 0), arguments and outputs as
  * gpe_objective.  All ranks call it collectively and all receive the same llh,
  * gradient and sigma2.  The gradient buffers (this rank's rows of L^-1 and a slab
- * of at most 512 MiB of its partial of A^-1) are allocated on the first want_grad
+ * of its partial of A^-1: 512 MiB, or 1/P of the triangle's tile rows when that is
+ * more and the triangle takes at most 2 GiB) are allocated on the first want_grad
  * call. */
 int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const double* hp,
                        int32_t n_hp, double nu_fixed, int32_t want_grad, double* llh_out,
                        double* grad_out, double* sigma2_out);
 
 /* Partition map (pure functions, no GPU): owner rank of tile row t and the number
- * of tile rows (including one augmented [f H] row: q + 1 <= 128) rank `rank` stores. */
+ * of tile rows rank `rank` stores for n points and q basis columns, including its
+ * share of the ceil((q+1)/128) augmented [f H]^T tile rows. */
 int32_t gpe_dist_owner(int32_t nranks, int32_t tile_row);
-int32_t gpe_dist_local_rows(int64_t n, int32_t nranks, int32_t rank);
+int32_t gpe_dist_local_rows(int64_t n, int32_t q, int32_t nranks, int32_t rank);
 
 /* Time of the last gpe_dist_objective: total and the part spent in collectives
  * (RCCL or loopback copies), ms, measured with HIP events on this rank. */

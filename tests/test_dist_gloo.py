@@ -27,14 +27,18 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("n,P", [(1, 1), (128, 2), (1000, 4), (16384, 8), (65536, 8), (700, 3)])
-def test_partition_map(n, P):
+@pytest.mark.parametrize("n,P,q", [(1, 1, 0), (128, 2, 3), (1000, 4, 11), (16384, 8, 11), (65536, 8, 21),
+                                   (700, 3, 0), (700, 3, 150), (1000, 4, 400)])
+def test_partition_map(n, P, q):
+    """Tile rows per rank including the ceil((q+1)/128) augmented rows (q = 150: two, as
+    set_data stores them for the linear mean of d = 150 inputs)."""
     nb = (n + 127) // 128
-    rows = distributed.partition(n, P)
-    assert sorted(t for r in rows.values() for t in r) == list(range(nb + 1))
+    na = (q + 1 + 127) // 128
+    rows = distributed.partition(n, P, q)
+    assert sorted(t for r in rows.values() for t in r) == list(range(nb + na))
     for r in range(P):
-        assert rows[r] == list(range(r, nb + 1, P))
-        assert native.dist_local_rows(n, P, r) == len(rows[r])
+        assert rows[r] == list(range(r, nb + na, P))
+        assert native.dist_local_rows(n, P, r, q) == len(rows[r])
     assert native.dist_owner(P, nb) == nb % P
 
 

@@ -174,25 +174,34 @@ def test_loopback_gradient_chunked_trtri(ctx, monkeypatch, P):
     assert ok, (g, gref, err)
 
 
-@pytest.mark.parametrize("P", [2, 3])
-def test_loopback_rank_memory(P):
+@pytest.mark.parametrize("n,P", [(4000, 2), (4000, 3), (10240, 4)])
+def test_loopback_rank_memory(n, P):
     """Each logical rank holds its own tile rows (of A and, after a gradient call, of
-    L^-1): the per-rank bytes follow the partition, not n^2."""
-    n, d = 4000, 3
+    L^-1): the per-rank bytes follow the partition, not n^2.  Upper bound after the
+    gradient: its rows of L^-1 plus at most three slab-sized buffers (the A^-1 partial's
+    slab, the TRTRI's gathered X11 and all-gather buffer), the slab being the whole
+    triangle's tile rows / P (at least 512 MiB, at most the whole) -- at n = 10240, P = 4
+    one n x n partial per rank (the round-4 slab) would exceed it."""
+    d = 3
     X, f, H = orc.synthetic_problem(n, d, seed=1)
     dc = native.DistContext(0, P)
     dc.set_data(X, f, H)
     nb = (n + 127) // 128
+    np_ = nb * 128
     val = [dc.rank_bytes(r) for r in range(P)]
     for r in range(P):
-        rows = native.dist_local_rows(n, P, r)
+        rows = native.dist_local_rows(n, P, r, d + 1)
         assert val[r] >= rows * 128 * (nb + 1) * 128 * 8            # its tile rows of A
         assert val[r] < (rows + 1) * 128 * (nb + 1) * 128 * 8 * 1.6   # plus panels and inputs
     dc.objective(native.GP4ML, native.KERNEL_STD, _hp(d), want_grad=True)
     grad = [dc.rank_bytes(r) for r in range(P)]
+    whole = nb * 128 * np_
+    slab = min(whole, max(1 << 26, whole // P)) * 8
     for r in range(P):
-        rows = native.dist_local_rows(n, P, r)
-        assert grad[r] - val[r] >= rows * 128 * nb * 128 * 8        # its rows of L^-1
+        rows = native.dist_local_rows(n, P, r, d + 1)
+        xrows = rows * 128 * nb * 128 * 8
+        assert grad[r] - val[r] >= xrows                            # its rows of L^-1
+        assert grad[r] - val[r] <= xrows + 3 * slab + (64 << 20), (grad[r] - val[r], xrows, slab)
     with pytest.raises(RuntimeError):
         dc.rank_bytes(P)
     dc.close()

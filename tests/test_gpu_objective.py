@@ -98,10 +98,20 @@ def test_objective_value_only_matches(ctx, n, d):
     ref = orc.objective_fast(X, f, H, hp, orc.GP4ML, orc.STD, True)[0]
     assert abs(b[0] - ref) <= 1e-10 * abs(ref), (b[0], ref)
     # MUCM's value is a difference of O(n) terms ((n - q) log sigma^2 against log|A|; 36 out
-    # of terms near 10^3 at n = 3000, d = 40): 1e-11 of it is ~1e-13 of the terms
+    # of terms near 10^3 at n = 3000, d = 40): 1e-11 of it is ~1e-13 of the terms.  Both
+    # GPU paths are also pinned to the oracle's MUCM value and sigma-hat^2, to 1e-10 of the
+    # largest cancelling term (so the looser cross-path bound cannot hide a drift of one)
     m = ctx.objective(orc.MUCM, orc.STD, hp[:-1], want_grad=False)
     mg = ctx.objective(orc.MUCM, orc.STD, hp[:-1], want_grad=True)
     assert abs(m[0] - mg[0]) <= 1e-11 * abs(mg[0]) and abs(m[2] - mg[2]) <= 1e-12 * mg[2]
+    mref, _, s2ref = orc.objective_fast(X, f, H, hp[:-1], orc.MUCM, orc.STD, True, want_grad=False)
+    A, _ = orc.kernel_var_ref(X, hp[:d], hp[d], orc.STD, True)
+    logdet_a = np.linalg.slogdet(A)[1]
+    q = H.shape[1]
+    terms = 0.5 * max(abs((n - q) * np.log(s2ref)), abs(logdet_a))
+    for got in (m, mg):
+        assert abs(got[0] - mref) <= 1e-10 * terms, (got[0], mref, terms)
+        assert abs(got[2] - s2ref) <= 1e-10 * s2ref, (got[2], s2ref)
 
 
 def test_value_only_not_pd(ctx):
