@@ -198,6 +198,12 @@ struct gpe_ctx {
   // the two-try bench 14.70 / 14.72 -> 14.78 / 14.81 evals/s and the Cholesky 28.4 -> 28.1 ms
   // against round 3's {4, 80}, {2, 40} (profiles/group_width_ab_r04.log)
   std::vector<std::pair<int, int>> potrf_groups = {{4, 48}, {2, 24}};
+  // super-blocks of the fused Cholesky (lazy far updates): up to potrf_sb consecutive column
+  // groups of one width >= 2 form a super-block; the columns beyond it receive its update
+  // as ONE trailing update of K = 128 x its width, spread over the next super-block's
+  // launches (1: every group updates the whole trailing matrix, K = 128 x its width;
+  // GPEMU_POTRF_SB)
+  int potrf_sb = 2;
   // the fused Cholesky on the context's high-priority stream (default 1; 0: on the
   // context stream, GPEMU_CHOL_PRIO=0)
   int chol_prio = 1;
@@ -685,33 +691,110 @@ int build_plan(gpe_ctx* c, Fact& F) {
     g += std::max(1, std::min(w, NB - g));
   }
   gs.push_back(NB);
+  // Super-blocks (lazy far updates).  Group 0 is a super-block of its own; after it, up to
+  // potrf_sb consecutive groups of one width >= 2 form one (width-1 groups stay single).
+  // For group gi with columns [gb, ge) in super-block [sb, se):
+  //   src0[gi]: start of the columns whose update its own columns still lack when it starts
+  //     -- the previous super-block when gi opens its super-block, else the previous group;
+  //   its launches carry (bulk segments, balanced over its W launches):
+  //     the update by [src0, gb) of its later columns [gb+1, ge) (the column factored next),
+  //     the update by [src0, gb) of the rest of its super-block [ge, se),
+  //     a share of the previous super-block's update of the columns beyond [se, NB)
+  //     (K = 128 x the previous super-block's width: the long-K far update, each far tile
+  //     read and written once per super-block instead of once per group).
+  // Every column j still receives every earlier column's update before it is factored: a
+  // far column gets super-block s's update during super-block s + 1, before s + 2 opens.
+  const int ng = (int)gs.size() - 1;
+  std::vector<int> sbs(ng), sbe(ng), src0(ng, 0);
+  {
+    int cur = 0, cnt = 0;
+    for (int gi = 0; gi < ng; ++gi) {
+      const int w = gs[gi + 1] - gs[gi];
+      const bool open = gi <= 1 || w < 2 || w != gs[gi] - gs[gi - 1] || cnt >= c->potrf_sb;
+      if (open) { cur = gs[gi]; cnt = 0; }
+      sbs[gi] = cur;
+      ++cnt;
+    }
+    for (int gi = ng - 1; gi >= 0; --gi) sbe[gi] = (gi + 1 < ng && sbs[gi + 1] == sbs[gi]) ? sbe[gi + 1] : gs[gi + 1];
+    for (int gi = 1; gi < ng; ++gi) src0[gi] = (sbs[gi] == gs[gi]) ? sbs[gi - 1] : gs[gi - 1];
+  }
+  // bulk segments of group gi: {a, b, g0, K}: columns [a, b) by columns [g0, g0 + K / 128)
+  struct Seg { int a, b, g0, K; };
+  std::vector<std::vector<Seg>> segs(ng);
+  {
+    auto cost = [&](int j, int K) { return (double)(NB - j) * K; };
+    for (int gi = 1; gi < ng; ++gi) {   // a super-block's rest: by src0, within the super-block
+      const int ge = gs[gi + 1], Kb = (gs[gi] - src0[gi]) * TILE;
+      if (ge < sbe[gi]) segs[gi].push_back({ge, sbe[gi], src0[gi], Kb});
+    }
+    // the far update of each super-block [s0, s1) (the previous one of its successor's
+    // groups), split over the successor's groups so their launches carry equal work
+    for (int gi = 1; gi < ng; ++gi) {
+      if (sbs[gi] != gs[gi]) continue;   // once per super-block, at its opening group
+      const int s0 = sbs[gi - 1], s1 = gs[gi], se = sbe[gi], Kf = (s1 - s0) * TILE;
+      std::vector<int> mem;
+      for (int gj = gi; gj < ng && sbs[gj] == sbs[gi]; ++gj) mem.push_back(gj);
+      std::vector<double> fixed(mem.size(), 0.0);
+      double F = 0.0, tot = 0.0;
+      for (int j = se; j < NB; ++j) F += cost(j, Kf);
+      for (size_t m = 0; m < mem.size(); ++m) {
+        const int gj = mem[m], Kb = (gs[gj] - src0[gj]) * TILE;
+        for (int j = gs[gj] + 1; j < gs[gj + 1]; ++j) fixed[m] += cost(j, Kb);
+        for (const Seg& sg : segs[gj])
+          for (int j = sg.a; j < sg.b; ++j) fixed[m] += cost(j, sg.K);
+        tot += fixed[m];
+      }
+      tot += F;
+      int j = se;
+      for (size_t m = 0; m < mem.size(); ++m) {
+        const double want = std::max(0.0, tot / mem.size() - fixed[m]);
+        const int a = j;
+        double got = 0.0;
+        while (j < NB && (m + 1 == mem.size() || got + 0.5 * cost(j, Kf) <= want)) got += cost(j++, Kf);
+        if (j > a) segs[mem[m]].push_back({a, j, s0, Kf});
+      }
+    }
+  }
   for (int va = 0; va < (pl.aug ? 2 : 1); ++va) {
   aug = va == 1;
   std::vector<int>& fidx = aug ? pl.fused_aug : pl.fused;
   for (int gi = 0; gi + 1 < (int)gs.size(); ++gi) {
     const int gb = gs[gi], ge = gs[gi + 1], W1 = ge - gb;
-    // previous group's bulk: columns [gb+1, NB) split into W1 parts
-    std::vector<std::pair<int, int>> rng(W1, {0, 0});   // share of [ge, NB) per part
+    // the group's bulk segments, column by column, split into W1 parts of equal work
+    // (part h also carries column gb + h + 1 by src0: the column factored next)
+    std::vector<std::vector<Seg>> part(W1);
     if (gi > 0) {
+      const int Kb = (gb - src0[gi]) * TILE;
       std::vector<double> load(W1, 0.0);
-      for (int h = 0; h + 1 < W1; ++h) load[h] = NB - (gb + h + 1);
+      for (int h = 0; h + 1 < W1; ++h) load[h] = (double)(NB - (gb + h + 1)) * Kb;
       double tot = 0.0;
       for (int h = 0; h < W1; ++h) tot += load[h];
-      for (int j = ge; j < NB; ++j) tot += NB - j;
-      int j = ge;
+      std::vector<std::pair<int, int>> cols;   // (column, segment)
+      for (int si = 0; si < (int)segs[gi].size(); ++si)
+        for (int j = segs[gi][si].a; j < segs[gi][si].b; ++j) {
+          cols.push_back({j, si});
+          tot += (double)(NB - j) * segs[gi][si].K;
+        }
+      size_t u = 0;
+      double cum = 0.0;
       for (int h = 0; h < W1; ++h) {
-        const int a = j;
+        cum += load[h];
         const double target = tot * (h + 1) / W1;
-        double cum = 0.0;
-        for (int u = 0; u <= h; ++u) cum += load[u];
-        for (int u = ge; u < a; ++u) cum += NB - u;
-        while (j < NB && (h == W1 - 1 || cum + 0.5 * (NB - j) <= target)) cum += NB - j++;
-        rng[h] = {a, j};
+        while (u < cols.size()) {
+          const Seg& sg = segs[gi][cols[u].second];
+          const double cj = (double)(NB - cols[u].first) * sg.K;
+          if (h < W1 - 1 && cum + 0.5 * cj > target) break;
+          cum += cj;
+          std::vector<Seg>& ps = part[h];
+          if (!ps.empty() && ps.back().b == cols[u].first && ps.back().g0 == sg.g0 && ps.back().K == sg.K) ++ps.back().b;
+          else ps.push_back({cols[u].first, cols[u].first + 1, sg.g0, sg.K});
+          ++u;
+        }
       }
     }
     for (int h = 0; h < W1; ++h) {
       const int t = gb + h;
-      const int p0 = (h == 0) ? (gi > 0 ? gs[gi - 1] : 0) : gb;
+      const int p0 = (h == 0) ? src0[gi] : gb;
       const int K = (t - p0) * TILE;
       const double al = K ? -1.0 : 1.0;
       const int m = NB - t - 1;
@@ -728,9 +811,9 @@ int build_plan(gpe_ctx* c, Fact& F) {
       if (aug) fp.push_back(augpanel(t, p0, K, al));
       for (size_t k = h0at, e = fp.size(); k < e; ++k) fp.push_back(half1(fp[k], pc_n));
       if (gi > 0) {
-        const int g0 = gs[gi - 1], Kb = (gb - g0) * TILE;
+        const int g0 = src0[gi], Kb = (gb - g0) * TILE;
         if (h + 1 < W1) bulk(fp, fl, t + 1, t + 2, g0, Kb);   // the column factored next
-        bulk(fp, fl, rng[h].first, rng[h].second, g0, Kb);
+        for (const Seg& sg : part[h]) bulk(fp, fl, sg.a, sg.b, sg.g0, sg.K);
       }
       fidx[t] = (int)pl.launches.size();
       add_launch(pl, 4, fp, fl);
@@ -756,7 +839,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
         gidx[gb] = fidx[gb];
         continue;
       }
-      const int g0 = gi > 0 ? gs[gi - 1] : 0, Kb = (gb - g0) * TILE;
+      const int g0 = src0[gi], Kb = (gb - g0) * TILE;
       std::vector<GemmProb> fp;
       double fl = 0.0;
       auto codes = [&](int pi, std::vector<unsigned>& out) {
@@ -828,9 +911,9 @@ int build_plan(gpe_ctx* c, Fact& F) {
         }
         npan[h] += 2 * pc_n;   // both halves of every panel tile post cnt_pan
       }
-      if (gi > 0 && ge < NB) {   // the columns after the group by the previous group
+      if (gi > 0 && !segs[gi].empty()) {   // the group's bulk segments (the rest of its super-block, a far share)
         const size_t b0 = fp.size();
-        bulk(fp, fl, ge, NB, g0, Kb);
+        for (const Seg& sg : segs[gi]) bulk(fp, fl, sg.a, sg.b, sg.g0, sg.K);
         std::vector<GemmProb> sub(fp.begin() + b0, fp.end());
         for (unsigned code : order_tiles(sub)) bulkc.push_back(code + ((unsigned)b0 << 24));
       }
@@ -1398,6 +1481,7 @@ gpe_ctx* gpe_create(int32_t device) {
     if (const char* eg = std::getenv("GPEMU_GROUP_P0")) c->grp_p0 = std::max(1, std::atoi(eg));
     if (const char* eg = std::getenv("GPEMU_GROUP_STRIDE")) c->grp_stride = std::max(0, std::atoi(eg));
     if (const char* ep = std::getenv("GPEMU_CHOL_PRIO")) c->chol_prio = std::atoi(ep) != 0;
+    if (const char* es = std::getenv("GPEMU_POTRF_SB")) c->potrf_sb = std::max(1, std::min(8, std::atoi(es)));
     if (const char* e3 = std::getenv("GPEMU_POTRF_W")) {
       c->potrf_groups.clear();
       std::string spec(e3);
@@ -2671,7 +2755,10 @@ int gpe_bench_gemm(gpe_ctx* c, int32_t trans_a, int32_t trans_b, int32_t mt, int
     fill(db, (size_t)K * N);
     fill(dc, (size_t)M * N);
     long long lda = trans_a ? K : M, ldb = trans_b ? K : N;
-    if (std::getenv("GPEMU_BENCH_HOT")) lda = ldb = 0;   // diagnostic: cache-resident operands
+    // diagnostics: GPEMU_BENCH_HOT=1 cache-resident operands (every k re-reads the same
+    // 128 values); =2 operands from a window of (tiles + K) x 128 doubles (ld = 128: L2-
+    // resident, every k still reads other values, so the MFMA inputs toggle as when cold)
+    if (const char* hot = std::getenv("GPEMU_BENCH_HOT")) lda = ldb = (std::atoi(hot) == 2) ? TILE : 0;
     GemmProb p = mkprob(da, lda, db, ldb, dc, M, mt, nt, K, lower ? G_CLOWER : 0, -1.0, beta);
     p.tile_begin = 0;
     p.ntiles = prob_tiles(p);

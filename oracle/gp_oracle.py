@@ -3,8 +3,9 @@
 This module is a NumPy/SciPy restatement of the reference algorithm
 (MathThyMod/GP_emu_UQSA, mounted read-only at /root/reference in the build
 container, never shipped).  It exists to CHECK the HIP path, never to run it:
-only ``tests/``, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of
-``bench.py`` may import it.  The product package ``gp_emu_uqsa_amd`` never
+only ``tests/``, ``__graft_entry__.smoke()``, the ``cpu_baseline`` leg of
+``bench.py`` and the dev timing tools that time the reference's CPU path beside the
+GPU (``tools/cpu_ref_c3.py``, ``tools/example_train_time.py``) may import it.  The product package ``gp_emu_uqsa_amd`` never
 imports this module and fails loudly when its HIP library is missing.
 
 Two restatements live here:

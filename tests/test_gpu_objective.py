@@ -203,6 +203,12 @@ _OTHER_ARITHMETIC = [
     {"GPEMU_POTRF_W": "8:40,3:20", "GPEMU_GROUP_STRIDE": "300"},
     {"GPEMU_POTRF_W": "8:40,3:20", "GPEMU_POTRF": "fused"},
     {"GPEMU_AUG": "0"},
+    # super-blocks: every group updating the whole trailing matrix (round 4), and super-
+    # blocks of three groups (far updates of K = 1536), both schedules
+    {"GPEMU_POTRF_SB": "1"},
+    {"GPEMU_POTRF_SB": "1", "GPEMU_POTRF": "fused"},
+    {"GPEMU_POTRF_SB": "3"},
+    {"GPEMU_POTRF_SB": "3", "GPEMU_POTRF": "fused", "GPEMU_POTRF_W": "4:8,2:4"},
 ]
 
 

@@ -48,15 +48,27 @@ for i, counters in enumerate(passes):
             for key, v in b.items():
                 if key not in ("ns", "kind"):
                     a[key] = v
-# 14 TRTRI + 1 LAUUM after the Cholesky's launches: 128 per step (GPEMU_POTRF=fused), or 72
-# per column group (the default for a lone evaluation: 12 groups of 4, 20 of 2, 40 of 1)
+# 14 TRTRI + 1 LAUUM after the Cholesky's launches: one per step (GPEMU_POTRF=fused), or
+# one per column group of width >= 2 and one per width-1 step (the default for a lone
+# evaluation); the widths as the library's (GPEMU_POTRF_W, default 4 while more than 48
+# tile columns remain, then 2 while more than 24).  Phases by each launch's first step.
+nb = -(-n // 128)
+widths = [(4, 48), (2, 24)]
+if os.environ.get("GPEMU_POTRF_W"):
+    widths = [tuple(int(v) for v in e.split(":")) for e in os.environ["GPEMU_POTRF_W"].split(",")]
+starts, g = [], 0
+while g < nb:
+    starts.append(g)
+    w = next((a for a, m in widths if nb - g > m), 1)
+    g += max(1, min(w, nb - g))
 nch = len(launches) - 15
-if nch == 128:
-    groups = {"chol 1-47": launches[1:48], "chol 48-87": launches[48:88], "chol 88-127": launches[88:128]}
-elif nch == 72:
-    groups = {"chol 0-47": launches[0:12], "chol 48-87": launches[12:32], "chol 88-127": launches[32:72]}
-else:
+first = list(range(nb)) if nch == nb else starts
+if len(first) != nch:
     groups = {"chol": launches[:nch]}
+else:
+    groups = {"chol 0-47": [], "chol 48-87": [], "chol 88-127": []}
+    for f, e in zip(first, launches[:nch]):
+        groups["chol 0-47" if f < 48 else ("chol 48-87" if f < 88 else "chol 88-127")].append(e)
 groups.update({"trtri": launches[nch:nch + 14], "lauum": launches[nch + 14:nch + 15]})
 out = {"n": n, "d": d, "schedule": os.environ.get("GPEMU_POTRF", "auto"), "phases": {}}
 for name, ls in groups.items():
