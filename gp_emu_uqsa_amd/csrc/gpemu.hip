@@ -201,9 +201,9 @@ struct gpe_ctx {
   // super-blocks of the fused Cholesky (lazy far updates): up to potrf_sb consecutive column
   // groups of one width >= 2 form a super-block; the columns beyond it receive its update
   // as ONE trailing update of K = 128 x its width, spread over the next super-block's
-  // launches (1: every group updates the whole trailing matrix, K = 128 x its width;
-  // GPEMU_POTRF_SB)
-  int potrf_sb = 2;
+  // launches (1: every group updates the whole trailing matrix, K = 128 x its width), while
+  // more than potrf_sb_min tile columns remain (GPEMU_POTRF_SB="groups:min_remaining")
+  int potrf_sb = 2, potrf_sb_min = 80;
   // the fused Cholesky on the context's high-priority stream (default 1; 0: on the
   // context stream, GPEMU_CHOL_PRIO=0)
   int chol_prio = 1;
@@ -692,7 +692,9 @@ int build_plan(gpe_ctx* c, Fact& F) {
   }
   gs.push_back(NB);
   // Super-blocks (lazy far updates).  Group 0 is a super-block of its own; after it, up to
-  // potrf_sb consecutive groups of one width >= 2 form one (width-1 groups stay single).
+  // potrf_sb consecutive groups of one width >= 2 form one while more than potrf_sb_min
+  // columns remain (later groups, and width-1 groups, stay single: there the longer pending
+  // update of a super-block's first column lengthens a chain the bulk no longer hides).
   // For group gi with columns [gb, ge) in super-block [sb, se):
   //   src0[gi]: start of the columns whose update its own columns still lack when it starts
   //     -- the previous super-block when gi opens its super-block, else the previous group;
@@ -710,7 +712,8 @@ int build_plan(gpe_ctx* c, Fact& F) {
     int cur = 0, cnt = 0;
     for (int gi = 0; gi < ng; ++gi) {
       const int w = gs[gi + 1] - gs[gi];
-      const bool open = gi <= 1 || w < 2 || w != gs[gi] - gs[gi - 1] || cnt >= c->potrf_sb;
+      const bool open = gi <= 1 || w < 2 || w != gs[gi] - gs[gi - 1] || cnt >= c->potrf_sb ||
+                        NB - gs[gi] <= c->potrf_sb_min;
       if (open) { cur = gs[gi]; cnt = 0; }
       sbs[gi] = cur;
       ++cnt;
@@ -1481,7 +1484,10 @@ gpe_ctx* gpe_create(int32_t device) {
     if (const char* eg = std::getenv("GPEMU_GROUP_P0")) c->grp_p0 = std::max(1, std::atoi(eg));
     if (const char* eg = std::getenv("GPEMU_GROUP_STRIDE")) c->grp_stride = std::max(0, std::atoi(eg));
     if (const char* ep = std::getenv("GPEMU_CHOL_PRIO")) c->chol_prio = std::atoi(ep) != 0;
-    if (const char* es = std::getenv("GPEMU_POTRF_SB")) c->potrf_sb = std::max(1, std::min(8, std::atoi(es)));
+    if (const char* es = std::getenv("GPEMU_POTRF_SB")) {
+      c->potrf_sb = std::max(1, std::min(8, std::atoi(es)));
+      if (const char* colon = std::strchr(es, ':')) c->potrf_sb_min = std::max(0, std::atoi(colon + 1));
+    }
     if (const char* e3 = std::getenv("GPEMU_POTRF_W")) {
       c->potrf_groups.clear();
       std::string spec(e3);

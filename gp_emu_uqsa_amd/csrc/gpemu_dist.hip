@@ -282,7 +282,9 @@ struct Rank {              // one rank's buffers (one per process over RCCL, P i
   // sweep
   double* A = nullptr;     // nloc*128 x (NB+1)*128, column-major
   double* logdet = nullptr;   // NB+1 (own steps; all-reduced)
-  double* dinv = nullptr;  // 128 x 128
+  // the step's broadcast block, 128 x (Kp + 128), ld 128: [-M | Dinv] with Dinv = L_kk^-1 and
+  // M = Dinv L(k, gb:k) (Kp = 128 (k - gb) pending columns of the group; P = 1: Dinv alone)
+  double* dinv = nullptr;
   double* panel = nullptr; // 2 x (NB+1)*128 x wmax*128: gathered panels of a group (by group parity)
   double* recv = nullptr;  // all-gather buffer, P segments of the largest panel
   double* gram = nullptr;  // Pc x Pc
@@ -351,6 +353,7 @@ struct gpe_dist {
   double* dr = nullptr;
   double* dinvdelta = nullptr;
   int* dinfo = nullptr;    // abort flag / failed pivot (all-reduced with max over RCCL)
+  int* dq = nullptr;       // NB counters: the diagonal tiles' pending-update blocks (G_DQUAD)
   double* cpart = nullptr; // contraction partials (scratch, stream-ordered)
   std::vector<Rank> ranks;   // local ranks (all P in loopback, one otherwise)
 
@@ -368,9 +371,9 @@ struct gpe_dist {
   int* dcnt = nullptr;       // [NB][P] panel tiles of rank r at step k
   GemmProb* dprobs = nullptr;
   unsigned* dtiles = nullptr;
-  std::vector<DLaunch> diag, panel_l, upd_next, upd_rest;   // per step (updates: group ends)
+  std::vector<DLaunch> diag, mrow, panel_l, upd_next, upd_rest;   // per step (updates: group ends)
   std::vector<int> maxT;                       // per step: max panel tiles over ranks
-  int T0 = 0;                                  // the most panel tiles any rank contributes
+  size_t recv_tiles = 0;                       // P > 1: tiles per rank segment of the group all-gather
   double* hpin = nullptr;
   size_t hpin_cap = 0;
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -443,6 +446,7 @@ int dalloc(gpe_dist* h, T** p, size_t count, size_t* acct = nullptr) {
 }
 
 void free_rank(Rank& R) {
+  if (R.trecv == R.recv) R.trecv = nullptr;   // aliased (ensure_grad)
   double** bufs[] = {&R.A, &R.logdet, &R.dinv, &R.panel, &R.recv, &R.gram, &R.X, &R.g1, &R.trecv,
                      &R.dZ, &R.dR2, &R.r2loc, &R.wpart, &R.slab, &R.csum};
   for (double** b : bufs) dfree(b);
@@ -674,6 +678,7 @@ int build_schedule(gpe_dist* h) {
   std::vector<GemmProb> probs;
   std::vector<unsigned> tiles;
   h->diag.assign(NB, DLaunch());
+  h->mrow.assign(NB, DLaunch());
   h->panel_l.assign(NB, DLaunch());
   h->upd_next.assign(NB, DLaunch());
   h->upd_rest.assign(NB, DLaunch());
@@ -689,14 +694,31 @@ int build_schedule(gpe_dist* h) {
     }
     // diagonal tile: owner's local row k / P, column k, less the pending update
     // L(k, gb:k) L(k, gb:k)^T from its own row; then factored and inverted into its Dinv
+    // (the Dinv block of the step's broadcast block)
+    const bool gath = gather_panels(h);
     DLaunch dl;
     dl.first = (int)probs.size();
     if (Rank* R = rank_slot(h, k % P)) {
       double* Ckk = R->A + (long long)(k / P) * TILE + (long long)k * TILE * R->ld;
       const double* Lk = R->A + (long long)(k / P) * TILE + (long long)gb * TILE * R->ld;
-      GemmProb p = dprob(Kp ? Lk : nullptr, R->ld, Kp ? Lk : nullptr, R->ld, Ckk, R->ld, 1, 1, Kp, G_DIAG,
-                         Kp ? -1.0 : 1.0, 1.0);
-      p.X = R->dinv;
+      // the pending update as DQ_N 32 x 32-block workgroups (as the single-GPU sweep), which
+      // the G_DIAG workgroup waits for (they precede it in the launch)
+      if (Kp > 0) {
+        GemmProb q = dprob(Lk, R->ld, nullptr, 0, Ckk, R->ld, DQ_N, 1, Kp, G_DQUAD, -1.0, 1.0);
+        q.post = h->dq + k;
+        q.diag_col0 = k * TILE;
+        q.tile_begin = dl.tiles;
+        q.ntiles = DQ_N;
+        dl.tiles += DQ_N;
+        probs.push_back(q);
+        ++dl.count;
+      }
+      GemmProb p = dprob(nullptr, R->ld, nullptr, R->ld, Ckk, R->ld, 1, 1, 0, G_DIAG, 1.0, 1.0);
+      if (Kp > 0) {
+        p.pre0 = h->dq + k;
+        p.pre0_n = DQ_N;
+      }
+      p.X = R->dinv + (long long)Kp * TILE;
       p.ldx = TILE;
       p.logdet = R->logdet + k;
       p.diag_col0 = k * TILE;
@@ -707,9 +729,10 @@ int build_schedule(gpe_dist* h) {
       probs.push_back(p);
       ++dl.count;
     }
-    // pending update of the panel tiles: A(i,k) -= L(i, gb:k) L(k, gb:k)^T over each
-    // local rank's rows i > k; L(k, gb:k) is row k of the rank's gathered panels
-    if (Kp > 0) {
+    // P = 1: pending update of the panel tiles, A(i,k) -= L(i, gb:k) L(k, gb:k)^T over the
+    // rows i > k, beside the factorisation (row k is the rank's own).  P > 1: the panel
+    // launch applies it (ranks other than the owner receive row k's part in the broadcast)
+    if (Kp > 0 && !gath) {
       for (Rank& R : h->ranks) {
         const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
         if (c == 0) continue;
@@ -725,14 +748,35 @@ int build_schedule(gpe_dist* h) {
       }
     }
     h->diag[k] = dl;
-    // panel: L(i,k) = A(i,k) Dinv^T over each local rank's rows i > k
+    // P > 1, Kp > 0: the owner's M block of the broadcast, -Dinv L(k, gb:k) (its own row)
+    if (gath && Kp > 0)
+      if (Rank* R = rank_slot(h, k % P)) {
+        DLaunch ml;
+        ml.first = (int)probs.size();
+        GemmProb p = dprob(R->dinv + (long long)Kp * TILE, TILE,
+                           R->A + (long long)(k / P) * TILE + (long long)gb * TILE * R->ld, R->ld, R->dinv, TILE,
+                           1, Kp / TILE, TILE, 0, -1.0, 0.0);
+        p.tile_begin = 0;
+        p.ntiles = Kp / TILE;
+        ml.tiles = p.ntiles;
+        ml.count = 1;
+        ml.kind = 1;
+        probs.push_back(p);
+        h->mrow[k] = ml;
+      }
+    // panel over each local rank's rows i > k: P = 1, L(i,k) = A(i,k) Dinv^T (pending update
+    // applied in the diagonal launch); P > 1, L(i,k) = [L(i, gb:k) A(i,k)] [-M Dinv]^T =
+    // (A(i,k) - L(i, gb:k) L(k, gb:k)^T) Dinv^T, one product with K = Kp + 128 over the
+    // row's columns gb..k (in place: each tile reads only its own rows before storing)
     DLaunch pl;
     pl.first = (int)probs.size();
     for (Rank& R : h->ranks) {
       const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
       if (c == 0) continue;
       double* Aik = R.A + (long long)a * TILE + (long long)k * TILE * R.ld;
-      GemmProb p = dprob(Aik, R.ld, R.dinv, TILE, Aik, R.ld, c, 1, TILE, 0, 1.0, 0.0);
+      GemmProb p = gath ? dprob(R.A + (long long)a * TILE + (long long)gb * TILE * R.ld, R.ld, R.dinv, TILE, Aik,
+                                R.ld, c, 1, Kp + TILE, 0, 1.0, 0.0)
+                        : dprob(Aik, R.ld, R.dinv + (long long)Kp * TILE, TILE, Aik, R.ld, c, 1, TILE, 0, 1.0, 0.0);
       p.tile_begin = pl.tiles;
       p.ntiles = c;
       pl.tiles += c;
@@ -896,7 +940,15 @@ int ensure_grad(gpe_dist* h) {
   }
   for (Rank& R : h->ranks) {
     DCHK(dalloc(h, &R.g1, (size_t)g1_need, &R.bytes));
-    DCHK(dalloc(h, &R.trecv, (size_t)rv_need, &R.bytes));
+    // the TRTRI's all-gather buffer runs after the sweep: it shares the sweep's group
+    // all-gather buffer when that is large enough (stream order separates their uses)
+    if (R.trecv == R.recv) R.trecv = nullptr;
+    if (R.recv && (size_t)rv_need <= (size_t)P * h->recv_tiles * TILE * TILE) {
+      dfree(&R.trecv);
+      R.trecv = R.recv;
+    } else {
+      DCHK(dalloc(h, &R.trecv, (size_t)rv_need, &R.bytes));
+    }
   }
   for (const auto& lv : lev) {
     const int s = lv.first, a = s / 2, cc = lv.second;
@@ -1131,37 +1183,51 @@ int kbuild(gpe_dist* h, int kernel, double nu, double s2, double rscale) {
   return GPE_OK;
 }
 
-// one column step of a group's chain: diag, Dinv broadcast, panel, pack + all-gather + unpermute
+// one column step of a group's chain: diag (the owner's factor), [the owner's M block],
+// ONE broadcast of [-M | Dinv] (128 KB x (1 + pending columns)), panel
 int step(gpe_dist* h, int k) {
   const int P = h->P, owner = k % P;
+  const long long Kp = (long long)(k - h->gstart[k]) * TILE;
   DCHK(launch(h, h->diag[k]));
-  DCHK(coll_bcast(h, &Rank::dinv, 0, (size_t)TILE * TILE, owner));
+  DCHK(launch(h, h->mrow[k]));
+  DCHK(coll_bcast(h, &Rank::dinv, 0, (size_t)TILE * (gather_panels(h) ? Kp + TILE : TILE),
+                  owner) );
   if (h->grad_now) {
     if (Rank* O = rank_slot(h, owner))
       DCHK_HIP(h, hipMemcpy2DAsync(O->X + (long long)(k / P) * TILE + (long long)k * TILE * O->ld,
-                                   O->ld * sizeof(double), O->dinv, TILE * sizeof(double), TILE * sizeof(double),
-                                   TILE, hipMemcpyDeviceToDevice, h->cs));
+                                   O->ld * sizeof(double), O->dinv + Kp * TILE, TILE * sizeof(double),
+                                   TILE * sizeof(double), TILE, hipMemcpyDeviceToDevice, h->cs));
   }
-  DCHK(launch(h, h->panel_l[k]));
+  return launch(h, h->panel_l[k]);
+}
+
+// P > 1, at the end of the group [gb, ge): every rank packs its tile rows below the group
+// (global rows >= ge) of the group's W columns, tile row by tile row; ONE all-gather; the
+// segments are unpermuted into the group's panel buffer in global row order, which the
+// trailing update reads (rows >= ge only: the chain needed no gathered rows)
+int gather_group(gpe_dist* h, int gb, int ge) {
+  if (!gather_panels(h)) return GPE_OK;
+  const int P = h->P, k = ge - 1, W = ge - gb, T = h->maxT[k];
+  if (T <= 0) return GPE_OK;
   const long long ldp = (long long)(h->NB + h->NA) * TILE;
-  const long long pcol = (long long)(k - h->gstart[k]) * TILE * ldp;   // block of k in its group's panels
-  const int T = h->maxT[k];
-  if (T > 0 && gather_panels(h)) {
-    const size_t seg = (size_t)T * TILE * TILE;
-    for (Rank& R : h->ranks) {
-      const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
-      if (c == 0) continue;
-      hipLaunchKernelGGL(k_dist_pack, dim3(c), dim3(256), 0, h->cs, R.A, R.ld, a, k,
-                         R.recv + (size_t)R.rank * seg);
-      DCHK_HIP(h, hipGetLastError());
-    }
-    DCHK(coll_allgather(h, &Rank::recv, seg));
-    for (Rank& R : h->ranks) {
-      hipLaunchKernelGGL(k_dist_unpermute, dim3(T, P), dim3(256), 0, h->cs, R.recv, (long long)seg,
-                         h->dli0 + (size_t)k * P, h->dcnt + (size_t)k * P, P, panel_of(h, R, k) + pcol, ldp);
+  const size_t blk = (size_t)T * TILE * TILE, seg = (size_t)W * blk;
+  for (Rank& R : h->ranks) {
+    const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
+    if (c == 0) continue;
+    for (int w = 0; w < W; ++w) {
+      hipLaunchKernelGGL(k_dist_pack, dim3(c), dim3(256), 0, h->cs, R.A, R.ld, a, gb + w,
+                         R.recv + (size_t)R.rank * seg + (size_t)w * blk);
       DCHK_HIP(h, hipGetLastError());
     }
   }
+  DCHK(coll_allgather(h, &Rank::recv, seg));
+  for (Rank& R : h->ranks)
+    for (int w = 0; w < W; ++w) {
+      hipLaunchKernelGGL(k_dist_unpermute, dim3(T, P), dim3(256), 0, h->cs, R.recv + (size_t)w * blk, (long long)seg,
+                         h->dli0 + (size_t)k * P, h->dcnt + (size_t)k * P, P,
+                         panel_of(h, R, k) + (long long)w * TILE * ldp, ldp);
+      DCHK_HIP(h, hipGetLastError());
+    }
   return GPE_OK;
 }
 
@@ -1192,6 +1258,7 @@ int group_sweep(gpe_dist* h) {
     h->cs = h->crit;
     if (g > 0) DCHK_HIP(h, hipStreamWaitEvent(h->crit, h->ev_next[g - 1], 0));
     for (int k = gb; k < ge; ++k) DCHK(step(h, k));
+    DCHK(gather_group(h, gb, ge));
     DCHK_HIP(h, hipEventRecord(h->ev_chain[g], h->crit));
     h->cs = h->stream;
     DCHK_HIP(h, hipStreamWaitEvent(h->stream, h->ev_chain[g], 0));
@@ -1299,6 +1366,7 @@ void gpe_dist_destroy(gpe_dist* h) {
   double** bufs[] = {&h->dX, &h->dXw, &h->dF, &h->dr, &h->dinvdelta, &h->cpart, &h->dT2};
   for (double** b : bufs) dfree(b);
   dfree(&h->dinfo);
+  dfree(&h->dq);
   dfree(&h->dli0);
   dfree(&h->dcnt);
   dfree(&h->dprobs);
@@ -1377,9 +1445,18 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
   DCHK(dalloc(h, &h->dinvdelta, (size_t)d, &h->shared_bytes));
   // local ranks and their sweep buffers
   build_groups(h);
+  DCHK(dalloc(h, &h->dq, (size_t)h->NB, &h->shared_bytes));
   const int NT = h->NB + h->NA;
   h->panel_sz = (size_t)NT * TILE * TILE * h->wmax;
-  h->T0 = nloc_of(NT - 1, h->P, 0);
+  // the group all-gather's segment: W column blocks of the most tile rows below the group
+  // any rank holds (rows >= ge)
+  h->recv_tiles = 0;
+  for (size_t g = 0; g + 1 < h->gs.size(); ++g) {
+    const int ge = h->gs[g + 1], W = ge - h->gs[g];
+    int T = 0;
+    for (int rr = 0; rr < h->P; ++rr) T = std::max(T, std::max(0, nloc_of(NT - 1, h->P, rr) - li0_of(ge - 1, h->P, rr)));
+    h->recv_tiles = std::max(h->recv_tiles, (size_t)T * W);
+  }
   for (int rr = 0; rr < h->P; ++rr) {
     if (!h->loop && rr != h->rank) continue;
     Rank R;
@@ -1390,10 +1467,10 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
     Rank& B = h->ranks.back();
     DCHK(dalloc(h, &B.A, (size_t)B.ld * (size_t)NT * TILE, &B.bytes));
     DCHK(dalloc(h, &B.logdet, (size_t)h->NB + 1, &B.bytes));
-    DCHK(dalloc(h, &B.dinv, (size_t)TILE * TILE, &B.bytes));
+    DCHK(dalloc(h, &B.dinv, (size_t)TILE * TILE * h->wmax, &B.bytes));
     if (gather_panels(h)) {
       DCHK(dalloc(h, &B.panel, 2 * h->panel_sz, &B.bytes));
-      DCHK(dalloc(h, &B.recv, (size_t)h->P * h->T0 * TILE * TILE, &B.bytes));
+      DCHK(dalloc(h, &B.recv, (size_t)h->P * h->recv_tiles * TILE * TILE, &B.bytes));
     }
     DCHK(dalloc(h, &B.gram, (size_t)Pc * Pc, &B.bytes));
   }
@@ -1451,6 +1528,7 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
       DCHK_HIP(h, hipMemsetAsync(R.X, 0, (size_t)R.ld * NB * TILE * sizeof(double), h->stream));
   }
   DCHK(kbuild(h, kernel, nu, s2, rscale));
+  DCHK_HIP(h, hipMemsetAsync(h->dq, 0, (size_t)NB * sizeof(int), h->stream));
   DCHK(group_sweep(h));
 
   // Gram of L^-1 [f H] = -(the augmented rows' diagonal block; its lower tiles), and

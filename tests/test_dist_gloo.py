@@ -95,42 +95,43 @@ def _sched_worker(rank, world, port, n, q, W, CW, out):
         mine = [t for t in range(nb + NA) if t % world == rank]
         loc = {t: full[t * B:(t + 1) * B, :].copy() for t in mine}     # own tile rows
         logdet = np.zeros(nb + 1)
-        gpanel = {}   # the group's gathered panel columns: gpanel[c][t] = L(t, c)
+        gpanel = {}   # the group's gathered panel columns below it: gpanel[c][t] = L(t, c), t >= ge
         for k in range(nb):
             owner = k % world
             gb, ge = gstart[k], gend[k]
-            if k == gb:
-                gpanel = {}
-            # pending update by the group's earlier columns: own diagonal and panel tiles
+            kp = (k - gb) * B                                         # pending columns [gb, k)
             rows = [t for t in mine if t > k]
-            for c in range(gb, k):
-                if owner == rank:
-                    loc[k][:, k * B:(k + 1) * B] -= loc[k][:, c * B:(c + 1) * B] @ loc[k][:, c * B:(c + 1) * B].T
-                for t in rows:
-                    loc[t][:, k * B:(k + 1) * B] -= loc[t][:, c * B:(c + 1) * B] @ gpanel[c][k].T
-            dinv = torch.zeros(B, B, dtype=torch.float64)
+            # the owner: its diagonal tile less the pending update from its own row, factored;
+            # broadcast block [-M | Dinv], M = Dinv L(k, gb:k) (one broadcast per step)
+            bc = torch.zeros(B, kp + B, dtype=torch.float64)
             if owner == rank:
+                for c in range(gb, k):
+                    loc[k][:, k * B:(k + 1) * B] -= loc[k][:, c * B:(c + 1) * B] @ loc[k][:, c * B:(c + 1) * B].T
                 L = np.linalg.cholesky(loc[k][:, k * B:(k + 1) * B])
                 loc[k][:, k * B:(k + 1) * B] = L
                 logdet[k] = np.log(np.diag(L)).sum()
-                dinv = torch.from_numpy(np.linalg.inv(L))
-            dist.broadcast(dinv, src=owner)
-            Dinv = dinv.numpy()
-            for t in rows:                                            # panel
-                loc[t][:, k * B:(k + 1) * B] = loc[t][:, k * B:(k + 1) * B] @ Dinv.T
-            maxT = max(len([t for t in range(nb + NA) if t % world == r and t > k]) for r in range(world))
-            send = torch.zeros(maxT, B, B, dtype=torch.float64)
-            for i, t in enumerate(rows):
-                send[i] = torch.from_numpy(loc[t][:, k * B:(k + 1) * B])
-            recv = [torch.zeros_like(send) for _ in range(world)]
-            dist.all_gather(recv, send)
-            panel = {}
-            for r in range(world):                                   # unpermute
-                rt = [t for t in range(nb + NA) if t % world == r and t > k]
-                for i, t in enumerate(rt):
-                    panel[t] = recv[r][i].numpy()
-            gpanel[k] = panel
-            if k + 1 == ge:                                           # group closes: own-row update
+                Dinv = np.linalg.inv(L)
+                bc = torch.from_numpy(np.hstack([-(Dinv @ loc[k][:, gb * B:k * B]), Dinv]))
+            dist.broadcast(bc, src=owner)
+            BC = bc.numpy()
+            for t in rows:                                            # panel: [L(t, gb:k) A(t,k)] [-M Dinv]^T
+                loc[t][:, k * B:(k + 1) * B] = loc[t][:, gb * B:(k + 1) * B] @ BC.T
+            if k + 1 == ge:                                           # group closes
+                # ONE all-gather of the group's columns on the rows below it, then the
+                # trailing update of the own rows
+                below = [[t for t in range(nb + NA) if t % world == r and t >= ge] for r in range(world)]
+                maxT = max(len(b) for b in below)
+                send = torch.zeros(max(maxT, 1), ge - gb, B, B, dtype=torch.float64)
+                for i, t in enumerate(below[rank]):
+                    for w in range(ge - gb):
+                        send[i, w] = torch.from_numpy(loc[t][:, (gb + w) * B:(gb + w + 1) * B])
+                recv = [torch.zeros_like(send) for _ in range(world)]
+                dist.all_gather(recv, send)
+                gpanel = {c: {} for c in range(gb, ge)}
+                for r in range(world):                               # unpermute
+                    for i, t in enumerate(below[r]):
+                        for w in range(ge - gb):
+                            gpanel[gb + w][t] = recv[r][i, w].numpy()
                 for t in [t for t in mine if t >= ge]:
                     for j in range(ge, t + 1):
                         for c in range(gb, ge):
@@ -206,9 +207,14 @@ def _sched_worker(rank, world, port, n, q, W, CW, out):
 
 @pytest.mark.parametrize("world,W,q,CW", [(2, 1, 3, 8), (3, 1, 11, 2), (2, 3, 19, 1), (3, 4, 3, 3)])
 def test_schedule_model_matches_dense(world, W, q, CW):
-    """W: column-group width (1 = a trailing update per column; 3 and 4 leave a ragged
-    last group of the 7 tile columns); q + 1 > 8 spreads [f H]^T over 2-3 augmented tile
-    rows; CW: the TRTRI's column-chunk width (1 and 2 split its upper levels)."""
+    """The row-block schedule of gpemu_dist.hip in NumPy over gloo ranks: per column step
+    ONE broadcast from the diagonal owner of [-M | Dinv] (M = Dinv L(k, gb:k): the group's
+    pending columns of row k ride with the inverse, so no rank needs a gathered panel row
+    inside the group), and ONE all-gather per column group of its columns on the rows below
+    it, before the group's trailing update.  W: column-group width (1 = a trailing update per
+    column; 3 and 4 leave a ragged last group of the 7 tile columns); q + 1 > 8 spreads
+    [f H]^T over 2-3 augmented tile rows; CW: the TRTRI's column-chunk width (1 and 2 split
+    its upper levels)."""
     n = 7 * B
     port = _free_port()
     with mp.Manager() as m:

@@ -94,8 +94,8 @@ for K in Ks:
         clk = per["GRBM_GUI_ACTIVE"][0] / 8 / (per["ns"][0] * 1e-9)
         row.update({"prof_ms": ns / 1e6, "clock_ghz": clk / 1e9,
                     "mfma_busy": per["SQ_VALU_MFMA_BUSY_CYCLES"][0] / (clk * per["ns"][0] * 1e-9 * 1024),
-                    "hbm_read_gb": 2.0 * 1024.0 * per["FETCH_SIZE"][1] / 1e9,
-                    "hbm_write_gb": 1024.0 * per["WRITE_SIZE"][2] / 1e9,
+                    "hbm_read_gb": 2.0 * 1024.0 * per["FETCH_SIZE"][0] / 1e9,
+                    "hbm_write_gb": 1024.0 * per["WRITE_SIZE"][0] / 1e9,
                     "algorithmic_gb": (2 * mt * 128 * K + 2 * (mt * 128) ** 2) * 8 / 1e9,
                     "prof_tflops": flops / (ns * 1e-9) / 1e12})
         row["hbm_tb_s"] = (row["hbm_read_gb"] + row["hbm_write_gb"]) / (row["prof_ms"] * 1e-3) / 1e3

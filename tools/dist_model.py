@@ -1,6 +1,7 @@
 """Predicted strong-scaling curve of the row-block objective (dev tool).
 
   python tools/dist_model.py --p1-ms MS --p1-value-ms MS [--points 16384] [--basis 11]
+                             [--dims 10] [--widths 8:160,4:80,2:40] [--chain-us 90]
 
 Counts, from the schedule of gpemu_dist.hip (column groups, recursive TRTRI chunks), the
 collectives one LLH + gradient issues and the bytes each rank receives in them, then
@@ -12,32 +13,57 @@ predicts the evaluation time at P ranks over xGMI as
 with the compute terms from the P = 1 loopback run (one GPU, no real collectives) and
 alpha / beta the per-collective latency and per-rank receive bandwidth of RCCL over the
 MI355X's xGMI (defaults: 25 us, 64 GB/s at P = 2 over one link, 300 GB/s at P >= 4).
-The sweep's collectives sit on the chain (the look-ahead overlaps the bulk, not them)."""
+The sweep's collectives sit on the chain (the look-ahead overlaps the bulk, not them).
+Round 5 schedule: per column step ONE broadcast of [-M | Dinv] from the diagonal owner
+(128 x 128 (1 + h) doubles at position h of its group), per column GROUP one all-gather of
+the group's columns on the rows below it.  Also the per-rank device memory (the
+allocations of gpe_dist_set_data / ensure_grad, descriptors left out)."""
 import argparse
 import json
 
 TILE = 128
 T2B = TILE * TILE * 8      # bytes per tile
+SLAB_DOUBLES = 1 << 26
 
 
-def sweep_collectives(nb, na, P):
-    """(count, bytes received per rank): Dinv broadcast + panel all-gather per step."""
+def nloc_of(nb, P, r):
+    return (nb - r) // P + 1 if r <= nb else 0
+
+
+def li0_of(k, P, r):
+    return 0 if k < r else (k - r) // P + 1
+
+
+def groups(nb, widths):
+    gs, g = [], 0
+    while g < nb:
+        gs.append(g)
+        w = next((a for a, m in widths if nb - g > m), 1)
+        g += max(1, min(w, nb - g))
+    gs.append(nb)
+    return gs
+
+
+def sweep_collectives(nb, na, P, widths):
+    """(count, bytes received per rank): a broadcast per step, an all-gather per group."""
+    nt = nb + na
     cnt, rb = 0, 0
-    for k in range(nb):
-        cnt += 1
-        rb += T2B if P > 1 else 0                                  # Dinv from its owner
-        tiles = nb + na - 1 - k                                     # panel tiles below k
-        seg = -(-tiles // P)                                        # max per rank
-        cnt += 1
-        rb += (P - 1) * seg * T2B                                   # all-gather (padded segments)
+    gs = groups(nb, widths)
+    for g in range(len(gs) - 1):
+        gb, ge = gs[g], gs[g + 1]
+        for k in range(gb, ge):
+            cnt += 1
+            rb += T2B * (1 + k - gb) if P > 1 else 0                 # [-M | Dinv] from its owner
+        T = max(max(0, nloc_of(nt - 1, P, r) - li0_of(ge - 1, P, r)) for r in range(P))
+        if T > 0:
+            cnt += 1
+            rb += (P - 1) * T * (ge - gb) * T2B                     # all-gather (padded segments)
     return cnt, rb
 
 
-def trtri_collectives(nb, P, slab_rows):
-    """(count, bytes received per rank) of the recursive TRTRI's chunked all-gathers."""
-    n_pad = nb * TILE
-    cap = slab_rows * TILE * n_pad * 8
-    cnt, rb = 0, 0
+def trtri_levels(nb, P, cap):
+    """Per level (s, chunk width, g1, s1, g2, s2) of the recursive TRTRI, as ensure_grad."""
+    out = []
     s = 2
     while s // 2 < nb:
         a = s // 2
@@ -53,6 +79,24 @@ def trtri_collectives(nb, P, slab_rows):
         cc = a
         while cc > 1 and not fits(cc):
             cc = (cc + 1) // 2
+        out.append((s, cc, g1, s1, g2, s2, pairs))
+        s *= 2
+    return out
+
+
+def slab_doubles(nb, n_pad, P):
+    whole = nb * TILE * n_pad
+    sd = SLAB_DOUBLES
+    if whole <= 4 * SLAB_DOUBLES:
+        sd = max(sd, whole // P)
+    return max(1, min(nb, sd // (TILE * n_pad))) * TILE * n_pad
+
+
+def trtri_collectives(nb, P, cap):
+    """(count, bytes received per rank) of the recursive TRTRI's chunked all-gathers."""
+    cnt, rb = 0, 0
+    for (s, cc, g1, s1, g2, s2, pairs) in trtri_levels(nb, P, cap * 8):
+        a = s // 2
         for j0 in range(0, a, cc):
             cw, rows1 = min(cc, a - j0), a - j0
             seg1 = sum(-(-rows1 // P) * cw for _ in pairs)
@@ -60,14 +104,42 @@ def trtri_collectives(nb, P, slab_rows):
             if P > 1:
                 cnt += 2
                 rb += (P - 1) * (seg1 + seg2) * T2B
-        s *= 2
     return cnt, rb
+
+
+def rank_memory_gb(nb, na, P, d, pc, widths, grad=True):
+    """Device bytes of rank 0 (the largest share), in GB."""
+    nt, n_pad = nb + na, nb * TILE
+    gs = groups(nb, widths)
+    wmax = max(gs[i + 1] - gs[i] for i in range(len(gs) - 1))
+    nloc = nloc_of(nt - 1, P, 0)
+    ld = max(nloc, 1) * TILE
+    b = ld * nt * TILE + (nb + 1) + TILE * TILE * wmax + pc * pc       # A rows, logdet, [-M|Dinv], Gram
+    recv = 0
+    if P > 1:
+        rt = max(max(max(0, nloc_of(nt - 1, P, r) - li0_of(gs[g + 1] - 1, P, r)) for r in range(P))
+                 * (gs[g + 1] - gs[g]) for g in range(len(gs) - 1))
+        recv = P * rt * TILE * TILE
+        b += 2 * nt * TILE * TILE * wmax + recv                          # panels, all-gather buffer
+    shared = n_pad * (2 * d + pc + 2) + nb * (nb + 1) // 2 * (d + 3)    # inputs, contraction partials
+    if grad:
+        sd = slab_doubles(nb, n_pad, P)
+        b += ld * nb * TILE + 2 * n_pad * pc + ld * na * TILE + n_pad * na * TILE + sd + d + 3
+        if P > 1:
+            g1n = rvn = 0
+            for (s, cc, g1, s1, g2, s2, pairs) in trtri_levels(nb, P, sd * 8):
+                g1n = max(g1n, g1 * cc * TILE * TILE)
+                rvn = max(rvn, P * s1 * cc * TILE * TILE, P * s2 * cc * TILE * TILE)
+            b += g1n + (0 if rvn <= recv else rvn)
+    return (b + shared) * 8 / 1e9
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--points", type=int, default=16384)
     ap.add_argument("--basis", type=int, default=11, help="q + 1")
+    ap.add_argument("--dims", type=int, default=10)
+    ap.add_argument("--widths", default="8:160,4:80,2:40", help="the row-block path's column-group widths")
     ap.add_argument("--p1-ms", type=float, default=None, help="loopback P=1 LLH+gradient ms")
     ap.add_argument("--p1-value-ms", type=float, default=None, help="loopback P=1 value-only ms")
     ap.add_argument("--chain-us", type=float, default=75.0, help="diagonal factor + panel per step, us")
@@ -75,14 +147,15 @@ def main():
     ap.add_argument("--beta2", type=float, default=64.0, help="GB/s per rank at P=2")
     ap.add_argument("--beta", type=float, default=300.0, help="GB/s per rank at P>=4")
     args = ap.parse_args()
+    widths = [tuple(int(v) for v in e.split(":")) for e in args.widths.split(",")]
     nb = -(-args.points // TILE)
     na = -(-args.basis // TILE)
     n_pad = nb * TILE
-    slab_rows = max(1, min(nb, (1 << 26) // (TILE * n_pad)))
     rows = []
     for P in (1, 2, 4, 8):
-        c_sw, b_sw = sweep_collectives(nb, na, P)
-        c_tr, b_tr = trtri_collectives(nb, P, slab_rows)
+        cap = slab_doubles(nb, n_pad, P)
+        c_sw, b_sw = sweep_collectives(nb, na, P, widths)
+        c_tr, b_tr = trtri_collectives(nb, P, cap)
         c_rest = 6                                                  # Gram, logdet, info, Z, W, sums
         b_rest = (P - 1) / P * (n_pad * args.basis * 8 * 2) if P > 1 else 0
         beta = (args.beta2 if P == 2 else args.beta) * 1e9
@@ -92,14 +165,16 @@ def main():
         row = {"P": P, "sweep_collectives": c_sw if P > 1 else 0, "sweep_recv_GB": b_sw / 1e9,
                "trtri_collectives": c_tr, "trtri_recv_GB": b_tr / 1e9,
                "comm_ms": comm_sweep + comm_tr + comm_rest,
-               "comm_sweep_ms": comm_sweep, "comm_trtri_ms": comm_tr}
+               "comm_sweep_ms": comm_sweep, "comm_trtri_ms": comm_tr,
+               "rank_memory_GB": rank_memory_gb(nb, na, P, args.dims, args.basis, widths)}
         if args.p1_ms and args.p1_value_ms:
             chain = nb * args.chain_us * 1e-3
             sweep = args.p1_value_ms
             grad = args.p1_ms - args.p1_value_ms
             bulk = max(0.0, sweep - chain)
-            # the chain (factor, broadcast, panel, all-gather per step) does not divide; the
-            # bulk does (taken as not overlapping the chain: at P = 1 this is the measurement)
+            # the chain (factor, broadcast, panel per step; the group all-gathers) does not
+            # divide; the bulk does (taken as not overlapping the chain: at P = 1 this is the
+            # measurement)
             t_sweep = chain + comm_sweep + bulk / P
             row["predicted_ms"] = t_sweep + grad / P + comm_tr + comm_rest
             row["speedup_vs_p1"] = args.p1_ms / row["predicted_ms"]

@@ -29,7 +29,7 @@ for i, counters in enumerate(passes):
     cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", *counters, "-d", odir, "-o", "run",
            "--output-format", "csv", "--", sys.executable, os.path.join(root, "tools", "prof_objective.py"),
            str(n), str(d), "1"]
-    subprocess.run(cmd, check=True, cwd=root, env=dict(os.environ, TMPDIR="/tmp"))
+    subprocess.run(cmd, check=True, cwd=root, env=dict(os.environ, TMPDIR="/tmp"), stdout=subprocess.DEVNULL)
     rows = {}
     for f in glob.glob(os.path.join(odir, "**", "*counter_collection*.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
