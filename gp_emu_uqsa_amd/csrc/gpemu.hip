@@ -23,6 +23,7 @@
 #include "../../include/gpemu.h"
 #include "gpemu_kernels.hpp"
 #include "gpemu_small.hpp"
+#include "gpemu_tiny.hpp"
 
 using namespace gpe;
 
@@ -207,6 +208,8 @@ struct gpe_ctx {
   // the fused Cholesky on the context's high-priority stream (default 1; 0: on the
   // context stream, GPEMU_CHOL_PRIO=0)
   int chol_prio = 1;
+  // n <= 128: the objective in two one-workgroup launches (gpemu_tiny.hpp; GPEMU_TINY=0 off)
+  bool tiny = true;
   hipStream_t stream2 = nullptr;   // the high-priority stream
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_host = nullptr;   // host-visible results of the value part are in hpin
@@ -1484,6 +1487,7 @@ gpe_ctx* gpe_create(int32_t device) {
     if (const char* eg = std::getenv("GPEMU_GROUP_P0")) c->grp_p0 = std::max(1, std::atoi(eg));
     if (const char* eg = std::getenv("GPEMU_GROUP_STRIDE")) c->grp_stride = std::max(0, std::atoi(eg));
     if (const char* ep = std::getenv("GPEMU_CHOL_PRIO")) c->chol_prio = std::atoi(ep) != 0;
+    if (const char* et = std::getenv("GPEMU_TINY")) c->tiny = std::atoi(et) != 0;
     if (const char* es = std::getenv("GPEMU_POTRF_SB")) {
       c->potrf_sb = std::max(1, std::min(8, std::atoi(es)));
       if (const char* colon = std::strchr(es, ':')) c->potrf_sb_min = std::max(0, std::atoi(colon + 1));
@@ -1530,6 +1534,10 @@ gpe_ctx* gpe_create(int32_t device) {
          hipFuncSetAttribute((const void*)k_gemm<false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
          hipFuncSetAttribute((const void*)k_xasm, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)(DB_LDS_DOUBLES * sizeof(double))) == hipSuccess;
+    const int tl = (G_LDS_LAUNCH_DOUBLES + 2 * TILE * TINY_DM) * (int)sizeof(double);
+    ok = ok && hipFuncSetAttribute((const void*)k_tiny_factor<8>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_tiny_factor<16>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_tiny_factor<32>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess;
     if (!ok) c->err = "hipFuncSetAttribute(max dynamic LDS) failed";
   }
   if (!ok) {
@@ -1655,6 +1663,101 @@ int gpe_gemm_stats(gpe_ctx* c, double* ms_out, double* launches_out, double* flo
   return GPE_OK;
 }
 
+// The objective of a training set of at most 128 points (gpemu_tiny.hpp): K-build, L, X =
+// L^-1, Z, Gram and A^-1 in one workgroup; the host's q x q algebra (the same functions as
+// the general path); R2, [sqrt(c) alpha, W] and the contraction in a second.  One copy in
+// each direction between them, one at the end.
+int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_hp, bool fitnug, double nu,
+                   double s2, double rscale, bool want_grad, double* llh_out, double* grad_out, double* sigma2_out) {
+  const int d = c->d, q = c->q, P = q + 1;
+  TinyArgs a;
+  for (int k = 0; k < d; ++k) {
+    // as scale_training: a zero or NaN length scale is the reference's LinAlgError
+    if (!(hp[k] > 0.0) && !(hp[k] < 0.0))
+      return fail(c, GPE_NOT_PD, "length scale delta[" + std::to_string(k) + "] is zero or NaN");
+    a.invd[k] = 1.0 / hp[k];
+  }
+  for (int k = d; k < TINY_DM; ++k) a.invd[k] = 0.0;
+  c->linv_valid = false;
+  c->zaug_valid = false;
+  c->tr.xdone = false;
+  HIPCHK(c, hipStreamSynchronize(c->stream2));   // (a failed sweep's leftovers, as factor_and_invert)
+  CHK(ensure_small(c, (size_t)P * P + 8));
+  CHK(ensure_pinned(c, (size_t)P * P + d + 64));
+  HIPCHK(c, hipMemsetAsync(c->dinfo, 0, sizeof(int), c->stream));
+  ev_rec(c, 0);
+  a.X = c->dX; a.F = c->dF;
+  a.r = (c->has_r && rscale != 0.0) ? c->dr : nullptr;
+  a.xw = c->dXw; a.L = c->tr.A; a.Xo = c->tr.B; a.Z = c->dZ; a.small = c->dsmall; a.abort_flag = c->dinfo;
+  a.n = (int)c->n; a.d = d; a.P = P; a.want_grad = want_grad ? 1 : 0;
+  a.s2 = s2; a.rscale = rscale;
+  kernel_consts(kernel, nu, true, &a.coff, &a.cdiag);
+  const size_t lds = (G_LDS_LAUNCH_DOUBLES + 2 * TILE * TINY_DM) * sizeof(double);
+  if (d <= 8) hipLaunchKernelGGL(k_tiny_factor<8>, dim3(1), dim3(256), lds, c->stream, a);
+  else if (d <= 16) hipLaunchKernelGGL(k_tiny_factor<16>, dim3(1), dim3(256), lds, c->stream, a);
+  else hipLaunchKernelGGL(k_tiny_factor<32>, dim3(1), dim3(256), lds, c->stream, a);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->hpin, c->dsmall, ((size_t)P * P + 2) * sizeof(double), hipMemcpyDeviceToHost,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const int info = (int)c->hpin[P * P + 1];
+  if (info != 0) {
+    c->err = "matrix not positive definite (pivot " + std::to_string(info) + ")";
+    return GPE_NOT_PD;
+  }
+  const double logdetA = 2.0 * c->hpin[P * P];
+  std::vector<double> G(c->hpin, c->hpin + (size_t)P * P);
+  SmallAlgebra sa = small_from_gram(G, P);
+  if (!sa.ok) {
+    c->err = "H^T A^-1 H not positive definite";
+    return GPE_NOT_PD;
+  }
+  const double n = (double)c->n;
+  double llh, sig2, cfac, gscale;
+  if (gp4ml) {
+    llh = 0.5 * (sa.quad + logdetA + sa.logdetQ + (n - q) * std::log(2.0 * M_PI));
+    sig2 = s2;
+    cfac = 1.0;
+    gscale = s2;
+  } else {
+    sig2 = sa.quad / (n - q - 2.0);
+    llh = 0.5 * ((n - q) * std::log(sig2) + logdetA + sa.logdetQ);
+    cfac = (n - q) / (sig2 * (n - q - 2.0));
+    gscale = sig2;
+  }
+  *llh_out = llh;
+  if (sigma2_out) *sigma2_out = sig2;
+  if (want_grad) {
+    const std::vector<double> T2 = small_t2(sa, q, cfac);
+    std::memcpy(c->hpin, T2.data(), T2.size() * sizeof(double));
+    HIPCHK(c, hipMemcpyAsync(c->dT2, c->hpin, T2.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    TinyGradArgs g;
+    g.Ainv = c->tr.A; g.Xo = c->tr.B; g.Z = c->dZ; g.T2 = c->dT2; g.xw = c->dXw;
+    g.rdiag = (gp4ml && kernel == GPE_KERNEL_STD && c->has_r) ? c->dr : nullptr;
+    g.sums = c->dcsum; g.abort_flag = c->dinfo;
+    g.n = (int)c->n; g.d = d; g.P = P;
+    if (d <= 8) hipLaunchKernelGGL(k_tiny_grad<8>, dim3(1), dim3(256), 0, c->stream, g);
+    else if (d <= 16) hipLaunchKernelGGL(k_tiny_grad<16>, dim3(1), dim3(256), 0, c->stream, g);
+    else hipLaunchKernelGGL(k_tiny_grad<32>, dim3(1), dim3(256), 0, c->stream, g);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(c->hpin, c->dcsum, (d + 3) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    double coff, cdiag;
+    kernel_consts(kernel, nu, true, &coff, &cdiag);
+    small_grad(c->hpin, d, kernel == GPE_KERNEL_ALT_NUG, nu, fitnug, gp4ml, gscale, s2, coff, cdiag, n_hp, grad_out,
+               g.rdiag != nullptr);
+  }
+  if (c->prof) {   // (one phase: the whole evaluation)
+    ev_rec(c, 7);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[7]);
+    for (int i = 0; i < 8; ++i) c->phase_ms[i] = 0.0;
+    c->phase_ms[6] = ms;
+  }
+  return GPE_OK;
+}
+
 int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp, int32_t n_hp,
                   double nu_fixed, int32_t want_grad, double* llh_out, double* grad_out,
                   double* sigma2_out) {
@@ -1680,6 +1783,9 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
     c->gev_used = 0;
     c->gemm_launches = c->gemm_flops = c->gemm_ms = 0.0;
   }
+  if (c->tiny && c->NB == 1 && d <= TINY_DM && q + 1 <= TINY_DM)
+    return tiny_objective(c, gp4ml, kernel, hp, n_hp, fitnug, nu, s2, rscale, want_grad != 0, llh_out, grad_out,
+                          sigma2_out);
 
   // z, w = L^-1 [f H] come out of the factorisation (augmented row); value only runs
   // no L^-1 at all
