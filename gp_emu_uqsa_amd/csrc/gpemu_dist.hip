@@ -353,7 +353,8 @@ struct gpe_dist {
   double* dr = nullptr;
   double* dinvdelta = nullptr;
   int* dinfo = nullptr;    // abort flag / failed pivot (all-reduced with max over RCCL)
-  int* dq = nullptr;       // NB counters: the diagonal tiles' pending-update blocks (G_DQUAD)
+  int* dq = nullptr;       // 3 x NB counters: the diagonal tiles' pending-update blocks (G_DQUAD);
+                           // P = 1: the diagonal flags and the panel halves' stored updates
   double* cpart = nullptr; // contraction partials (scratch, stream-ordered)
   std::vector<Rank> ranks;   // local ranks (all P in loopback, one otherwise)
 
@@ -722,6 +723,9 @@ int build_schedule(gpe_dist* h) {
       p.ldx = TILE;
       p.logdet = R->logdet + k;
       p.diag_col0 = k * TILE;
+      // P = 1: the factor releases this launch's panel tiles through a flag once L and
+      // the leaf inverses are stored (X is assembled after the sweep, k_xasm)
+      if (!gath) p.flag = h->dq + NB + k;
       p.tile_begin = dl.tiles;
       p.ntiles = 1;
       dl.tiles += 1;
@@ -729,21 +733,47 @@ int build_schedule(gpe_dist* h) {
       probs.push_back(p);
       ++dl.count;
     }
-    // P = 1: pending update of the panel tiles, A(i,k) -= L(i, gb:k) L(k, gb:k)^T over the
-    // rows i > k, beside the factorisation (row k is the rank's own).  P > 1: the panel
-    // launch applies it (ranks other than the owner receive row k's part in the broadcast)
-    if (Kp > 0 && !gath) {
-      for (Rank& R : h->ranks) {
-        const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
-        if (c == 0) continue;
-        GemmProb p = dprob(R.A + (long long)a * TILE + (long long)gb * TILE * R.ld, R.ld,
-                           panel_of(h, R, k) + (long long)k * TILE, ldp,
-                           R.A + (long long)a * TILE + (long long)k * TILE * R.ld, R.ld, c, 1, Kp, 0, -1.0, 1.0);
-        p.tile_begin = dl.tiles;
-        p.ntiles = c;
+    // P = 1 (the rank holds every row): the panel tiles ride in the same launch, as the
+    // single-GPU fused sweep's: each G_PHALF0 workgroup applies the pending update
+    // A(i,k) -= L(i, gb:k) L(k, gb:k)^T, stores it and posts, waits for the flag and solves
+    // rows 0-63 of L(i,k) = A(i,k) L_kk^-T by block substitution; each G_PHALF1 workgroup
+    // waits for the step's G_PHALF0 posts and solves rows 64-127.  (Dispatch follows the
+    // problem order: every wait points to earlier workgroups.)  P > 1: the panel launch
+    // after the broadcast applies the update and the inverse in one product.
+    if (!gath) {
+      Rank& R = h->ranks[0];
+      const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
+      if (c > 0) {
+        double* Ckk = R.A + (long long)k * TILE + (long long)k * TILE * R.ld;
+        GemmProb q = dprob(Kp ? R.A + (long long)a * TILE + (long long)gb * TILE * R.ld : nullptr, R.ld,
+                           Kp ? R.A + (long long)k * TILE + (long long)gb * TILE * R.ld : nullptr, R.ld,
+                           R.A + (long long)a * TILE + (long long)k * TILE * R.ld, R.ld, c, 1, Kp,
+                           G_PANEL | G_PHALF0, Kp ? -1.0 : 1.0, 1.0);
+        q.cpost = h->dq + 2 * NB + k;
+        q.X = R.dinv + (long long)Kp * TILE;
+        q.ldx = TILE;
+        q.flag = h->dq + NB + k;
+        q.diag_col0 = -TILE;   // (no GEMM_TRACE slot)
+        q.Ld = Ckk;
+        q.ldd = R.ld;
+        q.tile_begin = dl.tiles;
+        q.ntiles = c;
         dl.tiles += c;
-        dl.cdef = dl.cdef || gemm_cdef(p);
-        probs.push_back(p);
+        dl.cdef = dl.cdef || gemm_cdef(q);
+        probs.push_back(q);
+        ++dl.count;
+        GemmProb q1 = q;
+        q1.flags = G_PANEL | G_PHALF1;
+        q1.A = q1.B = nullptr;
+        q1.K = 0;
+        q1.alpha = 1.0;
+        q1.beta = 0.0;
+        q1.pre0 = q.cpost;
+        q1.pre0_n = c;
+        q1.cpost = nullptr;
+        q1.tile_begin = dl.tiles;
+        dl.tiles += c;
+        probs.push_back(q1);
         ++dl.count;
       }
     }
@@ -772,7 +802,7 @@ int build_schedule(gpe_dist* h) {
     pl.first = (int)probs.size();
     for (Rank& R : h->ranks) {
       const int a = li0_of(k, P, R.rank), c = std::max(0, R.nloc - a);
-      if (c == 0) continue;
+      if (c == 0 || !gath) continue;
       double* Aik = R.A + (long long)a * TILE + (long long)k * TILE * R.ld;
       GemmProb p = gath ? dprob(R.A + (long long)a * TILE + (long long)gb * TILE * R.ld, R.ld, R.dinv, TILE, Aik,
                                 R.ld, c, 1, Kp + TILE, 0, 1.0, 0.0)
@@ -1190,8 +1220,7 @@ int step(gpe_dist* h, int k) {
   const long long Kp = (long long)(k - h->gstart[k]) * TILE;
   DCHK(launch(h, h->diag[k]));
   DCHK(launch(h, h->mrow[k]));
-  DCHK(coll_bcast(h, &Rank::dinv, 0, (size_t)TILE * (gather_panels(h) ? Kp + TILE : TILE),
-                  owner) );
+  if (gather_panels(h)) DCHK(coll_bcast(h, &Rank::dinv, 0, (size_t)TILE * (Kp + TILE), owner));
   if (h->grad_now) {
     if (Rank* O = rank_slot(h, owner))
       DCHK_HIP(h, hipMemcpy2DAsync(O->X + (long long)(k / P) * TILE + (long long)k * TILE * O->ld,
@@ -1445,7 +1474,7 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
   DCHK(dalloc(h, &h->dinvdelta, (size_t)d, &h->shared_bytes));
   // local ranks and their sweep buffers
   build_groups(h);
-  DCHK(dalloc(h, &h->dq, (size_t)h->NB, &h->shared_bytes));
+  DCHK(dalloc(h, &h->dq, 3 * (size_t)h->NB, &h->shared_bytes));
   const int NT = h->NB + h->NA;
   h->panel_sz = (size_t)NT * TILE * TILE * h->wmax;
   // the group all-gather's segment: W column blocks of the most tile rows below the group
@@ -1528,8 +1557,16 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
       DCHK_HIP(h, hipMemsetAsync(R.X, 0, (size_t)R.ld * NB * TILE * sizeof(double), h->stream));
   }
   DCHK(kbuild(h, kernel, nu, s2, rscale));
-  DCHK_HIP(h, hipMemsetAsync(h->dq, 0, (size_t)NB * sizeof(int), h->stream));
+  DCHK_HIP(h, hipMemsetAsync(h->dq, 0, 3 * (size_t)NB * sizeof(int), h->stream));
   DCHK(group_sweep(h));
+  // P = 1: the sweep's factors stored L and the leaf inverses only (flag mode): the
+  // TRTRI's leaves X(t, t) are assembled here for every diagonal tile at once
+  if (h->grad_now && !gather_panels(h))
+    for (Rank& R : h->ranks) {
+      if (R.nlx == 0) continue;
+      hipLaunchKernelGGL(k_xasm, dim3(NB), dim3(256), DB_LDS_DOUBLES * sizeof(double), h->stream, R.A, R.X, R.ld);
+      DCHK_HIP(h, hipGetLastError());
+    }
 
   // Gram of L^-1 [f H] = -(the augmented rows' diagonal block; its lower tiles), and
   // Z = L^-1 [f H], from the owners of the augmented tile rows: each places its rows of
