@@ -171,6 +171,7 @@ static __global__ void __launch_bounds__(256) k_tiny_grad(TinyGradArgs a) {
   __shared__ double ws[TILE * TINY_DM];   // Wa = [sqrt(c) alpha, W]
   __shared__ double xs[TILE * DM];
   __shared__ double t2[TINY_DM * TINY_DM];
+  __shared__ double xk[32 * TILE];        // 32 rows of X at a time ([kk][j])
   __shared__ double red[4 * (DM + 3)];
   if (a.abort_flag && *a.abort_flag) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -202,16 +203,24 @@ static __global__ void __launch_bounds__(256) k_tiny_grad(TinyGradArgs a) {
 #pragma unroll
   for (int u = 0; u < TINY_DM / 2; ++u) zs[i * TINY_DM + h + 2 * u] = rv[u];
   __syncthreads();
-  // Wa = X^T R2: row j = i of Wa over rows k >= j of X (column j of X, global)
+  // Wa = X^T R2: row j = i of Wa over rows k >= j of X, X staged 32 rows at a time
+  // (coalesced: a column's 32 rows are contiguous)
   {
     double w[TINY_DM / 2];
 #pragma unroll
     for (int u = 0; u < TINY_DM / 2; ++u) w[u] = 0.0;
-    const double* xcol = a.Xo + i * TILE;
-    for (int k = i; k < TILE; ++k) {
-      const double x = xcol[k];
+    for (int k0 = 0; k0 < TILE; k0 += 32) {
+      for (int e = tid; e < 32 * TILE; e += 256) {
+        const int kk = e & 31, j = e >> 5;
+        xk[kk * TILE + j] = a.Xo[k0 + kk + j * TILE];
+      }
+      __syncthreads();
+      for (int kk = max(0, i - k0); kk < 32; ++kk) {
+        const double x = xk[kk * TILE + i];
 #pragma unroll
-      for (int u = 0; u < TINY_DM / 2; ++u) w[u] = fma(x, zs[k * TINY_DM + h + 2 * u], w[u]);
+        for (int u = 0; u < TINY_DM / 2; ++u) w[u] = fma(x, zs[(k0 + kk) * TINY_DM + h + 2 * u], w[u]);
+      }
+      __syncthreads();
     }
 #pragma unroll
     for (int u = 0; u < TINY_DM / 2; ++u) ws[i * TINY_DM + h + 2 * u] = w[u];
