@@ -419,10 +419,21 @@ void split_k(std::vector<GemmProb>& probs, double* part, int* tcnt) {
 // Order the tiles of one launch: rows (problem, ti) sorted longest-first, greedily
 // packed into 8 bins of equal work (one per XCD under round-robin dispatch, so a
 // row's A panel stays in one XCD's L2), bins interleaved block by block.
+// GPEMU_XCD_BLOCK=b (dev A/B): instead of whole rows, b x b blocks of tiles go to the XCD
+// bins, so the tiles one XCD runs at once share b A panels and b B panels in its L2
+int xcd_block() {
+  static const int b = [] {
+    const char* e = std::getenv("GPEMU_XCD_BLOCK");
+    return e ? std::max(0, std::min(64, std::atoi(e))) : 0;
+  }();
+  return b;
+}
+
 std::vector<unsigned> order_tiles(const std::vector<GemmProb>& probs) {
   struct Row { int p, ti; double w; std::vector<int> tj; };
   std::vector<Row> rows;
   std::vector<unsigned> tail;   // G_PANEL tiles wait on the G_DIAG tile: dispatch them last
+  const int xb = xcd_block();
   for (int p = 0; p < (int)probs.size(); ++p) {
     const GemmProb& P = probs[p];
     if (P.flags & G_PANEL) {
@@ -435,8 +446,30 @@ std::vector<unsigned> order_tiles(const std::vector<GemmProb>& probs) {
       if (P.flags & G_KBEG_TI) kb = ti * TILE;
       if (P.flags & G_KEND_TI) ke = std::min(ke, (ti * P.kti_mul + P.kti_off + 1) * TILE);
       const double wt = (double)std::max(ke - kb, 0) + 2.0 * GK;   // + fixed per-tile cost
-      Row r{p, ti, 0.0, {}};
       const int tjmax = (P.flags & G_CLOWER) ? ti : P.nt - 1;
+      if (xb > 1 && !(P.flags & (G_DQUAD | G_DIAG))) {   // one "row" per b x b block of tiles
+        for (int tj0 = 0; tj0 <= tjmax; tj0 += xb) {
+          if (ti % xb) {   // rows of a block after its first join the first's entries
+            Row* r0 = nullptr;
+            for (auto it = rows.rbegin(); it != rows.rend(); ++it)
+              if (it->p == p && it->ti == ti - ti % xb && !it->tj.empty() && it->tj.front() / xb == tj0 / xb) {
+                r0 = &*it;
+                break;
+              }
+            if (r0) {
+              for (int tj = tj0; tj <= std::min(tjmax, tj0 + xb - 1); ++tj) r0->tj.push_back(tj + (ti % xb) * 4096);
+              r0->w += wt * (double)(std::min(tjmax, tj0 + xb - 1) - tj0 + 1);
+              continue;
+            }
+          }
+          Row r{p, ti, 0.0, {}};
+          for (int tj = tj0; tj <= std::min(tjmax, tj0 + xb - 1); ++tj) r.tj.push_back(tj);
+          r.w = wt * (double)r.tj.size();
+          rows.push_back(std::move(r));
+        }
+        continue;
+      }
+      Row r{p, ti, 0.0, {}};
       for (int tj = 0; tj <= tjmax; ++tj) r.tj.push_back(tj);
       r.w = wt * (double)r.tj.size();
       if (!r.tj.empty()) rows.push_back(std::move(r));
@@ -451,7 +484,8 @@ std::vector<unsigned> order_tiles(const std::vector<GemmProb>& probs) {
   for (const Row& r : rows) {
     int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
     load[x] += r.w;
-    for (int tj : r.tj) bins[x].push_back(((unsigned)r.p << 24) | ((unsigned)r.ti << 12) | (unsigned)tj);
+    for (int tj : r.tj)   // (block entries carry their row offset in tj / 4096)
+      bins[x].push_back(((unsigned)r.p << 24) | ((unsigned)(r.ti + tj / 4096) << 12) | (unsigned)(tj % 4096));
   }
   std::vector<unsigned> out;
   // a factored diagonal tile starts first, after the quadrants of its pending update
