@@ -1698,9 +1698,10 @@ int gpe_gemm_stats(gpe_ctx* c, double* ms_out, double* launches_out, double* flo
 }
 
 // The objective of a training set of at most 128 points (gpemu_tiny.hpp): K-build, L, X =
-// L^-1, Z, Gram and A^-1 in one workgroup; the host's q x q algebra (the same functions as
-// the general path); R2, [sqrt(c) alpha, W] and the contraction in a second.  One copy in
-// each direction between them, one at the end.
+// L^-1, Z, Gram, and A^-1 with its part of the contraction in one workgroup; the host's
+// q x q algebra (the same functions as the general path); R2, [sqrt(c) alpha, W] and the
+// -W W^T part of the contraction in a second.  One copy in each direction between them,
+// one at the end.
 int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_hp, bool fitnug, double nu,
                    double s2, double rscale, bool want_grad, double* llh_out, double* grad_out, double* sigma2_out) {
   const int d = c->d, q = c->q, P = q + 1;
@@ -1716,12 +1717,13 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
   c->zaug_valid = false;
   c->tr.xdone = false;
   HIPCHK(c, hipStreamSynchronize(c->stream2));   // (a failed sweep's leftovers, as factor_and_invert)
-  CHK(ensure_small(c, (size_t)P * P + 8));
-  CHK(ensure_pinned(c, (size_t)P * P + d + 64));
+  CHK(ensure_small(c, (size_t)P * P + d + 8));
+  CHK(ensure_pinned(c, (size_t)P * P + 2 * d + 64));
   HIPCHK(c, hipMemsetAsync(c->dinfo, 0, sizeof(int), c->stream));
   ev_rec(c, 0);
   a.X = c->dX; a.F = c->dF;
   a.r = (c->has_r && rscale != 0.0) ? c->dr : nullptr;
+  a.rdiag = (gp4ml && kernel == GPE_KERNEL_STD && c->has_r) ? c->dr : nullptr;
   a.xw = c->dXw; a.L = c->tr.A; a.Xo = c->tr.B; a.Z = c->dZ; a.small = c->dsmall; a.abort_flag = c->dinfo;
   a.n = (int)c->n; a.d = d; a.P = P; a.want_grad = want_grad ? 1 : 0;
   a.s2 = s2; a.rscale = rscale;
@@ -1731,9 +1733,10 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
   else if (d <= 16) hipLaunchKernelGGL(k_tiny_factor<16>, dim3(1), dim3(256), lds, c->stream, a);
   else hipLaunchKernelGGL(k_tiny_factor<32>, dim3(1), dim3(256), lds, c->stream, a);
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(c->hpin, c->dsmall, ((size_t)P * P + 2) * sizeof(double), hipMemcpyDeviceToHost,
-                           c->stream));
+  const size_t ns = (size_t)P * P + 2 + (want_grad ? d + 3 : 0);   // Gram, log|L|, column, A^-1 sums
+  HIPCHK(c, hipMemcpyAsync(c->hpin, c->dsmall, ns * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::vector<double> asums(c->hpin + (size_t)P * P + 2, c->hpin + ns);
   const int info = (int)c->hpin[P * P + 1];
   if (info != 0) {
     c->err = "matrix not positive definite (pivot " + std::to_string(info) + ")";
@@ -1766,8 +1769,8 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
     std::memcpy(c->hpin, T2.data(), T2.size() * sizeof(double));
     HIPCHK(c, hipMemcpyAsync(c->dT2, c->hpin, T2.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
     TinyGradArgs g;
-    g.Ainv = c->tr.A; g.Xo = c->tr.B; g.Z = c->dZ; g.T2 = c->dT2; g.xw = c->dXw;
-    g.rdiag = (gp4ml && kernel == GPE_KERNEL_STD && c->has_r) ? c->dr : nullptr;
+    g.Xo = c->tr.B; g.Z = c->dZ; g.T2 = c->dT2; g.xw = c->dXw;
+    g.rdiag = a.rdiag;
     g.sums = c->dcsum; g.abort_flag = c->dinfo;
     g.n = (int)c->n; g.d = d; g.P = P;
     if (d <= 8) hipLaunchKernelGGL(k_tiny_grad<8>, dim3(1), dim3(256), 0, c->stream, g);
@@ -1776,10 +1779,12 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(c->hpin, c->dcsum, (d + 3) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<double> red(d + 3);
+    for (int k = 0; k < d + 3; ++k) red[k] = asums[k] + c->hpin[k];   // the A^-1 and -W W^T parts
     double coff, cdiag;
     kernel_consts(kernel, nu, true, &coff, &cdiag);
-    small_grad(c->hpin, d, kernel == GPE_KERNEL_ALT_NUG, nu, fitnug, gp4ml, gscale, s2, coff, cdiag, n_hp, grad_out,
-               g.rdiag != nullptr);
+    small_grad(red.data(), d, kernel == GPE_KERNEL_ALT_NUG, nu, fitnug, gp4ml, gscale, s2, coff, cdiag, n_hp,
+               grad_out, g.rdiag != nullptr);
   }
   if (c->prof) {   // (one phase: the whole evaluation)
     ev_rec(c, 7);
