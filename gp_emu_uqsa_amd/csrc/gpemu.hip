@@ -208,7 +208,7 @@ struct gpe_ctx {
   // the fused Cholesky on the context's high-priority stream (default 1; 0: on the
   // context stream, GPEMU_CHOL_PRIO=0)
   int chol_prio = 1;
-  // n <= 128: the objective in two one-workgroup launches (gpemu_tiny.hpp; GPEMU_TINY=0 off)
+  // n <= 128: the objective in one one-workgroup launch (gpemu_tiny.hpp; GPEMU_TINY=0 off)
   bool tiny = true;
   hipStream_t stream2 = nullptr;   // the high-priority stream
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -1568,10 +1568,11 @@ gpe_ctx* gpe_create(int32_t device) {
          hipFuncSetAttribute((const void*)k_gemm<false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, gl) == hipSuccess &&
          hipFuncSetAttribute((const void*)k_xasm, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)(DB_LDS_DOUBLES * sizeof(double))) == hipSuccess;
-    const int tl = (G_LDS_LAUNCH_DOUBLES + 2 * TILE * TINY_DM) * (int)sizeof(double);
-    ok = ok && hipFuncSetAttribute((const void*)k_tiny_factor<8>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess &&
-         hipFuncSetAttribute((const void*)k_tiny_factor<16>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess &&
-         hipFuncSetAttribute((const void*)k_tiny_factor<32>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess;
+    const int tl = (G_LDS_LAUNCH_DOUBLES + 2 * TILE * TINY_ZP) * (int)sizeof(double);
+    ok = ok && hipFuncSetAttribute((const void*)k_tiny<4>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_tiny<8>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_tiny<16>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_tiny<32>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess;
     if (!ok) c->err = "hipFuncSetAttribute(max dynamic LDS) failed";
   }
   if (!ok) {
@@ -1698,10 +1699,10 @@ int gpe_gemm_stats(gpe_ctx* c, double* ms_out, double* launches_out, double* flo
 }
 
 // The objective of a training set of at most 128 points (gpemu_tiny.hpp): K-build, L, X =
-// L^-1, Z, Gram, and A^-1 with its part of the contraction in one workgroup; the host's
-// q x q algebra (the same functions as the general path); R2, [sqrt(c) alpha, W] and the
-// -W W^T part of the contraction in a second.  One copy in each direction between them,
-// one at the end.
+// L^-1, Z, Gram and, with the gradient, the q x q algebra, W and the contraction of
+// M = A^-1 - W W^T in one workgroup; one copy back (Gram, log|L|, the failed column, the
+// d + 3 sums), from which the host's small_from_gram / small_grad (the general path's)
+// give the LLH and the gradient.
 int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_hp, bool fitnug, double nu,
                    double s2, double rscale, bool want_grad, double* llh_out, double* grad_out, double* sigma2_out) {
   const int d = c->d, q = c->q, P = q + 1;
@@ -1725,18 +1726,18 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
   a.r = (c->has_r && rscale != 0.0) ? c->dr : nullptr;
   a.rdiag = (gp4ml && kernel == GPE_KERNEL_STD && c->has_r) ? c->dr : nullptr;
   a.xw = c->dXw; a.L = c->tr.A; a.Xo = c->tr.B; a.Z = c->dZ; a.small = c->dsmall; a.abort_flag = c->dinfo;
-  a.n = (int)c->n; a.d = d; a.P = P; a.want_grad = want_grad ? 1 : 0;
+  a.n = (int)c->n; a.d = d; a.P = P; a.want_grad = want_grad ? 1 : 0; a.mucm = gp4ml ? 0 : 1;
   a.s2 = s2; a.rscale = rscale;
   kernel_consts(kernel, nu, true, &a.coff, &a.cdiag);
-  const size_t lds = (G_LDS_LAUNCH_DOUBLES + 2 * TILE * TINY_DM) * sizeof(double);
-  if (d <= 8) hipLaunchKernelGGL(k_tiny_factor<8>, dim3(1), dim3(256), lds, c->stream, a);
-  else if (d <= 16) hipLaunchKernelGGL(k_tiny_factor<16>, dim3(1), dim3(256), lds, c->stream, a);
-  else hipLaunchKernelGGL(k_tiny_factor<32>, dim3(1), dim3(256), lds, c->stream, a);
+  const size_t lds = (G_LDS_LAUNCH_DOUBLES + 2 * TILE * TINY_ZP) * sizeof(double);
+  if (d <= 4) hipLaunchKernelGGL(k_tiny<4>, dim3(1), dim3(256), lds, c->stream, a);
+  else if (d <= 8) hipLaunchKernelGGL(k_tiny<8>, dim3(1), dim3(256), lds, c->stream, a);
+  else if (d <= 16) hipLaunchKernelGGL(k_tiny<16>, dim3(1), dim3(256), lds, c->stream, a);
+  else hipLaunchKernelGGL(k_tiny<32>, dim3(1), dim3(256), lds, c->stream, a);
   HIPCHK(c, hipGetLastError());
-  const size_t ns = (size_t)P * P + 2 + (want_grad ? d + 3 : 0);   // Gram, log|L|, column, A^-1 sums
+  const size_t ns = (size_t)P * P + 2 + (want_grad ? d + 4 : 0);   // Gram, log|L|, column, sums, Q flag
   HIPCHK(c, hipMemcpyAsync(c->hpin, c->dsmall, ns * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  std::vector<double> asums(c->hpin + (size_t)P * P + 2, c->hpin + ns);
   const int info = (int)c->hpin[P * P + 1];
   if (info != 0) {
     c->err = "matrix not positive definite (pivot " + std::to_string(info) + ")";
@@ -1765,26 +1766,14 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
   *llh_out = llh;
   if (sigma2_out) *sigma2_out = sig2;
   if (want_grad) {
-    const std::vector<double> T2 = small_t2(sa, q, cfac);
-    std::memcpy(c->hpin, T2.data(), T2.size() * sizeof(double));
-    HIPCHK(c, hipMemcpyAsync(c->dT2, c->hpin, T2.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    TinyGradArgs g;
-    g.Xo = c->tr.B; g.Z = c->dZ; g.T2 = c->dT2; g.xw = c->dXw;
-    g.rdiag = a.rdiag;
-    g.sums = c->dcsum; g.abort_flag = c->dinfo;
-    g.n = (int)c->n; g.d = d; g.P = P;
-    if (d <= 8) hipLaunchKernelGGL(k_tiny_grad<8>, dim3(1), dim3(256), 0, c->stream, g);
-    else if (d <= 16) hipLaunchKernelGGL(k_tiny_grad<16>, dim3(1), dim3(256), 0, c->stream, g);
-    else hipLaunchKernelGGL(k_tiny_grad<32>, dim3(1), dim3(256), 0, c->stream, g);
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipMemcpyAsync(c->hpin, c->dcsum, (d + 3) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    std::vector<double> red(d + 3);
-    for (int k = 0; k < d + 3; ++k) red[k] = asums[k] + c->hpin[k];   // the A^-1 and -W W^T parts
-    double coff, cdiag;
-    kernel_consts(kernel, nu, true, &coff, &cdiag);
-    small_grad(red.data(), d, kernel == GPE_KERNEL_ALT_NUG, nu, fitnug, gp4ml, gscale, s2, coff, cdiag, n_hp,
-               grad_out, g.rdiag != nullptr);
+    // the device's own Cholesky of Q (same arithmetic) refusing a Q the host's accepted
+    if (c->hpin[P * P + 2 + d + 3] != 0.0) {
+      c->err = "H^T A^-1 H not positive definite";
+      return GPE_NOT_PD;
+    }
+    (void)cfac;   // (the device's T2 carries sqrt(cfac))
+    small_grad(c->hpin + (size_t)P * P + 2, d, kernel == GPE_KERNEL_ALT_NUG, nu, fitnug, gp4ml, gscale, s2, a.coff,
+               a.cdiag, n_hp, grad_out, a.rdiag != nullptr);
   }
   if (c->prof) {   // (one phase: the whole evaluation)
     ev_rec(c, 7);
