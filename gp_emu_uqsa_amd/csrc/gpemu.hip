@@ -1571,6 +1571,7 @@ gpe_ctx* gpe_create(int32_t device) {
     const int tl = (G_LDS_LAUNCH_DOUBLES + 2 * TILE * TINY_ZP) * (int)sizeof(double);
     ok = ok && hipFuncSetAttribute((const void*)k_tiny<4>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess &&
          hipFuncSetAttribute((const void*)k_tiny<8>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_tiny<12>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess &&
          hipFuncSetAttribute((const void*)k_tiny<16>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess &&
          hipFuncSetAttribute((const void*)k_tiny<32>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess;
     if (!ok) c->err = "hipFuncSetAttribute(max dynamic LDS) failed";
@@ -1732,6 +1733,7 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
   const size_t lds = (G_LDS_LAUNCH_DOUBLES + 2 * TILE * TINY_ZP) * sizeof(double);
   if (d <= 4) hipLaunchKernelGGL(k_tiny<4>, dim3(1), dim3(256), lds, c->stream, a);
   else if (d <= 8) hipLaunchKernelGGL(k_tiny<8>, dim3(1), dim3(256), lds, c->stream, a);
+  else if (d <= 12) hipLaunchKernelGGL(k_tiny<12>, dim3(1), dim3(256), lds, c->stream, a);
   else if (d <= 16) hipLaunchKernelGGL(k_tiny<16>, dim3(1), dim3(256), lds, c->stream, a);
   else hipLaunchKernelGGL(k_tiny<32>, dim3(1), dim3(256), lds, c->stream, a);
   HIPCHK(c, hipGetLastError());

@@ -33,9 +33,9 @@ constexpr int TINY_DM = 32;   // basis columns held per row
 // doubles put 32 or 64 lanes of a wave on one bank: ~100 us per launch in a first version)
 constexpr int TINY_ZP = TINY_DM + 1;
 template <int DM> struct TinyPitch { static constexpr int v = DM + 1; };
-// the q x q algebra in zs once Z is consumed: Gram (P x P), Q's Cholesky (q x q), its
-// diagonal, beta, T2 ([k][p], pitch TINY_ZP)
-constexpr int TY_G = 0, TY_Q = 1024, TY_QD = 2048, TY_B = 2080, TY_T2 = 2112;
+// the q x q algebra in zs once Z is consumed: Gram (P x P), a flag, u, T2 ([k][p], pitch
+// TINY_ZP)
+constexpr int TY_G = 0, TY_QD = 2048, TY_B = 2080, TY_T2 = 2112;
 static_assert(TY_T2 + TINY_DM * TINY_ZP <= 128 * TINY_ZP, "algebra fits in zs");
 
 // dev-tool phase clocks (tools/hip/tiny_bench.hip): -DTINY_TIMING
@@ -293,7 +293,6 @@ static __global__ void __launch_bounds__(256) k_tiny(TinyArgs a) {
   __syncthreads();   // Z consumed: zs takes the algebra
   TINY_T(8);
   double* G = zs + TY_G;
-  double* Qa = zs + TY_Q;
   double* Qd = zs + TY_QD;
   double* bt = zs + TY_B;
   double* t2 = zs + TY_T2;
@@ -309,36 +308,64 @@ static __global__ void __launch_bounds__(256) k_tiny(TinyArgs a) {
   }
   for (int e = tid; e < TINY_DM * ZP; e += 256) t2[e] = 0.0;
   __syncthreads();
-  for (int e = tid; e < 32 * 32; e += 256) {   // Q = G[1:, 1:] (pitch 32)
-    const int i = e >> 5, k = e & 31;
-    Qa[e] = (i < q && k < q) ? G[(i + 1) * P + k + 1] : 0.0;
+  // The q x q algebra on wave 0, lane i < q holding row i of Q in registers (every loop
+  // over columns unrolled to 32, skipped past q): the Cholesky right-looking (each entry's
+  // terms in small_chol's order), u = Kq^-1 wz and the rows of Kq^-1 (small_fwd's and
+  // small_trinv's order of terms), the column entries passed by shuffles.  Kq^-1 goes to
+  // T2(c + 1, 1 + i) = Kq^-1(i, c), u to bt; then beta = Kq^-T u and quad = zz - |u|^2
+  // (= zz - wz^T Q^-1 wz) below.
+  if (wave == 0) {
+    const int i = lane;
+    double qr[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) qr[k] = (i < q && k < q) ? G[(i + 1) * P + k + 1] : 0.0;
+    bool okq = true;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      if (j < q && okq) {
+        const double piv = __shfl(qr[j], j, 64);
+        if (!(piv > 0.0)) okq = false;   // (uniform over the wave)
+        const double dj = sqrt(piv);
+        const double l = i == j ? dj : (i > j ? qr[j] / dj : 0.0);
+        qr[j] = l;
+#pragma unroll
+        for (int k = j + 1; k < 32; ++k)
+          if (k < q) qr[k] = fma(-l, __shfl(l, k, 64), qr[k]);   // (entries k > i: unused)
+      }
+    }
+    double acc = (i < q) ? G[(i + 1) * P] : 0.0, uval = 0.0;
+    double xr[32];
+#pragma unroll
+    for (int c = 0; c < 32; ++c) xr[c] = i == c ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      if (k < q && okq) {
+        const double dk = __shfl(qr[k], k, 64);   // L(k, k)
+        const double uk = __shfl(acc / dk, k, 64);
+        uval = i == k ? uk : uval;
+        acc = fma(-qr[k], uk, acc);
+#pragma unroll
+        for (int c = 0; c <= k; ++c) {
+          if (i == k) xr[c] = xr[c] / dk;
+          const double xkc = __shfl(xr[c], k, 64);
+          if (i > k) xr[c] = fma(-qr[k], xkc, xr[c]);
+        }
+      }
+    }
+    if (i < q) {
+      bt[i] = uval;
+#pragma unroll
+      for (int c = 0; c < 32; ++c)
+        if (c <= i) t2[(c + 1) * ZP + 1 + i] = xr[c];
+    }
+    if (lane == 0) Qd[0] = okq ? 0.0 : 1.0;
   }
   __syncthreads();
-  // Cholesky of Q (small_chol's order of terms): column j by the threads of its rows, the
-  // pivot by every thread
-  for (int j = 0; j < q; ++j) {
-    const double s = tiny_dot(Qa[j * 32 + j], Qa + j * 32, 1, Qa + j * 32, 1, 0, j);
-    if (!(s > 0.0)) {   // (uniform) H^T A^-1 H not positive definite
-      if (tid == 0) a.small[P * P + 2 + d + 3] = 1.0;
-      return;
-    }
-    const double dj = sqrt(s);
-    if (tid > j && tid < q) Qa[tid * 32 + j] = tiny_dot(Qa[tid * 32 + j], Qa + tid * 32, 1, Qa + j * 32, 1, 0, j) / dj;
-    if (tid == 0) Qd[j] = dj;
-    __syncthreads();
+  if (Qd[0] != 0.0) {   // (uniform) H^T A^-1 H not positive definite
+    if (tid == 0) a.small[P * P + 2 + d + 3] = 1.0;
+    return;
   }
   TINY_T(9);
-  // T2 = [[sqrt(c), 0], [-sqrt(c) beta, Kq^-T]] (small_t2): Kq^-1 one column per lane
-  // (small_trinv's forward substitution) into T2(c + 1, 1 + i) = Kq^-1(i, c); then
-  // u = Kq^-1 wz, beta = Kq^-T u and quad = zz - |u|^2 (= zz - wz^T Q^-1 wz)
-  if (tid < q) {
-    const int c = tid;
-    double* e = t2 + (c + 1) * ZP + 1;
-    for (int i = c; i < q; ++i) e[i] = tiny_dot(i == c ? 1.0 : 0.0, Qa + i * 32, 1, e, 1, c, i) / Qd[i];
-  }
-  __syncthreads();
-  if (tid < q) bt[tid] = -tiny_dot(0.0, t2 + 1 + tid + ZP, ZP, G + P, P, 0, tid + 1);   // u_i
-  __syncthreads();
   {
     const double quad = tiny_dot(G[0], bt, 1, bt, 1, 0, q);
     double cfac = 1.0;

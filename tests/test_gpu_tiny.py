@@ -53,7 +53,7 @@ def _hp(d, variant, fitn, kind):
     return np.array(hp)
 
 
-@pytest.mark.parametrize("n,d", [(60, 2), (100, 3), (128, 10), (97, 1), (128, 30), (40, 16), (5, 1)])
+@pytest.mark.parametrize("n,d", [(60, 2), (100, 3), (128, 10), (97, 1), (128, 30), (40, 16), (5, 1), (80, 6)])
 @pytest.mark.parametrize("case", CASES, ids=["gp4ml_fit", "gp4ml_fix", "mucm_fit", "mucm_fix", "alt_r", "std_r"])
 def test_tiny_matches_oracle_and_general(ctx, general, n, d, case):
     variant, kind, fitn, use_r = case
