@@ -142,6 +142,9 @@ struct gpe_ctx {
   double* dXsw = nullptr;
   size_t xs_cap = 0;
   double* dsmall = nullptr;  // generic small device scratch
+  double* dtiny = nullptr;   // n <= 128 path: X's image, W, the helpers' partials
+  int tiny_ek = 0, tiny_eg = 0;   // k_tiny's call ordinals (its sync words in dinfo[1..4])
+  bool tiny_dirty = true;         // zero dinfo[1..5] before the next k_tiny
   size_t small_cap = 0;
 
   // pinned host staging
@@ -1551,7 +1554,7 @@ gpe_ctx* gpe_create(int32_t device) {
     delete c;
     return nullptr;
   }
-  bool ok = dalloc(c, &c->dinfo, 4) == GPE_OK && dalloc(c, &c->dprobs, MAX_PROBS) == GPE_OK &&
+  bool ok = dalloc(c, &c->dinfo, 8) == GPE_OK && dalloc(c, &c->dprobs, MAX_PROBS) == GPE_OK &&
             ensure_shape_bufs(c, GPE_MAX_DIMS, GPE_MAX_COLS) == GPE_OK;
   for (int i = 0; i < 16 && ok; ++i) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
   if (ok) {
@@ -1592,7 +1595,7 @@ void gpe_destroy(gpe_ctx* c) {
                     c->dX, c->dXw, c->dF, c->dr, c->tr.A, c->tr.B, c->tr.logdet, c->aux.A, c->aux.B,
                     c->aux.logdet, c->dinvdelta, c->dZ,
                     c->dR2, c->dWa, c->dskp, c->dgpart, c->dgram, c->dT2, c->dcpart, c->dcsum,
-                    c->dW1, c->dW2, c->dW3, c->dXs, c->dXsw, c->dsmall, c->dRn, c->dNU,
+                    c->dW1, c->dW2, c->dW3, c->dXs, c->dXsw, c->dsmall, c->dtiny, c->dRn, c->dNU,
                     c->dVall, c->dXall, c->dTall};
   for (double* b : bufs)
     if (b) hipFree(b);
@@ -1699,11 +1702,13 @@ int gpe_gemm_stats(gpe_ctx* c, double* ms_out, double* launches_out, double* flo
   return GPE_OK;
 }
 
-// The objective of a training set of at most 128 points (gpemu_tiny.hpp): K-build, L, X =
-// L^-1, Z, Gram and, with the gradient, the q x q algebra, W and the contraction of
-// M = A^-1 - W W^T in one workgroup; one copy back (Gram, log|L|, the failed column, the
-// d + 3 sums), from which the host's small_from_gram / small_grad (the general path's)
-// give the LLH and the gradient.
+// The objective of a training set of at most 128 points (gpemu_tiny.hpp): ONE launch of
+// k_tiny (workgroup 0: L, X = L^-1, Z, Gram and, with the gradient, the q x q algebra and W;
+// nine helper workgroups: the K-build and the contraction of M = A^-1 - W W^T), which
+// writes Gram, log|L|, the failed column and the d + 3 sums straight into the pinned host
+// buffer; the host's small_from_gram / small_grad (the general path's) give the LLH and the
+// gradient.  No memset (the sync words count up over the calls; zeroed only after a call
+// that did not end cleanly) and no copy.
 int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_hp, bool fitnug, double nu,
                    double s2, double rscale, bool want_grad, double* llh_out, double* grad_out, double* sigma2_out) {
   const int d = c->d, q = c->q, P = q + 1;
@@ -1719,27 +1724,34 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
   c->zaug_valid = false;
   c->tr.xdone = false;
   HIPCHK(c, hipStreamSynchronize(c->stream2));   // (a failed sweep's leftovers, as factor_and_invert)
-  CHK(ensure_small(c, (size_t)P * P + d + 8));
+  constexpr size_t tiny_doubles = 36 * DB_BS + TILE * 32 + TINY_NH * 64;
+  if (!c->dtiny) CHK(dalloc(c, &c->dtiny, tiny_doubles));
   CHK(ensure_pinned(c, (size_t)P * P + 2 * d + 64));
-  HIPCHK(c, hipMemsetAsync(c->dinfo, 0, sizeof(int), c->stream));
+  if (c->tiny_dirty || c->tiny_ek > (1 << 26)) {   // the sync words and the abort flag
+    HIPCHK(c, hipMemsetAsync(c->dinfo + 1, 0, (TINY_SYNC_INTS + 1) * sizeof(int), c->stream));
+    c->tiny_ek = c->tiny_eg = 0;
+    c->tiny_dirty = false;
+  }
   ev_rec(c, 0);
   a.X = c->dX; a.F = c->dF;
   a.r = (c->has_r && rscale != 0.0) ? c->dr : nullptr;
   a.rdiag = (gp4ml && kernel == GPE_KERNEL_STD && c->has_r) ? c->dr : nullptr;
-  a.xw = c->dXw; a.L = c->tr.A; a.Xo = c->tr.B; a.Z = c->dZ; a.small = c->dsmall; a.abort_flag = c->dinfo;
+  a.xw = c->dXw; a.L = c->tr.A; a.Xo = c->tr.B; a.Z = c->dZ; a.small = c->hpin; a.abort_flag = c->dinfo + 1 + TINY_SYNC_INTS;
+  a.K = c->tr.A; a.Xp = c->dtiny; a.Wg = c->dtiny + 36 * DB_BS; a.part = a.Wg + TILE * 32; a.sync = c->dinfo + 1;
   a.n = (int)c->n; a.d = d; a.P = P; a.want_grad = want_grad ? 1 : 0; a.mucm = gp4ml ? 0 : 1;
+  a.ek = ++c->tiny_ek;
+  a.eg = want_grad ? ++c->tiny_eg : c->tiny_eg;
   a.s2 = s2; a.rscale = rscale;
   kernel_consts(kernel, nu, true, &a.coff, &a.cdiag);
   const size_t lds = (G_LDS_LAUNCH_DOUBLES + 2 * TILE * TINY_ZP) * sizeof(double);
-  if (d <= 4) hipLaunchKernelGGL(k_tiny<4>, dim3(1), dim3(256), lds, c->stream, a);
-  else if (d <= 8) hipLaunchKernelGGL(k_tiny<8>, dim3(1), dim3(256), lds, c->stream, a);
-  else if (d <= 12) hipLaunchKernelGGL(k_tiny<12>, dim3(1), dim3(256), lds, c->stream, a);
-  else if (d <= 16) hipLaunchKernelGGL(k_tiny<16>, dim3(1), dim3(256), lds, c->stream, a);
-  else hipLaunchKernelGGL(k_tiny<32>, dim3(1), dim3(256), lds, c->stream, a);
+  c->tiny_dirty = true;   // (until this call has ended cleanly: its sync words are then consistent)
+  if (d <= 4) hipLaunchKernelGGL(k_tiny<4>, dim3(1 + TINY_NH), dim3(256), lds, c->stream, a);
+  else if (d <= 8) hipLaunchKernelGGL(k_tiny<8>, dim3(1 + TINY_NH), dim3(256), lds, c->stream, a);
+  else if (d <= 12) hipLaunchKernelGGL(k_tiny<12>, dim3(1 + TINY_NH), dim3(256), lds, c->stream, a);
+  else if (d <= 16) hipLaunchKernelGGL(k_tiny<16>, dim3(1 + TINY_NH), dim3(256), lds, c->stream, a);
+  else hipLaunchKernelGGL(k_tiny<32>, dim3(1 + TINY_NH), dim3(256), lds, c->stream, a);
   HIPCHK(c, hipGetLastError());
-  const size_t ns = (size_t)P * P + 2 + (want_grad ? d + 4 : 0);   // Gram, log|L|, column, sums, Q flag
-  HIPCHK(c, hipMemcpyAsync(c->hpin, c->dsmall, ns * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));   // (the kernel wrote its outputs to hpin)
   const int info = (int)c->hpin[P * P + 1];
   if (info != 0) {
     c->err = "matrix not positive definite (pivot " + std::to_string(info) + ")";
@@ -1785,6 +1797,7 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
     for (int i = 0; i < 8; ++i) c->phase_ms[i] = 0.0;
     c->phase_ms[6] = ms;
   }
+  c->tiny_dirty = false;
   return GPE_OK;
 }
 

@@ -33,15 +33,15 @@ constexpr int TINY_DM = 32;   // basis columns held per row
 // doubles put 32 or 64 lanes of a wave on one bank: ~100 us per launch in a first version)
 constexpr int TINY_ZP = TINY_DM + 1;
 template <int DM> struct TinyPitch { static constexpr int v = DM + 1; };
-// the q x q algebra in zs once Z is consumed: Gram (P x P), a flag, u, T2 ([k][p], pitch
-// TINY_ZP)
-constexpr int TY_G = 0, TY_QD = 2048, TY_B = 2080, TY_T2 = 2112;
+// the q x q algebra in zs once Z is consumed: Gram (P x P), Q's Cholesky (q x q, pitch 32),
+// its diagonal, u, T2 ([k][p], pitch TINY_ZP)
+constexpr int TY_G = 0, TY_Q = 1024, TY_QD = 2048, TY_B = 2080, TY_T2 = 2112;
 static_assert(TY_T2 + TINY_DM * TINY_ZP <= 128 * TINY_ZP, "algebra fits in zs");
 
 // dev-tool phase clocks (tools/hip/tiny_bench.hip): -DTINY_TIMING
 #ifdef TINY_TIMING
-__device__ unsigned long long tiny_tsc[12];
-#define TINY_T(s) do { __syncthreads(); if (threadIdx.x == 0) tiny_tsc[s] = wall_clock64(); } while (0)
+__device__ unsigned long long tiny_tsc[12], tiny_clk[12];   // 100 MHz wall clock, shader clock
+#define TINY_T(s) do { __syncthreads(); if (threadIdx.x == 0) { tiny_tsc[s] = wall_clock64(); tiny_clk[s] = clock64(); } } while (0)
 #else
 #define TINY_T(s) do {} while (0)
 #endif
@@ -55,12 +55,72 @@ struct TinyArgs {
   double* L;            // out: L (ld 128)
   double* Xo;           // out: X = L^-1 (ld 128, zero upper)
   double* Z;            // out: Z = L^-1 [f H] (ld 128, P columns)
-  double* small;        // out: Gram (P x P) | log|L| | failed column | d + 3 sums | Q not PD
-  int* abort_flag;      // set to the failed column as the general path's Cholesky does
+  double* small;        // out (pinned host memory): Gram (P x P) | log|L| | failed column |
+                        // d + 3 sums | Q not PD
+  double* K;            // the helpers' K-build in the block-packed image's layout; L's buffer
+  double* Xp;           // X's LDS image (block-packed, 36 x DB_BS doubles)
+  double* Wg;           // W for the helpers (128 x 32, row-major)
+  double* part;         // the helpers' partial sums (TINY_NH x 64)
+  int* sync;            // [0] K-build count, [1] X flag, [2] W flag, [3] ticket: monotone
+                        // over the context's calls (zeroed after a failed one)
+  int* abort_flag;      // the failed column (or 1: Q not positive definite); zero on entry
+  int ek, eg;           // this call's ordinal among all calls / gradient calls since the zeroing
   int n, d, P, want_grad, mucm;
   double s2, coff, cdiag, rscale;
   double invd[32];
 };
+
+constexpr int TINY_NH = 9;
+constexpr int TINY_SYNC_INTS = 4;
+
+// Hand-offs between the workgroups of one k_tiny launch without agent fences (each a
+// write-back or invalidate of ~1.7-6.5 us on the chain, three of them in a row before): every
+// handed-off byte stored and loaded `sc1` (global_store/load ... sc1: L2, not L1), every
+// storing wave's vmcnt(0) wait and the workgroup's barrier before ONE lane's counter add or
+// sc1 flag store; the consumer polls sc1, then a barrier before its loads (the MI355X
+// guide's measured sc1 hand-off form, one workgroup per CU).
+typedef __attribute__((address_space(1))) double tiny_gdouble;
+typedef __attribute__((address_space(1))) int tiny_gint;
+__device__ __forceinline__ void tiny_st(double* p, double v) {
+  __hip_atomic_store((tiny_gdouble*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double tiny_ld(const double* p) {
+  return __hip_atomic_load((tiny_gdouble*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int tiny_ldi(const int* p) {
+  return __hip_atomic_load((tiny_gint*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// every wave's stores landed, then one lane signals (add 1, or store v when v > 0)
+__device__ __forceinline__ void tiny_signal(int* p, int v) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (v > 0) __hip_atomic_store((tiny_gint*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_fetch_add((tiny_gint*)p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// one lane polls until *p >= want (1) or the launch aborted (2); 0 after ~1 s (never
+// expected); the result in *st for every thread after the barrier
+__device__ __forceinline__ int tiny_wait(const int* p, int want, const int* abort_flag, int* st) {
+  if (threadIdx.x == 0) {
+    int v = 0;
+    for (long it = 0; it < (1l << 22); ++it) {
+      if (tiny_ldi(p) >= want) { v = 1; break; }
+      if (abort_flag && tiny_ldi(abort_flag)) { v = 2; break; }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    *st = v;
+  }
+  __syncthreads();
+  const int v = *st;
+  __syncthreads();
+  return v;
+}
+__host__ __device__ constexpr int tiny_tri_row(int b) {   // row of lower-triangle entry b
+  int r = 0;
+  while ((r + 1) * (r + 2) / 2 <= b) ++r;
+  return r;
+}   // helper workgroups: 4 waves each, one lower 16 x 16 block per wave
 
 // N pieces per thread (index threadIdx.x + 256 u): every load, then every store
 template <int N, class Ld, class St>
@@ -128,79 +188,192 @@ __device__ __forceinline__ double tiny_dot(double s, const double* a, int sa, co
   return s;
 }
 
+// s -= sum_{k < k1} x[k]^2 and t -= sum_{k < k1} y[k] x[k] together (two chains in flight)
+__device__ __forceinline__ void tiny_dot2(double& s, double& t, const double* x, const double* y, int k1) {
+  for (int c = 0; c < k1; c += 8) {
+    double xv[8], yv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      xv[u] = x[c + u];
+      yv[u] = y[c + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool in = c + u < k1;
+      const double xm = in ? xv[u] : 0.0;
+      s = fma(-xm, xm, s);
+      t = fma(-(in ? yv[u] : 0.0), xm, t);
+    }
+  }
+}
+
 typedef double tiny_d4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ tiny_d4 tiny_mfma(double a, double b, tiny_d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+// A helper workgroup (blockIdx 1 .. TINY_NH): wave w of helper h owns lower block b = 4h + w
+// = (bi, bj) of the 16 x 16 grid.  First its 256 entries of the K-build (k_pairs' training
+// mode, in the MFMA accumulator layout: lane -> rows 16 bi + lane / 16 + 4 r, column
+// 16 bj + lane % 16), written to K and their exp(-s) kept; then, once workgroup 0 has
+// published W, M(bi, bj) = X^T X - W W^T (MFMA, X and W from L2) contracted into the d + 3
+// sums; the last helper to finish adds the nine partials in helper order.
+template <int DM>
+__device__ void tiny_helper(const TinyArgs& a, double* lds) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = blockIdx.x - 1;
+  const int m16 = lane & 15, k4 = lane >> 4;
+  const int n = a.n, d = a.d, P = a.P;
+  int bi = 0;
+  const int b = 4 * h + wave;
+  while ((bi + 1) * (bi + 2) / 2 <= b) ++bi;
+  const int bj = b - bi * (bi + 1) / 2;
+  const int j = 16 * bj + m16;
+  auto coord = [&](int i, int k) { return (k < d && i < n) ? a.X[i * d + k] * a.invd[k] : 0.0; };
+  double xj[DM];
+#pragma unroll
+  for (int k = 0; k < DM; ++k) xj[k] = coord(j, k);
+  double xi[4][DM];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int k = 0; k < DM; ++k) xi[r][k] = coord(16 * bi + k4 + 4 * r, k);
+  double ex[4];
+  {
+    const double pre = a.s2 * a.coff;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 16 * bi + k4 + 4 * r;
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < DM; ++k) {
+        const double df = xi[r][k] - xj[k];
+        s = fma(df, df, s);
+      }
+      ex[r] = exp(-s);
+      double v = pre * ex[r];
+      const bool pad = i >= n || j >= n;
+      const bool diag = i == j;
+      double vd = a.s2 * a.cdiag;
+      if (a.r && i < n) vd += a.rscale * a.r[i];
+      v = pad ? (diag ? 1.0 : 0.0) : (diag ? vd : v);
+      if (i >= j) tiny_st(a.K + db_blk(bi, bj) + db_e(i & 15, m16), v);
+    }
+  }
+  tiny_signal(&a.sync[0], 0);
+  if (!a.want_grad) return;
+  int* st = reinterpret_cast<int*>(lds);
+  // M(bi, bj) = X^T X (as soon as workgroup 0 has published X) - W W^T (once W is out)
+  if (tiny_wait(&a.sync[1], a.eg, a.abort_flag, st) != 1) return;
+  tiny_d4 acc = {0.0, 0.0, 0.0, 0.0};
+  {
+    double av[8][4], bv[8][4];   // X's blocks (kb, bi) and (kb, bj): 4 operands per lane each
+#pragma unroll
+    for (int kb = 0; kb < 8; ++kb)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        // X(16 kb + k, 16 bi + m) (zero above the diagonal of a diagonal block)
+        const int k = 4 * s + k4;
+        av[kb][s] = (kb >= bi && !(kb == bi && k < m16)) ? tiny_ld(a.Xp + db_blk(kb, bi) + db_e(k, m16)) : 0.0;
+        bv[kb][s] = (kb >= bi && !(kb == bj && k < m16)) ? tiny_ld(a.Xp + db_blk(kb, bj) + db_e(k, m16)) : 0.0;
+      }
+#pragma unroll
+    for (int kb = 0; kb < 8; ++kb)
+      if (kb >= bi)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = tiny_mfma(av[kb][s], bv[kb][s], acc);
+  }
+  if (tiny_wait(&a.sync[2], a.eg, a.abort_flag, st) != 1) return;   // (aborted: Q failed)
+  {
+    const int ks = (P + 3) >> 2;
+    double av[8], bv[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      av[s] = s < ks ? -tiny_ld(a.Wg + (16 * bi + m16) * 32 + 4 * s + k4) : 0.0;
+      bv[s] = s < ks ? tiny_ld(a.Wg + (16 * bj + m16) * 32 + 4 * s + k4) : 0.0;
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      if (s < ks) acc = tiny_mfma(av[s], bv[s], acc);
+  }
+  TinySums<DM> sm;
+  sm.zero();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = 16 * bi + k4 + 4 * r;
+    const bool ok = i < n && j < n && i >= j;
+    const double m = ok ? acc[r] : 0.0;
+    const bool dg = i == j;
+    double df2[DM];
+#pragma unroll
+    for (int k = 0; k < DM; ++k) {
+      const double df = xi[r][k] - xj[k];
+      df2[k] = df * df;
+    }
+    sm.t += dg ? m : 0.0;
+    sm.r += (dg && ok && a.rdiag) ? m * a.rdiag[i] : 0.0;
+    const double me = dg ? 0.0 : m * ex[r];
+    sm.e += me;
+#pragma unroll
+    for (int k = 0; k < DM; ++k) sm.acc[k] = fma(me, df2[k], sm.acc[k]);
+  }
+  double* red = lds + 8;   // (past st)
+  sm.reduce(d, red, red + 4 * (DM + 3));
+  if (tid < d + 3) tiny_st(a.part + h * 64 + tid, red[4 * (DM + 3) + tid]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add((tiny_gint*)&a.sync[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *st = old == TINY_NH * a.eg - 1;
+  }
+  __syncthreads();
+  if (*st && tid < d + 3) {   // the last helper: the nine partials in helper order
+    double v = 0.0;
+    for (int g = 0; g < TINY_NH; ++g) v += tiny_ld(a.part + g * 64 + tid);
+    a.small[P * P + 2 + tid] = v;
+  }
+#ifdef TINY_TIMING
+  if (*st && tid == 0) tiny_tsc[7] = wall_clock64();
+#endif
+}
+
 template <int DM>
 static __global__ void __launch_bounds__(256) k_tiny(TinyArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  constexpr int XP = TinyPitch<DM>::v, ZP = TINY_ZP;
+  if (blockIdx.x > 0) {
+    tiny_helper<DM>(a, lds);
+    return;
+  }
+  constexpr int ZP = TINY_ZP;
   double* lb = lds;                              // db_factor_invert's image + extras
-  double* r1 = lds + G_LDS_LAUNCH_DOUBLES;       // 128 x ZP: scaled points, [f H], Y, W
-  double* zs = r1 + TILE * ZP;                   // 128 x ZP: Z, the q x q algebra, scaled points
+  double* r1 = lds + G_LDS_LAUNCH_DOUBLES;       // 128 x ZP: [f H], Y, W
+  double* zs = r1 + TILE * ZP;                   // 128 x ZP: Z, the q x q algebra
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int m16 = lane & 15, k4 = lane >> 4;     // MFMA operand lane -> (row m16, k k4)
   const int n = a.n, d = a.d, P = a.P, q = P - 1;
   const int npb = (P + 15) >> 4;                 // 16-column blocks of [f H]
   TINY_T(0);
-  auto xw_ld = [&](int e) {   // scaled coordinate e = i DM + k (k_scale_points' product)
+  // the scaled points (k_scale_points' product) for the later calls, while the helpers
+  // build K
+  tiny_stage<TILE * DM / 256>([&](int e) {
     const int i = e / DM, k = e - i * DM;
     return (k < d && i < n) ? a.X[i * d + k] * a.invd[k] : 0.0;
-  };
-  tiny_stage<TILE * DM / 256>(xw_ld, [&](int e, double v) {
+  }, [&](int e, double v) {
     const int i = e / DM, k = e - i * DM;
-    r1[i * XP + k] = v;
     if (k < d) a.xw[i * d + k] = v;
   });
-  __syncthreads();
   TINY_T(1);
-  // K-build of the lower half into the block-packed image (k_pairs' training mode): lane
-  // rows ra = lane and rb = 127 - lane, wave g their columns c = g (mod 4) -- 32 or 33
-  // entries per lane, KU at a time (their exp chains overlap)
   {
-    const int ra = lane, rb = 127 - lane, g = wave;
-    double xa[DM], xb[DM];
-#pragma unroll
-    for (int k = 0; k < DM; ++k) {
-      xa[k] = r1[ra * XP + k];
-      xb[k] = r1[rb * XP + k];
-    }
-    const double pre = a.s2 * a.coff;
-    double va = a.s2 * a.cdiag, vb = va;
-    if (a.r && ra < n) va += a.rscale * a.r[ra];
-    if (a.r && rb < n) vb += a.rscale * a.r[rb];
-    const int na = ra >= g ? (ra - g) / 4 + 1 : 0;
-    const int tot = na + (rb - g) / 4 + 1;
-    constexpr int KU = DM <= 16 ? 4 : 2;
-    for (int it = 0; it < tot; it += KU) {
-      double s[KU];
-      int ii[KU], cc[KU];
-#pragma unroll
-      for (int u = 0; u < KU; ++u) {
-        const int t = min(it + u, tot - 1);
-        const bool inA = t < na;
-        ii[u] = inA ? ra : rb;
-        cc[u] = g + 4 * (inA ? t : t - na);
-        s[u] = 0.0;
-#pragma unroll
-        for (int k = 0; k < DM; ++k) {
-          const double df = (inA ? xa[k] : xb[k]) - r1[cc[u] * XP + k];
-          s[u] = fma(df, df, s[u]);
-        }
+    if (tiny_wait(&a.sync[0], TINY_NH * a.ek, nullptr, reinterpret_cast<int*>(r1)) != 1) {   // (never expected)
+      if (tid == 0) {
+        a.small[P * P + 1] = -1.0;
+        if (a.abort_flag) atomicCAS(a.abort_flag, 0, GEMM_WAIT_TIMEOUT);
       }
-#pragma unroll
-      for (int u = 0; u < KU; ++u) {
-        const int i = ii[u], c = cc[u];
-        double v = pre * exp(-s[u]);
-        const bool pad = i >= n || c >= n;
-        const bool diag = i == c;
-        v = pad ? (diag ? 1.0 : 0.0) : (diag ? (i == ra ? va : vb) : v);
-        if (it + u < tot) lb[db_off(i, c)] = v;
-      }
+      return;
     }
   }
+  // the helpers' image of K's lower half (the diagonal blocks' upper entries unused)
+  tiny_stage<36 * DB_BS / 256 + 1>([&](int e) { return e < 36 * DB_BS ? tiny_ld(a.K + e) : 0.0; },
+                                   [&](int e, double v) { if (e < 36 * DB_BS) lb[e] = v; });
   __syncthreads();
   TINY_T(2);
   const int bad = db_factor_invert(lb, a.L, TILE, a.Xo, TILE, a.small + P * P, [] {}, true);
@@ -210,6 +383,11 @@ static __global__ void __launch_bounds__(256) k_tiny(TinyArgs a) {
       if (a.abort_flag) atomicCAS(a.abort_flag, 0, bad);
     }
     return;
+  }
+  if (a.want_grad) {   // X's image for the helpers
+    __syncthreads();   // (the assembled image complete)
+    for (int e = tid; e < 36 * DB_BS; e += 256) tiny_st(a.Xp + e, lb[e]);
+    tiny_signal(&a.sync[1], a.eg);
   }
   TINY_T(3);
   // [f H] -> r1 ([i][p], pitch ZP; columns P .. 16 npb zero)
@@ -293,6 +471,7 @@ static __global__ void __launch_bounds__(256) k_tiny(TinyArgs a) {
   __syncthreads();   // Z consumed: zs takes the algebra
   TINY_T(8);
   double* G = zs + TY_G;
+  double* Qa = zs + TY_Q;
   double* Qd = zs + TY_QD;
   double* bt = zs + TY_B;
   double* t2 = zs + TY_T2;
@@ -308,64 +487,42 @@ static __global__ void __launch_bounds__(256) k_tiny(TinyArgs a) {
   }
   for (int e = tid; e < TINY_DM * ZP; e += 256) t2[e] = 0.0;
   __syncthreads();
-  // The q x q algebra on wave 0, lane i < q holding row i of Q in registers (every loop
-  // over columns unrolled to 32, skipped past q): the Cholesky right-looking (each entry's
-  // terms in small_chol's order), u = Kq^-1 wz and the rows of Kq^-1 (small_fwd's and
-  // small_trinv's order of terms), the column entries passed by shuffles.  Kq^-1 goes to
-  // T2(c + 1, 1 + i) = Kq^-1(i, c), u to bt; then beta = Kq^-T u and quad = zz - |u|^2
-  // (= zz - wz^T Q^-1 wz) below.
-  if (wave == 0) {
-    const int i = lane;
-    double qr[32];
-#pragma unroll
-    for (int k = 0; k < 32; ++k) qr[k] = (i < q && k < q) ? G[(i + 1) * P + k + 1] : 0.0;
-    bool okq = true;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      if (j < q && okq) {
-        const double piv = __shfl(qr[j], j, 64);
-        if (!(piv > 0.0)) okq = false;   // (uniform over the wave)
-        const double dj = sqrt(piv);
-        const double l = i == j ? dj : (i > j ? qr[j] / dj : 0.0);
-        qr[j] = l;
-#pragma unroll
-        for (int k = j + 1; k < 32; ++k)
-          if (k < q) qr[k] = fma(-l, __shfl(l, k, 64), qr[k]);   // (entries k > i: unused)
-      }
-    }
-    double acc = (i < q) ? G[(i + 1) * P] : 0.0, uval = 0.0;
-    double xr[32];
-#pragma unroll
-    for (int c = 0; c < 32; ++c) xr[c] = i == c ? 1.0 : 0.0;
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      if (k < q && okq) {
-        const double dk = __shfl(qr[k], k, 64);   // L(k, k)
-        const double uk = __shfl(acc / dk, k, 64);
-        uval = i == k ? uk : uval;
-        acc = fma(-qr[k], uk, acc);
-#pragma unroll
-        for (int c = 0; c <= k; ++c) {
-          if (i == k) xr[c] = xr[c] / dk;
-          const double xkc = __shfl(xr[c], k, 64);
-          if (i > k) xr[c] = fma(-qr[k], xkc, xr[c]);
-        }
-      }
-    }
-    if (i < q) {
-      bt[i] = uval;
-#pragma unroll
-      for (int c = 0; c < 32; ++c)
-        if (c <= i) t2[(c + 1) * ZP + 1 + i] = xr[c];
-    }
-    if (lane == 0) Qd[0] = okq ? 0.0 : 1.0;
+  for (int e = tid; e < 32 * 32; e += 256) {   // Q = G[1:, 1:] (pitch 32)
+    const int i = e >> 5, k = e & 31;
+    Qa[e] = (i < q && k < q) ? G[(i + 1) * P + k + 1] : 0.0;
   }
   __syncthreads();
-  if (Qd[0] != 0.0) {   // (uniform) H^T A^-1 H not positive definite
-    if (tid == 0) a.small[P * P + 2 + d + 3] = 1.0;
-    return;
+  // Cholesky of Q (small_chol's order of terms): column j by the threads of its rows, the
+  // pivot by every thread
+  for (int j = 0; j < q; ++j) {
+    // the pivot's sum (every thread) and row tid's (threads j < tid < q) in one pass
+    const int ti = (tid > j && tid < q) ? tid : j;
+    double s = Qa[j * 32 + j], t = Qa[ti * 32 + j];
+    tiny_dot2(s, t, Qa + j * 32, Qa + ti * 32, j);
+    if (!(s > 0.0)) {   // (uniform) H^T A^-1 H not positive definite
+      if (tid == 0) {
+        a.small[P * P + 2 + d + 3] = 1.0;
+        __hip_atomic_store((tiny_gint*)a.abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // helpers stop
+      }
+      return;
+    }
+    const double dj = sqrt(s);
+    if (tid > j && tid < q) Qa[tid * 32 + j] = t / dj;
+    if (tid == 0) Qd[j] = dj;
+    __syncthreads();
   }
   TINY_T(9);
+  // T2 = [[sqrt(c), 0], [-sqrt(c) beta, Kq^-T]] (small_t2): Kq^-1 one column per lane
+  // (small_trinv's forward substitution) into T2(c + 1, 1 + i) = Kq^-1(i, c); then
+  // u = Kq^-1 wz, beta = Kq^-T u and quad = zz - |u|^2 (= zz - wz^T Q^-1 wz)
+  if (tid < q) {
+    const int c = tid;
+    double* e = t2 + (c + 1) * ZP + 1;
+    for (int i = c; i < q; ++i) e[i] = tiny_dot(i == c ? 1.0 : 0.0, Qa + i * 32, 1, e, 1, c, i) / Qd[i];
+  }
+  __syncthreads();
+  if (tid < q) bt[tid] = -tiny_dot(0.0, t2 + 1 + tid + ZP, ZP, G + P, P, 0, tid + 1);   // u_i
+  __syncthreads();
   {
     const double quad = tiny_dot(G[0], bt, 1, bt, 1, 0, q);
     double cfac = 1.0;
@@ -402,72 +559,14 @@ static __global__ void __launch_bounds__(256) k_tiny(TinyArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) r1[(16 * (2 * wave + u) + k4 + 4 * r) * ZP + 16 * bp + m16] = wacc[u][bp][r];
   }
-  // the scaled points again (pitch XP) in zs
-  tiny_stage<TILE * DM / 256>(xw_ld, [&](int e, double v) { zs[(e / DM) * XP + e % DM] = v; });
-  __syncthreads();
-  TINY_T(6);
-  // M = X^T X - W W^T over the 36 lower 16 x 16 blocks (wave w: rows w and 7 - w, all
-  // their column blocks: 9 each), each entry (i >= j, both < n) contracted in place
-  constexpr int RI = DM <= 16 ? 4 : 1;   // entries contracted together (register budget)
-  TinySums<DM> sm;
-  sm.zero();
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int bi = u ? 7 - wave : wave;
-    if (16 * bi >= n) continue;
-    for (int bj = 0; bj <= bi; ++bj) {
-      if (16 * bj >= n) break;
-      tiny_d4 acc = {0.0, 0.0, 0.0, 0.0};
-      for (int kb = bi; kb < 8; ++kb) {
-        double av[4], bv[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          av[s] = xlo(kb, bi, 4 * s + k4, m16);
-          bv[s] = xlo(kb, bj, 4 * s + k4, m16);
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) acc = tiny_mfma(av[s], bv[s], acc);
-      }
-      for (int s = 0; s < ks; ++s)
-        acc = tiny_mfma(-r1[(16 * bi + m16) * ZP + 4 * s + k4], r1[(16 * bj + m16) * ZP + 4 * s + k4], acc);
-      const int j = 16 * bj + m16;
-      double xj[DM];
-#pragma unroll
-      for (int k = 0; k < DM; ++k) xj[k] = zs[j * XP + k];
-#pragma unroll
-      for (int r0 = 0; r0 < 4; r0 += RI) {
-        double df2[RI][DM], s[RI];
-#pragma unroll
-        for (int rr = 0; rr < RI; ++rr) {
-          const int i = 16 * bi + k4 + 4 * (r0 + rr);
-          s[rr] = 0.0;
-#pragma unroll
-          for (int k = 0; k < DM; ++k) {
-            const double df = zs[i * XP + k] - xj[k];
-            df2[rr][k] = df * df;
-            s[rr] += df2[rr][k];
-          }
-        }
-#pragma unroll
-        for (int rr = 0; rr < RI; ++rr) {
-          const int i = 16 * bi + k4 + 4 * (r0 + rr);
-          const bool ok = i < n && j < n && i >= j;
-          const double m = ok ? acc[r0 + rr] : 0.0;
-          const bool dg = i == j;
-          sm.t += dg ? m : 0.0;
-          sm.r += (dg && ok && a.rdiag) ? m * a.rdiag[i] : 0.0;
-          const double me = dg ? 0.0 : m * exp(-s[rr]);
-          sm.e += me;
-#pragma unroll
-          for (int k = 0; k < DM; ++k) sm.acc[k] = fma(me, df2[rr][k], sm.acc[k]);
-        }
-      }
-    }
+  // W to L2 for the helpers, then the flag
+  for (int e = tid; e < TILE * 32; e += 256) {
+    const int i = e >> 5, k = e & 31;
+    tiny_st(a.Wg + e, k < 16 * npb ? r1[i * ZP + k] : 0.0);
   }
-  __syncthreads();   // (red below reuses r1)
-  sm.reduce(d, r1, a.small + P * P + 2);
   if (tid == 0) a.small[P * P + 2 + d + 3] = 0.0;
-  TINY_T(7);
+  tiny_signal(&a.sync[2], a.eg);
+  TINY_T(6);
 }
 
 }  // namespace gpe
