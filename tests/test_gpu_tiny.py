@@ -132,3 +132,45 @@ def test_tiny_not_pd_then_usable(ctx):
     mean, var = ctx.posterior(xs, orc.linear_basis(xs), beta, hp[-1], full_var=True)
     m_ref, v_ref = orc.posterior_ref(X, f, H, A, xs, orc.linear_basis(xs), beta, hp[-1], hp[:2], hp[2], orc.STD)
     assert np.max(np.abs(mean - m_ref)) < 1e-8 and np.max(np.abs(var - v_ref)) < 1e-8
+
+
+def test_tiny_concurrent_contexts_and_big_neighbour():
+    """Three contexts on three threads, each with its own stream: two run n <= 128 objectives
+    (the one-launch path's cross-workgroup hand-offs then share the GPU with each other) and
+    one an n = 4096 objective beside them (uneven load); every result equals the same call
+    run alone, and the sync words stay consistent over 40 mixed gradient / value calls."""
+    import threading
+    probs = [orc.synthetic_problem(n, d, seed=s) for n, d, s in ((128, 10, 31), (77, 3, 32), (4096, 10, 33))]
+    hps = [np.concatenate([np.linspace(0.4, 0.8, d), [1e-3, 1.1]]) for d in (10, 3, 10)]
+    ctxs = [native.Context(0) for _ in range(3)]
+    th = []
+    try:
+        alone = []
+        for c, (X, f, H), hp in zip(ctxs, probs, hps):
+            c.set_data(X, f, H)
+            alone.append((c.objective(orc.GP4ML, orc.STD, hp), c.objective(orc.GP4ML, orc.STD, hp, want_grad=False)))
+        errors = []
+
+        def run(k):
+            try:
+                reps = 4 if k == 2 else 40
+                for it in range(reps):
+                    want = it % 3 != 2
+                    llh, g, s2 = ctxs[k].objective(orc.GP4ML, orc.STD, hps[k], want_grad=want)
+                    ref = alone[k][0] if want else alone[k][1]
+                    if llh != ref[0] or (want and not np.array_equal(g, ref[1])):
+                        errors.append((k, it, llh, ref[0]))
+            except Exception as e:   # noqa: BLE001 (reported below)
+                errors.append((k, repr(e)))
+
+        th = [threading.Thread(target=run, args=(k,)) for k in range(3)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert not any(t.is_alive() for t in th), "a context did not finish"
+        assert not errors, errors[:5]
+    finally:
+        for k, c in enumerate(ctxs):   # (a context still in use by its thread stays open)
+            if k >= len(th) or not th[k].is_alive():
+                c.close()
