@@ -193,6 +193,17 @@ __global__ void __launch_bounds__(256) k_dist_pack(const double* Aloc, long long
   }
 }
 
+// one 128 x 128 tile src (ld lds) -> dst (ld ldd): 16 workgroups of 8 columns, 16-byte
+// accesses (a hipMemcpy2DAsync of the same tile: 16 us per step on the chain)
+__global__ void __launch_bounds__(256) k_dist_tile(const double* src, long long lds, double* dst, long long ldd) {
+  const int c = blockIdx.x * 8 + (threadIdx.x >> 5), i = (threadIdx.x & 31) * 4;
+  const double2* s = reinterpret_cast<const double2*>(src + i + c * lds);
+  double2* o = reinterpret_cast<double2*>(dst + i + c * ldd);
+  const double2 a = s[0], b = s[1];
+  o[0] = a;
+  o[1] = b;
+}
+
 // gathered segment of rank r (blockIdx.y), tile t -> panel rows of global tile (li0_r + t) P + r
 __global__ void __launch_bounds__(256) k_dist_unpermute(const double* recv, long long seg,
                                                         const int* li0, const int* cnt, int P,
@@ -1222,10 +1233,11 @@ int step(gpe_dist* h, int k) {
   DCHK(launch(h, h->mrow[k]));
   if (gather_panels(h)) DCHK(coll_bcast(h, &Rank::dinv, 0, (size_t)TILE * (Kp + TILE), owner));
   if (h->grad_now) {
-    if (Rank* O = rank_slot(h, owner))
-      DCHK_HIP(h, hipMemcpy2DAsync(O->X + (long long)(k / P) * TILE + (long long)k * TILE * O->ld,
-                                   O->ld * sizeof(double), O->dinv + Kp * TILE, TILE * sizeof(double),
-                                   TILE * sizeof(double), TILE, hipMemcpyDeviceToDevice, h->cs));
+    if (Rank* O = rank_slot(h, owner)) {   // the diagonal tile of X = L^-1 (Dinv)
+      hipLaunchKernelGGL(k_dist_tile, dim3(TILE / 8), dim3(256), 0, h->cs, O->dinv + Kp * TILE, (long long)TILE,
+                         O->X + (long long)(k / P) * TILE + (long long)k * TILE * O->ld, (long long)O->ld);
+      DCHK_HIP(h, hipGetLastError());
+    }
   }
   return launch(h, h->panel_l[k]);
 }
