@@ -24,6 +24,7 @@
 #include "gpemu_kernels.hpp"
 #include "gpemu_small.hpp"
 #include "gpemu_tiny.hpp"
+#include "gpemu_snb.hpp"
 
 using namespace gpe;
 
@@ -145,6 +146,10 @@ struct gpe_ctx {
   double* dtiny = nullptr;   // n <= 128 path: X's image, W, the helpers' partials
   int tiny_ek = 0, tiny_eg = 0;   // k_tiny's call ordinals (its sync words in dinfo[1..4])
   bool tiny_dirty = true;         // zero dinfo[1..5] before the next k_tiny
+  double* dsnb = nullptr;         // 2-4 tiles (k_snb): X^T, [f H]^T, Z^T, W, T2, scratch, partials
+  long long snb_np = 0;
+  int snb_hc = 0, snb_mf = 0;   // k_snb's counters (dinfo[8..9]; abort dinfo[10])
+  bool snb_dirty = true;
   size_t small_cap = 0;
 
   // pinned host staging
@@ -1554,7 +1559,7 @@ gpe_ctx* gpe_create(int32_t device) {
     delete c;
     return nullptr;
   }
-  bool ok = dalloc(c, &c->dinfo, 8) == GPE_OK && dalloc(c, &c->dprobs, MAX_PROBS) == GPE_OK &&
+  bool ok = dalloc(c, &c->dinfo, 12) == GPE_OK && dalloc(c, &c->dprobs, MAX_PROBS) == GPE_OK &&
             ensure_shape_bufs(c, GPE_MAX_DIMS, GPE_MAX_COLS) == GPE_OK;
   for (int i = 0; i < 16 && ok; ++i) ok = hipEventCreate(&c->ev[i]) == hipSuccess;
   if (ok) {
@@ -1576,7 +1581,12 @@ gpe_ctx* gpe_create(int32_t device) {
          hipFuncSetAttribute((const void*)k_tiny<8>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess &&
          hipFuncSetAttribute((const void*)k_tiny<12>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess &&
          hipFuncSetAttribute((const void*)k_tiny<16>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess &&
-         hipFuncSetAttribute((const void*)k_tiny<32>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess;
+         hipFuncSetAttribute((const void*)k_tiny<32>, hipFuncAttributeMaxDynamicSharedMemorySize, tl) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_snb<4>, hipFuncAttributeMaxDynamicSharedMemorySize, SNB_LDS_DOUBLES * 8) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_snb<8>, hipFuncAttributeMaxDynamicSharedMemorySize, SNB_LDS_DOUBLES * 8) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_snb<12>, hipFuncAttributeMaxDynamicSharedMemorySize, SNB_LDS_DOUBLES * 8) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_snb<16>, hipFuncAttributeMaxDynamicSharedMemorySize, SNB_LDS_DOUBLES * 8) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k_snb<32>, hipFuncAttributeMaxDynamicSharedMemorySize, SNB_LDS_DOUBLES * 8) == hipSuccess;
     if (!ok) c->err = "hipFuncSetAttribute(max dynamic LDS) failed";
   }
   if (!ok) {
@@ -1595,7 +1605,7 @@ void gpe_destroy(gpe_ctx* c) {
                     c->dX, c->dXw, c->dF, c->dr, c->tr.A, c->tr.B, c->tr.logdet, c->aux.A, c->aux.B,
                     c->aux.logdet, c->dinvdelta, c->dZ,
                     c->dR2, c->dWa, c->dskp, c->dgpart, c->dgram, c->dT2, c->dcpart, c->dcsum,
-                    c->dW1, c->dW2, c->dW3, c->dXs, c->dXsw, c->dsmall, c->dtiny, c->dRn, c->dNU,
+                    c->dW1, c->dW2, c->dW3, c->dXs, c->dXsw, c->dsmall, c->dtiny, c->dsnb, c->dRn, c->dNU,
                     c->dVall, c->dXall, c->dTall};
   for (double* b : bufs)
     if (b) hipFree(b);
@@ -1724,9 +1734,9 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
   c->zaug_valid = false;
   c->tr.xdone = false;
   HIPCHK(c, hipStreamSynchronize(c->stream2));   // (a failed sweep's leftovers, as factor_and_invert)
-  constexpr size_t tiny_doubles = 36 * DB_BS + TILE * 32 + TINY_NH * 64;
+  constexpr size_t tiny_doubles = 36 * DB_BS + TILE * 32;
   if (!c->dtiny) CHK(dalloc(c, &c->dtiny, tiny_doubles));
-  CHK(ensure_pinned(c, (size_t)P * P + 2 * d + 64));
+  CHK(ensure_pinned(c, (size_t)P * P + 2 * d + 64 + TINY_NH * 64));
   if (c->tiny_dirty || c->tiny_ek > (1 << 26)) {   // the sync words and the abort flag
     HIPCHK(c, hipMemsetAsync(c->dinfo + 1, 0, (TINY_SYNC_INTS + 1) * sizeof(int), c->stream));
     c->tiny_ek = c->tiny_eg = 0;
@@ -1737,7 +1747,7 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
   a.r = (c->has_r && rscale != 0.0) ? c->dr : nullptr;
   a.rdiag = (gp4ml && kernel == GPE_KERNEL_STD && c->has_r) ? c->dr : nullptr;
   a.xw = c->dXw; a.L = c->tr.A; a.Xo = c->tr.B; a.Z = c->dZ; a.small = c->hpin; a.abort_flag = c->dinfo + 1 + TINY_SYNC_INTS;
-  a.K = c->tr.A; a.Xp = c->dtiny; a.Wg = c->dtiny + 36 * DB_BS; a.part = a.Wg + TILE * 32; a.sync = c->dinfo + 1;
+  a.K = c->tr.A; a.Xp = c->dtiny; a.Wg = c->dtiny + 36 * DB_BS; a.sync = c->dinfo + 1;
   a.n = (int)c->n; a.d = d; a.P = P; a.want_grad = want_grad ? 1 : 0; a.mucm = gp4ml ? 0 : 1;
   a.ek = ++c->tiny_ek;
   a.eg = want_grad ? ++c->tiny_eg : c->tiny_eg;
@@ -1786,8 +1796,15 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
       return GPE_NOT_PD;
     }
     (void)cfac;   // (the device's T2 carries sqrt(cfac))
-    small_grad(c->hpin + (size_t)P * P + 2, d, kernel == GPE_KERNEL_ALT_NUG, nu, fitnug, gp4ml, gscale, s2, a.coff,
-               a.cdiag, n_hp, grad_out, a.rdiag != nullptr);
+    double red[TINY_DM + 3];
+    const double* part = c->hpin + (size_t)P * P + 2 + d + 4;
+    for (int k = 0; k < d + 3; ++k) {   // the helpers' partials in helper order
+      double v = 0.0;
+      for (int h = 0; h < TINY_NH; ++h) v += part[h * 64 + k];
+      red[k] = v;
+    }
+    small_grad(red, d, kernel == GPE_KERNEL_ALT_NUG, nu, fitnug, gp4ml, gscale, s2, a.coff, a.cdiag, n_hp,
+               grad_out, a.rdiag != nullptr);
   }
   if (c->prof) {   // (one phase: the whole evaluation)
     ev_rec(c, 7);
@@ -1798,6 +1815,118 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
     c->phase_ms[6] = ms;
   }
   c->tiny_dirty = false;
+  return GPE_OK;
+}
+
+// The objective of 2-4 tiles (128 < n <= 512, gpemu_snb.hpp): ONE launch of k_snb
+// (workgroup 0: the diagonal factors, the Gram and the q x q algebra; 32 helper workgroups:
+// K-build, panels and updates with [f H]^T as an augmented row, X = L^-1, W and the
+// contraction), outputs straight into the pinned host buffer; the host's small_from_gram /
+// small_grad as in tiny_objective.
+int snb_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_hp, bool fitnug, double nu,
+                  double s2, double rscale, bool want_grad, double* llh_out, double* grad_out, double* sigma2_out) {
+  const int d = c->d, q = c->q, P = q + 1, NB = c->NB;
+  const long long np = c->n_pad;
+  SnbArgs a;
+  for (int k = 0; k < d; ++k) {
+    if (!(hp[k] > 0.0) && !(hp[k] < 0.0))
+      return fail(c, GPE_NOT_PD, "length scale delta[" + std::to_string(k) + "] is zero or NaN");
+    a.invd[k] = 1.0 / hp[k];
+  }
+  for (int k = d; k < TINY_DM; ++k) a.invd[k] = 0.0;
+  c->linv_valid = false;
+  c->zaug_valid = false;
+  c->tr.xdone = false;
+  HIPCHK(c, hipStreamSynchronize(c->stream2));
+  if (c->snb_np != np) {
+    c->snb_np = 0;
+    CHK(dalloc(c, &c->dsnb, (size_t)np * np + 3 * 32 * (size_t)np + TINY_DM * TINY_ZP + TILE * TILE));
+    c->snb_np = np;
+  }
+  CHK(ensure_pinned(c, (size_t)P * P + NB + 2 * d + 64 + SNB_NH * 64));
+  if (c->snb_dirty || c->snb_hc > (1 << 24)) {
+    HIPCHK(c, hipMemsetAsync(c->dinfo + 8, 0, (SNB_SYNC_INTS + 1) * sizeof(int), c->stream));
+    c->snb_hc = c->snb_mf = 0;
+    c->snb_dirty = false;
+  }
+  ev_rec(c, 0);
+  a.X = c->dX; a.F = c->dF;
+  a.r = (c->has_r && rscale != 0.0) ? c->dr : nullptr;
+  a.rdiag = (gp4ml && kernel == GPE_KERNEL_STD && c->has_r) ? c->dr : nullptr;
+  a.xw = c->dXw; a.A = c->tr.A; a.Lb = c->tr.B; a.Xt = c->dsnb;
+  a.Zt = a.Xt + np * np; a.Zo = a.Zt + 32 * np; a.Wg = a.Zo + 32 * np; a.T2g = a.Wg + 32 * np;
+  a.Xscr = a.T2g + TINY_DM * TINY_ZP;
+  a.small = c->hpin; a.sync = c->dinfo + 8; a.abort_flag = c->dinfo + 8 + SNB_SYNC_INTS;
+  a.n = (int)c->n; a.np = (int)np; a.NB = NB; a.d = d; a.P = P; a.want_grad = want_grad ? 1 : 0;
+  a.mucm = gp4ml ? 0 : 1;
+  a.hcb = c->snb_hc; a.mfb = c->snb_mf;
+  a.s2 = s2; a.rscale = rscale;
+  kernel_consts(kernel, nu, true, &a.coff, &a.cdiag);
+  const size_t lds = SNB_LDS_DOUBLES * sizeof(double);
+  c->snb_dirty = true;   // (until this call has ended cleanly)
+  const dim3 grid(1 + SNB_NH);
+  if (d <= 4) hipLaunchKernelGGL(k_snb<4>, grid, dim3(256), lds, c->stream, a);
+  else if (d <= 8) hipLaunchKernelGGL(k_snb<8>, grid, dim3(256), lds, c->stream, a);
+  else if (d <= 12) hipLaunchKernelGGL(k_snb<12>, grid, dim3(256), lds, c->stream, a);
+  else if (d <= 16) hipLaunchKernelGGL(k_snb<16>, grid, dim3(256), lds, c->stream, a);
+  else hipLaunchKernelGGL(k_snb<32>, grid, dim3(256), lds, c->stream, a);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));   // (the kernel wrote its outputs to hpin)
+  const double* h = c->hpin;
+  const int info = (int)h[P * P + NB];
+  if (info != 0) {
+    c->err = info < 0 ? std::string("k_snb: a workgroup wait timed out")
+                      : "matrix not positive definite (pivot " + std::to_string(info) + ")";
+    return info < 0 ? GPE_ERR_HIP : GPE_NOT_PD;
+  }
+  double logdetA = 0.0;
+  for (int k = 0; k < NB; ++k) logdetA += h[P * P + k];
+  logdetA *= 2.0;
+  std::vector<double> G(h, h + (size_t)P * P);
+  SmallAlgebra sa = small_from_gram(G, P);
+  if (!sa.ok) {
+    c->err = "H^T A^-1 H not positive definite";
+    return GPE_NOT_PD;
+  }
+  const double n = (double)c->n;
+  double llh, sig2, gscale;
+  if (gp4ml) {
+    llh = 0.5 * (sa.quad + logdetA + sa.logdetQ + (n - q) * std::log(2.0 * M_PI));
+    sig2 = s2;
+    gscale = s2;
+  } else {
+    sig2 = sa.quad / (n - q - 2.0);
+    llh = 0.5 * ((n - q) * std::log(sig2) + logdetA + sa.logdetQ);
+    gscale = sig2;
+  }
+  *llh_out = llh;
+  if (sigma2_out) *sigma2_out = sig2;
+  if (want_grad) {
+    if (h[P * P + NB + 1 + d + 3] != 0.0) {
+      c->err = "H^T A^-1 H not positive definite";
+      return GPE_NOT_PD;
+    }
+    double red[TINY_DM + 3];
+    const double* part = h + (size_t)P * P + NB + 1 + d + 4;
+    for (int k = 0; k < d + 3; ++k) {   // the helpers' partials in helper order
+      double v = 0.0;
+      for (int g = 0; g < SNB_NH; ++g) v += part[g * 64 + k];
+      red[k] = v;
+    }
+    small_grad(red, d, kernel == GPE_KERNEL_ALT_NUG, nu, fitnug, gp4ml, gscale, s2, a.coff, a.cdiag, n_hp,
+               grad_out, a.rdiag != nullptr);
+  }
+  if (c->prof) {
+    ev_rec(c, 7);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[7]);
+    for (int i = 0; i < 8; ++i) c->phase_ms[i] = 0.0;
+    c->phase_ms[6] = ms;
+  }
+  c->snb_hc += want_grad ? 4 * NB - 1 : 2 * NB;
+  c->snb_mf += NB + (want_grad ? 1 : 0);
+  c->snb_dirty = false;
   return GPE_OK;
 }
 
@@ -1829,6 +1958,9 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
   if (c->tiny && c->NB == 1 && d <= TINY_DM && q + 1 <= TINY_DM)
     return tiny_objective(c, gp4ml, kernel, hp, n_hp, fitnug, nu, s2, rscale, want_grad != 0, llh_out, grad_out,
                           sigma2_out);
+  if (c->tiny && c->NB >= 2 && c->NB <= SNB_MAXNB && d <= TINY_DM && q + 1 <= TINY_DM)
+    return snb_objective(c, gp4ml, kernel, hp, n_hp, fitnug, nu, s2, rscale, want_grad != 0, llh_out, grad_out,
+                         sigma2_out);
 
   // z, w = L^-1 [f H] come out of the factorisation (augmented row); value only runs
   // no L^-1 at all

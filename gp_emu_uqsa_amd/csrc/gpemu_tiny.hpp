@@ -56,13 +56,12 @@ struct TinyArgs {
   double* Xo;           // out: X = L^-1 (ld 128, zero upper)
   double* Z;            // out: Z = L^-1 [f H] (ld 128, P columns)
   double* small;        // out (pinned host memory): Gram (P x P) | log|L| | failed column |
-                        // d + 3 sums | Q not PD
+                        // (d + 3) | Q not PD | the helpers' partial sums (TINY_NH x 64)
   double* K;            // the helpers' K-build in the block-packed image's layout; L's buffer
   double* Xp;           // X's LDS image (block-packed, 36 x DB_BS doubles)
   double* Wg;           // W for the helpers (128 x 32, row-major)
-  double* part;         // the helpers' partial sums (TINY_NH x 64)
-  int* sync;            // [0] K-build count, [1] X flag, [2] W flag, [3] ticket: monotone
-                        // over the context's calls (zeroed after a failed one)
+  int* sync;            // [0] K-build count, [1] X flag, [2] W flag: monotone over the
+                        // context's calls (zeroed after a failed one)
   int* abort_flag;      // the failed column (or 1: Q not positive definite); zero on entry
   int ek, eg;           // this call's ordinal among all calls / gradient calls since the zeroing
   int n, d, P, want_grad, mucm;
@@ -71,7 +70,7 @@ struct TinyArgs {
 };
 
 constexpr int TINY_NH = 9;
-constexpr int TINY_SYNC_INTS = 4;
+constexpr int TINY_SYNC_INTS = 3;
 
 // Hand-offs between the workgroups of one k_tiny launch without agent fences (each a
 // write-back or invalidate of ~1.7-6.5 us on the chain, three of them in a row before): every
@@ -89,6 +88,16 @@ __device__ __forceinline__ double tiny_ld(const double* p) {
 }
 __device__ __forceinline__ int tiny_ldi(const int* p) {
   return __hip_atomic_load((tiny_gint*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// sc1 load through a buffer descriptor over [base, base + 4 GB): an ordinary load the compiler
+// batches (an atomic load is issued and waited for one at a time); the consumer form of the
+// sc1 hand-off ("buffer_load ... sc1", aux 16)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tiny_rsrc(const double* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, -1, 0x00020000);
+}
+__device__ __forceinline__ double tiny_bld(__amdgpu_buffer_rsrc_t r, long long idx) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(idx * 8), 0, 16);
+  return __longlong_as_double(((long long)v[1] << 32) | v[0]);
 }
 // every wave's stores landed, then one lane signals (add 1, or store v when v > 0)
 __device__ __forceinline__ void tiny_signal(int* p, int v) {
@@ -318,21 +327,10 @@ __device__ void tiny_helper(const TinyArgs& a, double* lds) {
   }
   double* red = lds + 8;   // (past st)
   sm.reduce(d, red, red + 4 * (DM + 3));
-  if (tid < d + 3) tiny_st(a.part + h * 64 + tid, red[4 * (DM + 3) + tid]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const int old = __hip_atomic_fetch_add((tiny_gint*)&a.sync[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *st = old == TINY_NH * a.eg - 1;
-  }
-  __syncthreads();
-  if (*st && tid < d + 3) {   // the last helper: the nine partials in helper order
-    double v = 0.0;
-    for (int g = 0; g < TINY_NH; ++g) v += tiny_ld(a.part + g * 64 + tid);
-    a.small[P * P + 2 + tid] = v;
-  }
+  // this helper's partial sums straight to the host, which adds the nine in helper order
+  if (tid < d + 3) a.small[P * P + 2 + d + 4 + h * 64 + tid] = red[4 * (DM + 3) + tid];
 #ifdef TINY_TIMING
-  if (*st && tid == 0) tiny_tsc[7] = wall_clock64();
+  if (tid == 0) atomicMax(&tiny_tsc[7], wall_clock64());
 #endif
 }
 

@@ -37,7 +37,7 @@ int main() {
   hipMemset(flag, 0, 4);
   TinyArgs a{};
   a.X = dX; a.F = dF; a.r = nullptr; a.rdiag = nullptr; a.xw = xw; a.L = L; a.Xo = Xo; a.Z = Z; a.small = small;
-  a.K = L; a.Xp = Xp; a.Wg = Wg; a.part = part; a.sync = flag + 1;
+  a.K = L; a.Xp = Xp; a.Wg = Wg; a.sync = flag + 1;
   a.abort_flag = flag; a.n = n; a.d = d; a.P = P; a.want_grad = 1; a.mucm = 0;
   a.s2 = 1.0; a.coff = 1.0; a.cdiag = 1.0 + 1e-2; a.rscale = 0.0;
   for (int k = 0; k < 32; ++k) a.invd[k] = k < d ? 1.0 / 0.6 : 0.0;

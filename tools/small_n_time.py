@@ -12,7 +12,7 @@ from gp_emu_uqsa_amd import native, synthetic  # noqa: E402
 
 d = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 ctx = native.Context(0)
-for n in (60, 100, 128, 300, 640, 1024, 2048, 4096, 8192):
+for n in (60, 100, 128, 200, 300, 384, 500, 640, 1024, 2048, 4096, 8192):
     X, f, H = synthetic.problem(n, d, seed=0)
     ctx.set_data(X, f, H)
     hp = np.concatenate([np.ones(d), [1e-3, 1.0]])
