@@ -377,7 +377,7 @@ __device__ void snb_helper(const SnbArgs& a, double* lds) {
   double* red = lds + 8;
   sm.reduce(d, red, red + 4 * (DM + 3));
   // this helper's partial sums straight to the host, which adds them in helper order (no
-  // ticket and no last-helper pass on the kernel's tail)
+  // cross-workgroup pass on the kernel's tail)
   if (tid < d + 3) a.small[P * P + NB + 1 + d + 4 + h * 64 + tid] = red[4 * (DM + 3) + tid];
 }
 

@@ -1,25 +1,26 @@
 // gpemu_tiny.hpp -- the objective of a training set of at most 128 points (one 128 x 128
-// tile: the reference's examples, toy-sim's 60 and toysim3D's 100 points) in ONE one-
-// workgroup launch instead of the general path's ~20 small launches and copies.
+// tile: the reference's examples, toy-sim's 60 and toysim3D's 100 points) in ONE launch of
+// k_tiny instead of the general path's ~20 small launches and copies.
 //
-// k_tiny, with everything in LDS after the first staging:
-//   scaled points; K-build straight into the block-packed LDS image of db_factor_invert
-//   (rows i and 127 - i per lane, every wave the same number of entries); L and X = L^-1
-//   (assembled in LDS); Z = X [f H] (16 x 16 x 4 fp64 MFMA on X's blocks); the Gram Z^T Z.
-//   Value only: stop there (Gram, log|L| and the failed column go to the host, whose q x q
-//   algebra gives the LLH).  With the gradient, on: Y = X^T Z (MFMA); the q x q algebra of
-//   the host's small_from_gram / small_t2 (Cholesky of Q = H^T A^-1 H one column per
-//   barrier, beta and sqrt(c) on one lane, Kq^-1 one column per lane); W = Y T2 =
-//   X^T (Z T2) = [sqrt(c) alpha, Kq^-1-scaled L^-T L^-1 H] (MFMA); M = A^-1 - W W^T
-//   = X^T X - W W^T in 16 x 16 MFMA blocks, each contracted where it sits in the
-//   accumulators into the d + 3 sums of k_contract (<M, E (.) D_k>, <M, E>, tr M,
-//   sum M_ii r_i), four entries at a time so their exp chains overlap.
-// The host computes the LLH from the Gram with the same small_from_gram as the general
-// path, and the gradient from the d + 3 sums with the same small_grad.
-// The arithmetic of every quantity is the general path's formula (the K-build's entries
-// are k_pairs' to the bit: same scaled coordinates, same fma order, same selects); products
-// and sums run in other orders than the general path's GEMMs and k_contract, so results
-// agree to rounding.
+// Workgroup 0 (everything after the first staging in LDS): K's image in (built by the
+//   helpers), db_factor_invert (L and X = L^-1 assembled in LDS), X's image out to the
+//   helpers, Z = X [f H] (16 x 16 x 4 fp64 MFMA on X's blocks), the Gram Z^T Z.  Value only:
+//   stop there (Gram, log|L| and the failed column go to the host, whose q x q algebra gives
+//   the LLH).  With the gradient, on: Y = X^T Z (MFMA); the q x q algebra of the host's
+//   small_from_gram / small_t2 (Cholesky of Q = H^T A^-1 H one column per barrier, beta and
+//   sqrt(c), Kq^-1 one column per lane); W = Y T2 = X^T (Z T2) = [sqrt(c) alpha,
+//   Kq^-1-scaled L^-T L^-1 H] (MFMA), out to the helpers.
+// TINY_NH helper workgroups, wave w of helper h owning lower 16 x 16 block 4h + w: its K-build
+//   entries (k_pairs' arithmetic); then, once X is out, its block of X^T X (MFMA) and, once W
+//   is out, - W W^T and the contraction of its entries in the accumulators into the d + 3 sums
+//   of k_contract (<M, E (.) D_k>, <M, E>, tr M, sum M_ii r_i); each helper's partial sums go
+//   to the host, which adds them in helper order.
+// The host computes the LLH from the Gram with the same small_from_gram as the general path,
+// and the gradient from the d + 3 sums with the same small_grad.
+// The arithmetic of every quantity is the general path's formula (the K-build's entries are
+// k_pairs' to the bit: same scaled coordinates, same fma order, same selects); products and
+// sums run in other orders than the general path's GEMMs and k_contract, so results agree to
+// rounding.
 // Global -> LDS staging issues every load of a thread before its first LDS store (a load /
 // store pair per loop iteration put one memory latency per iteration in sequence).
 // Limits: n <= 128, d <= 32, q + 1 <= 32 (the host takes the general path otherwise).
@@ -226,7 +227,7 @@ __device__ __forceinline__ tiny_d4 tiny_mfma(double a, double b, tiny_d4 c) {
 // mode, in the MFMA accumulator layout: lane -> rows 16 bi + lane / 16 + 4 r, column
 // 16 bj + lane % 16), written to K and their exp(-s) kept; then, once workgroup 0 has
 // published W, M(bi, bj) = X^T X - W W^T (MFMA, X and W from L2) contracted into the d + 3
-// sums; the last helper to finish adds the nine partials in helper order.
+// sums; each helper's partial sums go to the host.
 template <int DM>
 __device__ void tiny_helper(const TinyArgs& a, double* lds) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = blockIdx.x - 1;
@@ -271,6 +272,7 @@ __device__ void tiny_helper(const TinyArgs& a, double* lds) {
   tiny_signal(&a.sync[0], 0);
   if (!a.want_grad) return;
   int* st = reinterpret_cast<int*>(lds);
+  const auto rXp = tiny_rsrc(a.Xp), rWg = tiny_rsrc(a.Wg);
   // M(bi, bj) = X^T X (as soon as workgroup 0 has published X) - W W^T (once W is out)
   if (tiny_wait(&a.sync[1], a.eg, a.abort_flag, st) != 1) return;
   tiny_d4 acc = {0.0, 0.0, 0.0, 0.0};
@@ -282,8 +284,12 @@ __device__ void tiny_helper(const TinyArgs& a, double* lds) {
       for (int s = 0; s < 4; ++s) {
         // X(16 kb + k, 16 bi + m) (zero above the diagonal of a diagonal block)
         const int k = 4 * s + k4;
-        av[kb][s] = (kb >= bi && !(kb == bi && k < m16)) ? tiny_ld(a.Xp + db_blk(kb, bi) + db_e(k, m16)) : 0.0;
-        bv[kb][s] = (kb >= bi && !(kb == bj && k < m16)) ? tiny_ld(a.Xp + db_blk(kb, bj) + db_e(k, m16)) : 0.0;
+        // (every load unconditional, so they issue back to back; out-of-range blocks read block 0)
+        const bool ia = kb >= bi && !(kb == bi && k < m16), ib = kb >= bi && !(kb == bj && k < m16);
+        const double va = tiny_bld(rXp, (kb >= bi ? db_blk(kb, bi) : 0) + db_e(k, m16));
+        const double vb = tiny_bld(rXp, (kb >= bi ? db_blk(kb, bj) : 0) + db_e(k, m16));
+        av[kb][s] = ia ? va : 0.0;
+        bv[kb][s] = ib ? vb : 0.0;
       }
 #pragma unroll
     for (int kb = 0; kb < 8; ++kb)
@@ -297,8 +303,9 @@ __device__ void tiny_helper(const TinyArgs& a, double* lds) {
     double av[8], bv[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      av[s] = s < ks ? -tiny_ld(a.Wg + (16 * bi + m16) * 32 + 4 * s + k4) : 0.0;
-      bv[s] = s < ks ? tiny_ld(a.Wg + (16 * bj + m16) * 32 + 4 * s + k4) : 0.0;
+      const double va = tiny_bld(rWg, (16 * bi + m16) * 32 + 4 * s + k4), vb = tiny_bld(rWg, (16 * bj + m16) * 32 + 4 * s + k4);
+      av[s] = s < ks ? -va : 0.0;
+      bv[s] = s < ks ? vb : 0.0;
     }
 #pragma unroll
     for (int s = 0; s < 8; ++s)
@@ -370,7 +377,8 @@ static __global__ void __launch_bounds__(256) k_tiny(TinyArgs a) {
     }
   }
   // the helpers' image of K's lower half (the diagonal blocks' upper entries unused)
-  tiny_stage<36 * DB_BS / 256 + 1>([&](int e) { return e < 36 * DB_BS ? tiny_ld(a.K + e) : 0.0; },
+  const auto rK = tiny_rsrc(a.K);
+  tiny_stage<36 * DB_BS / 256 + 1>([&](int e) { return tiny_bld(rK, min(e, 36 * DB_BS - 1)); },
                                    [&](int e, double v) { if (e < 36 * DB_BS) lb[e] = v; });
   __syncthreads();
   TINY_T(2);
