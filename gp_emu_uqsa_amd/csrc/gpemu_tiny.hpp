@@ -366,9 +366,14 @@ static __global__ void __launch_bounds__(256) k_tiny(TinyArgs a) {
     const int i = e / DM, k = e - i * DM;
     if (k < d) a.xw[i * d + k] = v;
   });
+  // [f H] -> r1 ([i][p], pitch ZP; columns P .. 16 npb zero), also while the helpers build K
+  tiny_stage<TILE * TINY_DM / 256>([&](int e) {
+    const int i = e / TINY_DM, p = e - i * TINY_DM;
+    return p < P ? a.F[i + p * TILE] : 0.0;
+  }, [&](int e, double v) { r1[(e / TINY_DM) * ZP + e % TINY_DM] = v; });
   TINY_T(1);
   {
-    if (tiny_wait(&a.sync[0], TINY_NH * a.ek, nullptr, reinterpret_cast<int*>(r1)) != 1) {   // (never expected)
+    if (tiny_wait(&a.sync[0], TINY_NH * a.ek, nullptr, reinterpret_cast<int*>(zs)) != 1) {   // (never expected)
       if (tid == 0) {
         a.small[P * P + 1] = -1.0;
         if (a.abort_flag) atomicCAS(a.abort_flag, 0, GEMM_WAIT_TIMEOUT);
@@ -390,18 +395,8 @@ static __global__ void __launch_bounds__(256) k_tiny(TinyArgs a) {
     }
     return;
   }
-  if (a.want_grad) {   // X's image for the helpers
-    __syncthreads();   // (the assembled image complete)
-    for (int e = tid; e < 36 * DB_BS; e += 256) tiny_st(a.Xp + e, lb[e]);
-    tiny_signal(&a.sync[1], a.eg);
-  }
   TINY_T(3);
-  // [f H] -> r1 ([i][p], pitch ZP; columns P .. 16 npb zero)
-  tiny_stage<TILE * TINY_DM / 256>([&](int e) {
-    const int i = e / TINY_DM, p = e - i * TINY_DM;
-    return p < P ? a.F[i + p * TILE] : 0.0;
-  }, [&](int e, double v) { r1[(e / TINY_DM) * ZP + e % TINY_DM] = v; });
-  __syncthreads();
+  __syncthreads();   // (the assembled image complete)
   // X's element (i, k) from the image; the diagonal blocks hold other values across their
   // diagonal, read as zero (lower: k > i, or as X^T: k < i)
   auto xlo = [&](int bi, int bk, int i, int k) {   // X(16 bi + i, 16 bk + k), lower
@@ -453,6 +448,9 @@ static __global__ void __launch_bounds__(256) k_tiny(TinyArgs a) {
   if (tid == 0) a.small[P * P + 1] = 0.0;
   TINY_T(5);
   if (!a.want_grad) return;
+  // X's image for the helpers (off the chain until here: they need it only some 20 us before W)
+  for (int e = tid; e < 36 * DB_BS; e += 256) tiny_st(a.Xp + e, lb[e]);
+  tiny_signal(&a.sync[1], a.eg);
   // Y = X^T Z: blocks (bi, bp) over kb >= bi; written over [f H] (read before the barrier
   // above)
 #pragma unroll
