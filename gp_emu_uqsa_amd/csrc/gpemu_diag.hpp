@@ -350,7 +350,7 @@ __device__ __forceinline__ void db_syrk_pair(double* lb, int pa0, int pb0, int p
 template <int H>
 __device__ __forceinline__ void db_xlevel(double* lb) {
   constexpr int NBH = H / 16, NINST = 128 / (2 * H);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // diagonal blocks hold X in their lower part only
   auto xop = [&](int bi, int bk, int r, int c) -> double {
     const int off = (bi * (bi + 1) / 2 + bk) * DB_BS + db_e(r, c);
@@ -444,7 +444,10 @@ template <class OnFactored>
 __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long long ldl, double* Xg,
                                                 long long ldx, double* logdet_out, OnFactored on_factored,
                                                 bool assemble = true) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the wave index as a scalar: derived from tid >> 6 the compiler treats it as divergent,
+  // and the trailing update's block loop ran under exec masks with its MFMA pairs split
+  // by branches (s_nop between dependent MFMAs)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   double* xs = lb + 36 * DB_BS;           // current leaf inverse, 16 x 16 (db_e)
   double* xdiag = lb + DB_LDS_DOUBLES;    // 128 diagonal entries of X
   double* red = xdiag + 128;              // 4
@@ -504,7 +507,9 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
       db_syrk_block(lb, p1, p1, db_blk(jb + 1, jb + 1));
       DB_T(6);
       DB_TN(5);
+#ifndef DB_NO_LEAF   // dev probe: the update without the leaf beside it (wrong results)
       DB_LEAF(lb, xs, xdiag, jb + 1, flag);
+#endif
       DB_T(5);
     } else {
       DB_TN(7);

@@ -369,21 +369,26 @@ struct gpe_dist {
   double* cpart = nullptr; // contraction partials (scratch, stream-ordered)
   std::vector<Rank> ranks;   // local ranks (all P in loopback, one otherwise)
 
-  // column groups (as the single-GPU fused Cholesky): {width, min remaining tile
-  // columns}, first match wins, else 1 (GPEMU_DIST_W="8:160,4:80,2:40" style)
-  std::vector<std::pair<int, int>> groups = {{8, 160}, {4, 80}, {2, 40}};
+  // column groups: {width, min remaining tile columns}, first match wins, else 1
+  // (GPEMU_DIST_W="8:160,4:80,2:40" style).  Width 4 to the end: with the next group's
+  // update on the chain stream, the narrower tail groups of round 5 (2 and 1 wide) cost
+  // more in launches than their shorter pending updates saved (P = 1, n = 16384: value
+  // 30.7-30.9 -> 30.2-30.3 ms, gradient 75.4-75.5 -> 74.6-74.8, profiles/dist_w_r05z.log)
+  std::vector<std::pair<int, int>> groups = {{8, 160}, {4, 0}};
   std::vector<int> gstart;   // per step: first column of its group
   std::vector<int> gid;      // per step: index of its group
   std::vector<int> gs;       // group starts, then NB
   int wmax = 1;
   size_t panel_sz = 0;       // doubles per panel buffer (two per rank)
   std::vector<hipEvent_t> ev_chain, ev_next;   // per group (sweep or TRTRI, reused)
-  hipEvent_t ev_join = nullptr;
+  std::vector<hipEvent_t> ev_near, ev_far;     // per group: the sweep's near / far updates done
+  hipEvent_t ev_join = nullptr, ev_end = nullptr;
+  bool next_on_chain = true;                   // GPEMU_DIST_NEXT_ON_CHAIN=0: round-5 schedule
   int* dli0 = nullptr;       // [NB][P] first local row with global row > k
   int* dcnt = nullptr;       // [NB][P] panel tiles of rank r at step k
   GemmProb* dprobs = nullptr;
   unsigned* dtiles = nullptr;
-  std::vector<DLaunch> diag, mrow, panel_l, upd_next, upd_rest;   // per step (updates: group ends)
+  std::vector<DLaunch> diag, mrow, panel_l, upd_next, upd_near, upd_far;   // per step (updates: group ends)
   std::vector<int> maxT;                       // per step: max panel tiles over ranks
   size_t recv_tiles = 0;                       // P > 1: tiles per rank segment of the group all-gather
   double* hpin = nullptr;
@@ -693,7 +698,8 @@ int build_schedule(gpe_dist* h) {
   h->mrow.assign(NB, DLaunch());
   h->panel_l.assign(NB, DLaunch());
   h->upd_next.assign(NB, DLaunch());
-  h->upd_rest.assign(NB, DLaunch());
+  h->upd_near.assign(NB, DLaunch());
+  h->upd_far.assign(NB, DLaunch());
   h->maxT.assign(NB, 0);
   std::vector<int> li0((size_t)NB * P), cnt((size_t)NB * P);
   for (int k = 0; k < NB; ++k) {
@@ -827,12 +833,14 @@ int build_schedule(gpe_dist* h) {
     pl.kind = 4;
     h->panel_l[k] = pl;
     // the step closing a group: trailing update of each local rank's rows by the
-    // whole group, columns ge <= j <= i, K = 128 (ge - gb), in two launches: the next
-    // group's columns ge <= j < ge2 (its chain waits for these only), then j >= ge2
+    // whole group, columns ge <= j <= i, K = 128 (ge - gb), in three launches: the next
+    // group's columns ge <= j < ge2 (its chain waits for these), the group after it
+    // (ge2 <= j < ge3: the next chain's own next-group update waits for these), then the rest
     if (k + 1 != ge) continue;
     const int ge2 = next_group_end(h, k);
-    for (int part = 0; part < 2; ++part) {
-      const int j0 = part == 0 ? ge : ge2, j1 = part == 0 ? ge2 : NT;   // columns [j0, j1)
+    const int ge3 = ge2 < NB ? next_group_end(h, ge2 - 1) : NB;
+    for (int part = 0; part < 3; ++part) {
+      const int j0 = part == 0 ? ge : (part == 1 ? ge2 : ge3), j1 = part == 0 ? ge2 : (part == 1 ? ge3 : NT);
       DLaunch ul;
       ul.first = (int)probs.size();
       ul.list = (long long)tiles.size();
@@ -860,7 +868,7 @@ int build_schedule(gpe_dist* h) {
         std::copy(ord.begin(), ord.end(), tiles.begin() + ul.list);
       }
       ul.kind = 4;
-      (part == 0 ? h->upd_next : h->upd_rest)[k] = ul;
+      (part == 0 ? h->upd_next : (part == 1 ? h->upd_near : h->upd_far))[k] = ul;
     }
   }
   if ((int)probs.size() > DIST_DESC_MAX) return dfail(h, GPE_ERR_UNSUPPORTED, "distributed schedule too large");
@@ -1274,26 +1282,60 @@ int gather_group(gpe_dist* h, int gb, int ge) {
 
 int ensure_group_events(gpe_dist* h, size_t ng) {
   while (h->ev_chain.size() < ng) {
-    hipEvent_t a, b;
+    hipEvent_t a, b, c, d;
     DCHK_HIP(h, hipEventCreateWithFlags(&a, hipEventDisableTiming));
     DCHK_HIP(h, hipEventCreateWithFlags(&b, hipEventDisableTiming));
+    DCHK_HIP(h, hipEventCreateWithFlags(&c, hipEventDisableTiming));
+    DCHK_HIP(h, hipEventCreateWithFlags(&d, hipEventDisableTiming));
     h->ev_chain.push_back(a);
     h->ev_next.push_back(b);
+    h->ev_near.push_back(c);
+    h->ev_far.push_back(d);
   }
   return GPE_OK;
 }
 
 // The column groups with one group of look-ahead.  Group g's chain (its steps) runs on
-// the critical stream after the previous group's update of g's own columns; its
-// trailing update then runs on the compute stream, next group's columns first
-// (ev_next[g] releases the next chain), the rest behind them, overlapping the next
-// chain and its collectives.  The compute stream ends after every chain (it waited on
-// each ev_chain), so work queued on it afterwards follows the whole sweep.
+// the critical stream; its trailing update is three launches by columns: the next
+// group's (A), the group after it (B) and the rest (C).  A runs on the critical stream
+// right behind the chain, after B of the previous group (the only earlier update of
+// those columns still possibly running: everything before it on the compute stream is
+// done), so the next chain never queues behind the far update C of the previous group;
+// B and C run on the compute stream after the chain, overlapping the next chains.
+// Writers of one column's tiles never overlap: A(g) waits for B(g-1), which follows C(g-2)
+// on the compute stream.  A group's gather (P > 1) refills the panel buffer of group g-2
+// and waits for that group's C.  The compute stream finally waits for the critical one,
+// so work queued on it afterwards follows the whole sweep.
+// GPEMU_DIST_NEXT_ON_CHAIN=0: the round-5 schedule (A on the compute stream behind the
+// previous group's B and C; the next chain waits for it).
 int group_sweep(gpe_dist* h) {
   const int ng = (int)h->gs.size() - 1;
   DCHK(ensure_group_events(h, (size_t)ng));
   DCHK_HIP(h, hipEventRecord(h->ev_join, h->stream));
   DCHK_HIP(h, hipStreamWaitEvent(h->crit, h->ev_join, 0));
+  if (h->next_on_chain) {
+    for (int g = 0; g < ng; ++g) {
+      const int gb = h->gs[g], ge = h->gs[g + 1];
+      h->cs = h->crit;
+      for (int k = gb; k < ge; ++k) DCHK(step(h, k));
+      if (g >= 2 && gather_panels(h)) DCHK_HIP(h, hipStreamWaitEvent(h->crit, h->ev_far[g - 2], 0));
+      DCHK(gather_group(h, gb, ge));
+      DCHK_HIP(h, hipEventRecord(h->ev_chain[g], h->crit));
+      h->cs = h->stream;
+      DCHK_HIP(h, hipStreamWaitEvent(h->stream, h->ev_chain[g], 0));
+      DCHK(launch(h, h->upd_near[ge - 1]));
+      DCHK_HIP(h, hipEventRecord(h->ev_near[g], h->stream));
+      DCHK(launch(h, h->upd_far[ge - 1]));
+      DCHK_HIP(h, hipEventRecord(h->ev_far[g], h->stream));
+      h->cs = h->crit;
+      if (g >= 1) DCHK_HIP(h, hipStreamWaitEvent(h->crit, h->ev_near[g - 1], 0));
+      DCHK(launch(h, h->upd_next[ge - 1]));
+    }
+    DCHK_HIP(h, hipEventRecord(h->ev_end, h->crit));
+    DCHK_HIP(h, hipStreamWaitEvent(h->stream, h->ev_end, 0));
+    h->cs = h->stream;
+    return GPE_OK;
+  }
   for (int g = 0; g < ng; ++g) {
     const int gb = h->gs[g], ge = h->gs[g + 1];
     h->cs = h->crit;
@@ -1305,7 +1347,8 @@ int group_sweep(gpe_dist* h) {
     DCHK_HIP(h, hipStreamWaitEvent(h->stream, h->ev_chain[g], 0));
     DCHK(launch(h, h->upd_next[ge - 1]));
     DCHK_HIP(h, hipEventRecord(h->ev_next[g], h->stream));
-    DCHK(launch(h, h->upd_rest[ge - 1]));
+    DCHK(launch(h, h->upd_near[ge - 1]));
+    DCHK(launch(h, h->upd_far[ge - 1]));
   }
   h->cs = h->stream;
   return GPE_OK;
@@ -1363,6 +1406,7 @@ gpe_dist* gpe_dist_create(int32_t device, int32_t nranks, int32_t rank, const ui
   h->P = nranks;
   h->rank = unique_id ? rank : 0;
   h->loop = unique_id == nullptr;
+  if (const char* e = std::getenv("GPEMU_DIST_NEXT_ON_CHAIN")) h->next_on_chain = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPEMU_DIST_W")) {   // "4:80,2:40": {width, min remaining}
     h->groups.clear();
     std::string spec(e);
@@ -1382,6 +1426,7 @@ gpe_dist* gpe_dist_create(int32_t device, int32_t nranks, int32_t rank, const ui
   bool ok = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
             hipStreamCreateWithPriority(&h->crit, hipStreamNonBlocking, hi) == hipSuccess &&
             hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&h->ev_end, hipEventDisableTiming) == hipSuccess &&
             hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) == hipSuccess &&
             hipEventCreate(&h->e0) == hipSuccess && hipEventCreate(&h->e1) == hipSuccess &&
             hipMalloc((void**)&h->dinfo, sizeof(int)) == hipSuccess;
@@ -1423,7 +1468,10 @@ void gpe_dist_destroy(gpe_dist* h) {
   if (h->e1) (void)hipEventDestroy(h->e1);
   for (hipEvent_t e : h->ev_chain) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->ev_next) (void)hipEventDestroy(e);
+  for (hipEvent_t e : h->ev_near) (void)hipEventDestroy(e);
+  for (hipEvent_t e : h->ev_far) (void)hipEventDestroy(e);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+  if (h->ev_end) (void)hipEventDestroy(h->ev_end);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   if (h->crit) (void)hipStreamDestroy(h->crit);
   delete h;

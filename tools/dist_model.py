@@ -1,7 +1,7 @@
 """Predicted strong-scaling curve of the row-block objective (dev tool).
 
   python tools/dist_model.py --p1-ms MS --p1-value-ms MS [--points 16384] [--basis 11]
-                             [--dims 10] [--widths 8:160,4:80,2:40] [--chain-us 90]
+                             [--dims 10] [--widths 8:160,4:0] [--chain-us 90]
 
 Counts, from the schedule of gpemu_dist.hip (column groups, recursive TRTRI chunks), the
 collectives one LLH + gradient issues and the bytes each rank receives in them, then
@@ -139,7 +139,7 @@ def main():
     ap.add_argument("--points", type=int, default=16384)
     ap.add_argument("--basis", type=int, default=11, help="q + 1")
     ap.add_argument("--dims", type=int, default=10)
-    ap.add_argument("--widths", default="8:160,4:80,2:40", help="the row-block path's column-group widths")
+    ap.add_argument("--widths", default="8:160,4:0", help="the row-block path's column-group widths")
     ap.add_argument("--p1-ms", type=float, default=None, help="loopback P=1 LLH+gradient ms")
     ap.add_argument("--p1-value-ms", type=float, default=None, help="loopback P=1 value-only ms")
     ap.add_argument("--chain-us", type=float, default=75.0, help="diagonal factor + panel per step, us")
