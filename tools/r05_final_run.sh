@@ -5,7 +5,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 case "$1" in
-  check) bash tools/gpu_check.sh r05z ;;
+  check) bash tools/gpu_check.sh ${2:-r05z} ;;
   profile)
     timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_r05.log 2>&1 || exit 1
     tail -2 gpurun_out/smoke_r05.log
