@@ -529,8 +529,13 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
         int r1 = rr;
         while ((r1 + 1) * (r1 + 2) / 2 <= b1) ++r1;
         const int ib1 = jb + 1 + r1, kb1 = jb + 1 + (b1 - r1 * (r1 + 1) / 2);
-        db_syrk_pair(lb, db_blk(ib, jb), db_blk(kb, jb), db_blk(ib, kb),
-                     has1 ? db_blk(ib1, jb) : 0, has1 ? db_blk(kb1, jb) : 0, has1 ? db_blk(ib1, kb1) : 0, has1);
+        // without a second block the first one goes twice: db_syrk_pair reads both C blocks
+        // before writing either, so both write the same values -- and the pair stays
+        // branch-free (under has1 its loads and MFMAs were split by ~20 branches: a pair
+        // took 2000 shader cycles against 860 in a loop of this shape, tools/hip/syrk_probe.hip;
+        // the factor 1-1.5 us faster, profiles/db_probe_r05f.log)
+        db_syrk_pair(lb, db_blk(ib, jb), db_blk(kb, jb), db_blk(ib, kb), db_blk(has1 ? ib1 : ib, jb),
+                     db_blk(has1 ? kb1 : kb, jb), has1 ? db_blk(ib1, kb1) : db_blk(ib, kb), true);
       }
       for (int ib = jb + wave - 1; ib < 8; ib += 3) {
         if (ib == jb) db_put_block<1>(lb, db_blk(jb, jb), lg_at(jb, jb), ldl);

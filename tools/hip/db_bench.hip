@@ -10,8 +10,11 @@ using namespace gpe;
 __device__ unsigned long long db_tsc[8];   // stays zero: untimed build
 #endif
 
+__device__ unsigned long long db_clk[2];   // shader cycles, wall ticks (100 MHz) of the factor
+
 __global__ void __launch_bounds__(256) k_db(double* A, long long ld, double* X, double* lg, int* info) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
+  const unsigned long long c0 = clock64(), w0 = wall_clock64();
   for (int e = threadIdx.x; e < 128 * 128; e += 256) {
     const int i = e & 127, k = e >> 7;
     if (i >= k) lds[db_off(i, k)] = A[i + k * ld];
@@ -19,6 +22,10 @@ __global__ void __launch_bounds__(256) k_db(double* A, long long ld, double* X, 
   __syncthreads();
   const int bad = db_factor_invert(lds, A, ld, X, ld, lg, [] {});
   if (bad && threadIdx.x == 0) *info = bad;
+  if (threadIdx.x == 0) {
+    atomicAdd(&db_clk[0], clock64() - c0);
+    atomicAdd(&db_clk[1], wall_clock64() - w0);
+  }
 }
 
 int main() {
@@ -72,5 +79,8 @@ int main() {
   const char* nm[8] = {"total", "leaf+update", "panel", "X assembly", "L/X out", "leaf (w0)", "diag syrk (w0)",
                        "update (w1)"};
   for (int i = 0; i < 8; ++i) printf("  %-14s %.1f us (mean)\n", nm[i], t[i] * 0.01 / reps);
+  unsigned long long ck[2];
+  hipMemcpyFromSymbol(ck, HIP_SYMBOL(db_clk), sizeof(ck));
+  printf("  kernel body %.1f us (mean), shader clock %.2f GHz\n", ck[1] * 0.01 / reps, (double)ck[0] / (ck[1] * 10.0));
   return 0;
 }
