@@ -427,6 +427,20 @@ __device__ __forceinline__ void db_put_block(const double* lb, int off, double* 
 
 __device__ __forceinline__ int db_blk(int bi, int bk) { return (bi * (bi + 1) / 2 + bk) * DB_BS; }
 
+// row of entry b of a row-major lower triangle (b = r (r + 1) / 2 + c), b < 28: a packed
+// table of 3-bit rows for b < 21, row 6 beyond -- a few scalar operations instead of a loop
+__host__ __device__ constexpr unsigned long long db_tri_rows() {
+  unsigned long long t = 0;
+  for (int b = 0, r = 0; b < 21; ++b) {
+    while ((r + 1) * (r + 2) / 2 <= b) ++r;
+    t |= (unsigned long long)r << (3 * b);
+  }
+  return t;
+}
+__device__ __forceinline__ int db_tri_row(int b) {
+  return b >= 21 ? 6 : (int)((db_tri_rows() >> (3 * b)) & 7);
+}
+
 // Factor + invert the tile held block-packed in lb[0 .. 36*DB_BS).  Writes L (lower)
 // to Lg, X = L^-1 (full tile, zero upper) to Xg, returns 0 or the 1-based column
 // of the first bad pivot; *logdet_out (thread 0) = sum log L_jj.
@@ -521,13 +535,11 @@ __device__ __forceinline__ int db_factor_invert(double* lb, double* Lg, long lon
       // time (one at a time, the update's LDS round trips held wave 0's leaf at twice its
       // stand-alone time: factor 78.7 -> 73.4 us with pairs, tools/hip/db_bench.hip)
       for (int b = wave; b < cnt; b += 6) {
-        int rr = 0;
-        while ((rr + 1) * (rr + 2) / 2 <= b) ++rr;
+        const int rr = db_tri_row(b);
         const int ib = jb + 1 + rr, kb = jb + 1 + (b - rr * (rr + 1) / 2);
         const int b1 = b + 3;
         const bool has1 = b1 < cnt;
-        int r1 = rr;
-        while ((r1 + 1) * (r1 + 2) / 2 <= b1) ++r1;
+        const int r1 = db_tri_row(b1);
         const int ib1 = jb + 1 + r1, kb1 = jb + 1 + (b1 - r1 * (r1 + 1) / 2);
         // without a second block the first one goes twice: db_syrk_pair reads both C blocks
         // before writing either, so both write the same values -- and the pair stays
