@@ -150,6 +150,8 @@ struct gpe_ctx {
   long long snb_np = 0;
   int snb_hc = 0, snb_mf = 0;   // k_snb's counters (dinfo[8..9]; abort dinfo[10])
   bool snb_dirty = true;
+  double onel_tag = 0.0;          // the one-launch objectives' call tag (never repeats)
+  int dbg_skip_wait = -1;         // GPEMU_DEBUG_SKIP_WAIT (tests): a helper gives up its first wait
   size_t small_cap = 0;
 
   // pinned host staging
@@ -1530,6 +1532,7 @@ gpe_ctx* gpe_create(int32_t device) {
     if (const char* eg = std::getenv("GPEMU_GROUP_STRIDE")) c->grp_stride = std::max(0, std::atoi(eg));
     if (const char* ep = std::getenv("GPEMU_CHOL_PRIO")) c->chol_prio = std::atoi(ep) != 0;
     if (const char* et = std::getenv("GPEMU_TINY")) c->tiny = std::atoi(et) != 0;
+    if (const char* ed = std::getenv("GPEMU_DEBUG_SKIP_WAIT")) c->dbg_skip_wait = std::atoi(ed);
     if (const char* es = std::getenv("GPEMU_POTRF_SB")) {
       c->potrf_sb = std::max(1, std::min(8, std::atoi(es)));
       if (const char* colon = std::strchr(es, ':')) c->potrf_sb_min = std::max(0, std::atoi(colon + 1));
@@ -1752,8 +1755,11 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
   a.ek = ++c->tiny_ek;
   a.eg = want_grad ? ++c->tiny_eg : c->tiny_eg;
   a.s2 = s2; a.rscale = rscale;
+  a.dbg_skip = c->dbg_skip_wait;
+  a.tag = ++c->onel_tag;
   kernel_consts(kernel, nu, true, &a.coff, &a.cdiag);
   const size_t lds = (G_LDS_LAUNCH_DOUBLES + 2 * TILE * TINY_ZP) * sizeof(double);
+  c->hpin[P * P + 1] = -2.0;   // (workgroup 0 overwrites it on every path; -2: it did not)
   c->tiny_dirty = true;   // (until this call has ended cleanly: its sync words are then consistent)
   if (d <= 4) hipLaunchKernelGGL(k_tiny<4>, dim3(1 + TINY_NH), dim3(256), lds, c->stream, a);
   else if (d <= 8) hipLaunchKernelGGL(k_tiny<8>, dim3(1 + TINY_NH), dim3(256), lds, c->stream, a);
@@ -1763,6 +1769,10 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));   // (the kernel wrote its outputs to hpin)
   const int info = (int)c->hpin[P * P + 1];
+  if (info < 0) {   // a wait ran out (-1) or workgroup 0 never reported (-2): not the matrix's doing
+    c->err = info == -1 ? std::string("k_tiny: a workgroup wait timed out") : "k_tiny: workgroup 0 did not complete";
+    return GPE_ERR_HIP;   // (tiny_dirty stays set: the next call zeroes the sync words)
+  }
   if (info != 0) {
     c->err = "matrix not positive definite (pivot " + std::to_string(info) + ")";
     return GPE_NOT_PD;
@@ -1798,6 +1808,11 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
     (void)cfac;   // (the device's T2 carries sqrt(cfac))
     double red[TINY_DM + 3];
     const double* part = c->hpin + (size_t)P * P + 2 + d + 4;
+    for (int h = 0; h < TINY_NH; ++h)   // every helper's sums are this call's (a helper that gave up a wait never tags them)
+      if (part[h * 64 + 63] != a.tag) {
+        c->err = "k_tiny: helper " + std::to_string(h) + " did not finish (a wait timed out)";
+        return GPE_ERR_HIP;
+      }
     for (int k = 0; k < d + 3; ++k) {   // the helpers' partials in helper order
       double v = 0.0;
       for (int h = 0; h < TINY_NH; ++h) v += part[h * 64 + k];
@@ -1819,7 +1834,7 @@ int tiny_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_h
 }
 
 // The objective of 2-4 tiles (128 < n <= 512, gpemu_snb.hpp): ONE launch of k_snb
-// (workgroup 0: the diagonal factors, the Gram and the q x q algebra; 32 helper workgroups:
+// (workgroup 0: the diagonal factors, the Gram and the q x q algebra; SNB_NH = 48 helper workgroups:
 // K-build, panels and updates with [f H]^T as an augmented row, X = L^-1, W and the
 // contraction), outputs straight into the pinned host buffer; the host's small_from_gram /
 // small_grad as in tiny_objective.
@@ -1861,8 +1876,11 @@ int snb_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_hp
   a.mucm = gp4ml ? 0 : 1;
   a.hcb = c->snb_hc; a.mfb = c->snb_mf;
   a.s2 = s2; a.rscale = rscale;
+  a.dbg_skip = c->dbg_skip_wait;
+  a.tag = ++c->onel_tag;
   kernel_consts(kernel, nu, true, &a.coff, &a.cdiag);
   const size_t lds = SNB_LDS_DOUBLES * sizeof(double);
+  c->hpin[P * P + NB] = -2.0;   // (workgroup 0 overwrites it on every path; -2: it did not)
   c->snb_dirty = true;   // (until this call has ended cleanly)
   const dim3 grid(1 + SNB_NH);
   if (d <= 4) hipLaunchKernelGGL(k_snb<4>, grid, dim3(256), lds, c->stream, a);
@@ -1875,8 +1893,9 @@ int snb_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_hp
   const double* h = c->hpin;
   const int info = (int)h[P * P + NB];
   if (info != 0) {
-    c->err = info < 0 ? std::string("k_snb: a workgroup wait timed out")
-                      : "matrix not positive definite (pivot " + std::to_string(info) + ")";
+    c->err = info == -1   ? std::string("k_snb: a workgroup wait timed out")
+             : info < 0 ? std::string("k_snb: workgroup 0 did not complete")
+                        : "matrix not positive definite (pivot " + std::to_string(info) + ")";
     return info < 0 ? GPE_ERR_HIP : GPE_NOT_PD;
   }
   double logdetA = 0.0;
@@ -1908,6 +1927,11 @@ int snb_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_hp
     }
     double red[TINY_DM + 3];
     const double* part = h + (size_t)P * P + NB + 1 + d + 4;
+    for (int g = 0; g < SNB_NH; ++g)   // every helper's sums are this call's
+      if (part[g * 64 + 63] != a.tag) {
+        c->err = "k_snb: helper " + std::to_string(g) + " did not finish (a wait timed out)";
+        return GPE_ERR_HIP;
+      }
     for (int k = 0; k < d + 3; ++k) {   // the helpers' partials in helper order
       double v = 0.0;
       for (int g = 0; g < SNB_NH; ++g) v += part[g * 64 + k];

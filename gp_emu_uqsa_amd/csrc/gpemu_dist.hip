@@ -319,6 +319,8 @@ struct DLaunch {           // one grouped k_gemm launch
   int kind = 0;            // 0 <false,false> (the fused instance: G_DIAG problems), 1 <false,true>,
                            // 2 <true,true>, 3 <true,false>, 4 <false,false> (plain)
   bool cdef = false;       // k_gemm's CDEF instance (gemm_cdef of some problem)
+  int* ticket = nullptr;   // FUSED launches with in-launch waits: list positions by atomic
+                           // ticket (k_gemm), so progress never depends on dispatch order
 };
 
 // one column chunk of one level of the recursive TRTRI (see ensure_grad)
@@ -364,8 +366,9 @@ struct gpe_dist {
   double* dr = nullptr;
   double* dinvdelta = nullptr;
   int* dinfo = nullptr;    // abort flag / failed pivot (all-reduced with max over RCCL)
-  int* dq = nullptr;       // 3 x NB counters: the diagonal tiles' pending-update blocks (G_DQUAD);
-                           // P = 1: the diagonal flags and the panel halves' stored updates
+  int* dq = nullptr;       // 4 x NB counters: the diagonal tiles' pending-update blocks (G_DQUAD);
+                           // P = 1: the diagonal flags and the panel halves' stored updates;
+                           // the diagonal launches' tickets
   double* cpart = nullptr; // contraction partials (scratch, stream-ordered)
   std::vector<Rank> ranks;   // local ranks (all P in loopback, one otherwise)
 
@@ -794,6 +797,9 @@ int build_schedule(gpe_dist* h) {
         ++dl.count;
       }
     }
+    // in-launch waits (quadrants -> factor, factor -> panel halves, halves -> halves): the
+    // workgroups take their positions by ticket, as the single-GPU sweep's
+    if (dl.count > 1) dl.ticket = h->dq + 3 * NB + k;
     h->diag[k] = dl;
     // P > 1, Kp > 0: the owner's M block of the broadcast, -Dinv L(k, gb:k) (its own row)
     if (gath && Kp > 0)
@@ -899,7 +905,7 @@ int launch(gpe_dist* h, const DLaunch& L, bool grad = false) {
       case 3: hipLaunchKernelGGL((k_gemm<true, false, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
       case 4: hipLaunchKernelGGL((k_gemm<false, false, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
       default:   // kind 0 launches may carry G_DIAG / G_PANEL problems
-        hipLaunchKernelGGL((k_gemm<false, false, true, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
+        hipLaunchKernelGGL((k_gemm<false, false, true, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, L.ticket); break;
     }
   } else {
     switch (L.kind) {
@@ -908,7 +914,7 @@ int launch(gpe_dist* h, const DLaunch& L, bool grad = false) {
       case 3: hipLaunchKernelGGL((k_gemm<true, false>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
       case 4: hipLaunchKernelGGL((k_gemm<false, false>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
       default:   // kind 0 launches may carry G_DIAG / G_PANEL problems
-        hipLaunchKernelGGL((k_gemm<false, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, nullptr); break;
+        hipLaunchKernelGGL((k_gemm<false, false, true>), g, b, lds, h->cs, pr, L.count, tl, h->dinfo, L.ticket); break;
     }
   }
   DCHK_HIP(h, hipGetLastError());
@@ -1534,7 +1540,7 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
   DCHK(dalloc(h, &h->dinvdelta, (size_t)d, &h->shared_bytes));
   // local ranks and their sweep buffers
   build_groups(h);
-  DCHK(dalloc(h, &h->dq, 3 * (size_t)h->NB, &h->shared_bytes));
+  DCHK(dalloc(h, &h->dq, 4 * (size_t)h->NB, &h->shared_bytes));
   const int NT = h->NB + h->NA;
   h->panel_sz = (size_t)NT * TILE * TILE * h->wmax;
   // the group all-gather's segment: W column blocks of the most tile rows below the group
@@ -1617,7 +1623,7 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
       DCHK_HIP(h, hipMemsetAsync(R.X, 0, (size_t)R.ld * NB * TILE * sizeof(double), h->stream));
   }
   DCHK(kbuild(h, kernel, nu, s2, rscale));
-  DCHK_HIP(h, hipMemsetAsync(h->dq, 0, 3 * (size_t)NB * sizeof(int), h->stream));
+  DCHK_HIP(h, hipMemsetAsync(h->dq, 0, 4 * (size_t)NB * sizeof(int), h->stream));
   DCHK(group_sweep(h));
   // P = 1: the sweep's factors stored L and the leaf inverses only (flag mode): the
   // TRTRI's leaves X(t, t) are assembled here for every diagonal tile at once

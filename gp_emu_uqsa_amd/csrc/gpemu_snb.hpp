@@ -60,10 +60,13 @@ struct SnbArgs {
   double* T2g;          // 32 x 33: T2 (row k, column p) from workgroup 0
   double* Xscr;         // 128 x 128: db_factor_invert's own X stores (read by nobody)
   double* small;        // out (pinned host memory): Gram (P x P) | log|L(k,k)| (NB) | failed
-                        // column | (d + 3) | Q not PD | the helpers' partial sums (SNB_NH x 64)
+                        // column | (d + 3) | Q not PD | the helpers' partial sums (SNB_NH x 64,
+                        // slot 63 of each: the call's tag once the helper's sums are in)
   int* sync;            // [0] hc, [1] mf (count up over calls)
-  int* abort_flag;      // zero on entry
+  int* abort_flag;      // zero on entry; a wait that runs out raises it (GEMM_WAIT_TIMEOUT)
   int n, np, NB, d, P, want_grad, mucm;
+  int dbg_skip;         // dev switch (tests): this helper gives up its first wait; else -1
+  double tag;           // this call's tag (never repeats in a context) for the helpers' sums
   int hcb, mfb;         // the counters' values before this call (hc in phases)
   double s2, coff, cdiag, rscale;
   double invd[32];
@@ -110,8 +113,11 @@ __device__ void snb_helper(const SnbArgs& a, double* lds) {
     SNB_TH(ph);
     ++ph;
   };
+  // (a wait that runs out raises the abort flag: every other waiter stops, workgroup 0
+  // reports the call as failed, and this helper's sums never carry the call's tag)
+  const bool skip = (int)blockIdx.x - 1 == a.dbg_skip;
   auto wait_hc = [&]() { return tiny_wait(&a.sync[0], (a.hcb + ph) * SNB_NH, a.abort_flag, st) == 1; };
-  auto wait_mf = [&](int v) { return tiny_wait(&a.sync[1], a.mfb + v, a.abort_flag, st) == 1; };
+  auto wait_mf = [&](int v) { return tiny_wait(&a.sync[1], a.mfb + v, a.abort_flag, st, skip && v == 1) == 1; };
   // the scaled points (k_scale_points' product) staged in LDS once per workgroup (rows of
   // DM + 1 doubles, zero past d and n): the K-build's and the contraction's coordinates
   double* xs = lds + 64 + 4 * 16 * 33;   // (past st, red and the W phase's Y rows)
@@ -379,6 +385,7 @@ __device__ void snb_helper(const SnbArgs& a, double* lds) {
   // this helper's partial sums straight to the host, which adds them in helper order (no
   // cross-workgroup pass on the kernel's tail)
   if (tid < d + 3) a.small[P * P + NB + 1 + d + 4 + h * 64 + tid] = red[4 * (DM + 3) + tid];
+  if (tid == 0) a.small[P * P + NB + 1 + d + 4 + h * 64 + 63] = a.tag;
 }
 
 template <int DM>
@@ -401,11 +408,10 @@ static __global__ void __launch_bounds__(256) k_snb(SnbArgs a) {
     // (helper phases up to update k - 1: the K-build, a panel and an update per step, and with
     // the gradient the two X-row phases of steps 1 .. k - 2)
     const int upd = 1 + 2 * k + (a.want_grad ? 2 * max(0, k - 2) : 0);
-    if (tiny_wait(&a.sync[0], (a.hcb + upd) * SNB_NH, nullptr, st) != 1) {
-      if (tid == 0) {
-        a.small[P * P + NB] = -1.0;
-        if (a.abort_flag) atomicCAS(a.abort_flag, 0, GEMM_WAIT_TIMEOUT);
-      }
+    if (tiny_wait(&a.sync[0], (a.hcb + upd) * SNB_NH, a.abort_flag, st) != 1) {
+      // (a helper's wait ran out, or this one did: the abort flag is up either way; only
+      // workgroup 0 itself raises it otherwise, after this loop)
+      if (tid == 0) a.small[P * P + NB] = -1.0;
       return;
     }
     const long long c0 = 128ll * k;
@@ -457,8 +463,10 @@ static __global__ void __launch_bounds__(256) k_snb(SnbArgs a) {
   }
   // the Gram of Z = L^-1 [f H] (Z^T from the last panel) out of LDS
   // (helper phases up to the last panel: as above, and the X rows of steps 1 .. NB - 2)
-  if (tiny_wait(&a.sync[0], (a.hcb + 2 * NB + (a.want_grad ? 2 * max(0, NB - 2) : 0)) * SNB_NH, a.abort_flag, st) != 1)
+  if (tiny_wait(&a.sync[0], (a.hcb + 2 * NB + (a.want_grad ? 2 * max(0, NB - 2) : 0)) * SNB_NH, a.abort_flag, st) != 1) {
+    if (tid == 0) a.small[P * P + NB] = -1.0;   // (never the previous call's Gram as a success)
     return;
+  }
   SNB_T(16);
   // Z^T (P x np) into LDS, rows of np + 1 doubles (the MFMA's 16 operand rows on distinct
   // banks): every load of a thread in flight, then the stores

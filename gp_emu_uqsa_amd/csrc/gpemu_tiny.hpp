@@ -57,7 +57,8 @@ struct TinyArgs {
   double* Xo;           // out: X = L^-1 (ld 128, zero upper)
   double* Z;            // out: Z = L^-1 [f H] (ld 128, P columns)
   double* small;        // out (pinned host memory): Gram (P x P) | log|L| | failed column |
-                        // (d + 3) | Q not PD | the helpers' partial sums (TINY_NH x 64)
+                        // (d + 3) | Q not PD | the helpers' partial sums (TINY_NH x 64,
+                        // slot 63 of each: the call's tag once the helper's sums are in)
   double* K;            // the helpers' K-build in the block-packed image's layout; L's buffer
   double* Xp;           // X's LDS image (block-packed, 36 x DB_BS doubles)
   double* Wg;           // W for the helpers (128 x 32, row-major)
@@ -66,6 +67,8 @@ struct TinyArgs {
   int* abort_flag;      // the failed column (or 1: Q not positive definite); zero on entry
   int ek, eg;           // this call's ordinal among all calls / gradient calls since the zeroing
   int n, d, P, want_grad, mucm;
+  int dbg_skip;         // dev switch (tests): this helper gives up its first wait; else -1
+  double tag;           // this call's tag (never repeats in a context) for the helpers' sums
   double s2, coff, cdiag, rscale;
   double invd[32];
 };
@@ -110,15 +113,21 @@ __device__ __forceinline__ void tiny_signal(int* p, int v) {
   }
 }
 // one lane polls until *p >= want (1) or the launch aborted (2); 0 after ~1 s (never
-// expected); the result in *st for every thread after the barrier
-__device__ __forceinline__ int tiny_wait(const int* p, int want, const int* abort_flag, int* st) {
+// expected: the waiter then raises the abort flag itself, so every other waiter of the
+// launch stops at its next poll instead of running out its own budget); the result in *st
+// for every thread after the barrier.  The two words are loaded together each poll.
+// skip (the dev switch GPEMU_DEBUG_SKIP_WAIT, tests only): give up at once, as a timeout.
+__device__ __forceinline__ int tiny_wait(const int* p, int want, int* abort_flag, int* st, bool skip = false) {
   if (threadIdx.x == 0) {
     int v = 0;
-    for (long it = 0; it < (1l << 22); ++it) {
-      if (tiny_ldi(p) >= want) { v = 1; break; }
-      if (abort_flag && tiny_ldi(abort_flag)) { v = 2; break; }
+    for (long it = skip ? (1l << 22) : 0; it < (1l << 22); ++it) {
+      const int x = tiny_ldi(p);
+      const int ab = abort_flag ? tiny_ldi(abort_flag) : 0;
+      if (x >= want) { v = 1; break; }
+      if (ab) { v = 2; break; }
       __builtin_amdgcn_s_sleep(2);
     }
+    if (v == 0 && abort_flag) atomicCAS(abort_flag, 0, GEMM_WAIT_TIMEOUT);
     *st = v;
   }
   __syncthreads();
@@ -274,7 +283,7 @@ __device__ void tiny_helper(const TinyArgs& a, double* lds) {
   int* st = reinterpret_cast<int*>(lds);
   const auto rXp = tiny_rsrc(a.Xp), rWg = tiny_rsrc(a.Wg);
   // M(bi, bj) = X^T X (as soon as workgroup 0 has published X) - W W^T (once W is out)
-  if (tiny_wait(&a.sync[1], a.eg, a.abort_flag, st) != 1) return;
+  if (tiny_wait(&a.sync[1], a.eg, a.abort_flag, st, h == a.dbg_skip) != 1) return;
   tiny_d4 acc = {0.0, 0.0, 0.0, 0.0};
   {
     double av[8][4], bv[8][4];   // X's blocks (kb, bi) and (kb, bj): 4 operands per lane each
@@ -334,8 +343,10 @@ __device__ void tiny_helper(const TinyArgs& a, double* lds) {
   }
   double* red = lds + 8;   // (past st)
   sm.reduce(d, red, red + 4 * (DM + 3));
-  // this helper's partial sums straight to the host, which adds the nine in helper order
+  // this helper's partial sums straight to the host, which adds the nine in helper order,
+  // then the call's tag (the host refuses a helper whose slot does not carry it)
   if (tid < d + 3) a.small[P * P + 2 + d + 4 + h * 64 + tid] = red[4 * (DM + 3) + tid];
+  if (tid == 0) a.small[P * P + 2 + d + 4 + h * 64 + 63] = a.tag;
 #ifdef TINY_TIMING
   if (tid == 0) atomicMax(&tiny_tsc[7], wall_clock64());
 #endif
@@ -373,11 +384,8 @@ static __global__ void __launch_bounds__(256) k_tiny(TinyArgs a) {
   }, [&](int e, double v) { r1[(e / TINY_DM) * ZP + e % TINY_DM] = v; });
   TINY_T(1);
   {
-    if (tiny_wait(&a.sync[0], TINY_NH * a.ek, nullptr, reinterpret_cast<int*>(zs)) != 1) {   // (never expected)
-      if (tid == 0) {
-        a.small[P * P + 1] = -1.0;
-        if (a.abort_flag) atomicCAS(a.abort_flag, 0, GEMM_WAIT_TIMEOUT);
-      }
+    if (tiny_wait(&a.sync[0], TINY_NH * a.ek, a.abort_flag, reinterpret_cast<int*>(zs)) != 1) {   // (never expected)
+      if (tid == 0) a.small[P * P + 1] = -1.0;   // (tiny_wait raised the abort flag)
       return;
     }
   }

@@ -135,7 +135,7 @@ def test_scale_point_4096(ctx):
     ctx.set_data(X, f, H)
     llh, grad, _ = ctx.objective(orc.GP4ML, orc.STD, z["hp"])
     assert abs(llh - float(z["llh"])) <= 1e-10 * abs(float(z["llh"])), (llh, float(z["llh"]))
-    ok, err = _grad_ok(grad, z["grad"], tol=1e-6)
+    ok, err = _grad_ok(grad, z["grad"])   # (1e-7 of scale, as every other size)
     assert ok, (err, grad, z["grad"])
 
 

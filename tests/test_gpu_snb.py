@@ -1,5 +1,5 @@
-"""The objective for 128 < n <= 512 (gpemu_snb.hpp: one launch, a factor workgroup and 32
-helper workgroups) against the oracle and against the general path of the same library
+"""The objective for 128 < n <= 512 (gpemu_snb.hpp: one launch, a factor workgroup and
+SNB_NH = 48 helper workgroups) against the oracle and against the general path of the same library
 (GPEMU_TINY=0), for the variants the general path's golden tests cover: gp4ml / MUCM, std /
 alt-nugget kernel with per-point r, fitted / fixed nugget, the std kernel's set_r sigma
 gradient, 2 to 4 tiles with ragged last tiles, d from 1 to 30, q + 1 up to 32; a non-positive-
