@@ -25,6 +25,7 @@
 #include "gpemu_small.hpp"
 #include "gpemu_tiny.hpp"
 #include "gpemu_snb.hpp"
+#include "gpemu_ozaki.hpp"
 
 using namespace gpe;
 
@@ -151,6 +152,15 @@ struct gpe_ctx {
   int snb_hc = 0, snb_mf = 0;   // k_snb's counters (dinfo[8..9]; abort dinfo[10])
   bool snb_dirty = true;
   double onel_tag = 0.0;          // the one-launch objectives' call tag (never repeats)
+  // the objective's A^-1 on the int8 matrix cores (gpemu_ozaki.hpp): GPEMU_OZAKI=0 keeps the
+  // fp64 LAUUM; GPEMU_OZAKI_MODULI sets the number of moduli (default 16: 53-bit operands)
+  int oz_on = 1, oz_nmod = OZ_MAXMOD;
+  int oz_np2 = 0, oz_list_len = 0;
+  OzConst oz_c{};
+  int8_t* dozp = nullptr;         // the N int8 planes of X (lower 256-column panels)
+  int8_t* dozr = nullptr;         // the N residue bytes of every lower 256-tile entry
+  int* dozx = nullptr;            // per-column exponents
+  unsigned* dozl = nullptr;       // k_oz_gemm's tile list
   int dbg_skip_wait = -1;         // GPEMU_DEBUG_SKIP_WAIT (tests): a helper gives up its first wait
   size_t small_cap = 0;
 
@@ -1533,6 +1543,8 @@ gpe_ctx* gpe_create(int32_t device) {
     if (const char* ep = std::getenv("GPEMU_CHOL_PRIO")) c->chol_prio = std::atoi(ep) != 0;
     if (const char* et = std::getenv("GPEMU_TINY")) c->tiny = std::atoi(et) != 0;
     if (const char* ed = std::getenv("GPEMU_DEBUG_SKIP_WAIT")) c->dbg_skip_wait = std::atoi(ed);
+    if (const char* eo = std::getenv("GPEMU_OZAKI")) c->oz_on = std::atoi(eo) != 0;
+    if (const char* em = std::getenv("GPEMU_OZAKI_MODULI")) c->oz_nmod = std::max(8, std::min(OZ_MAXMOD, std::atoi(em)));
     if (const char* es = std::getenv("GPEMU_POTRF_SB")) {
       c->potrf_sb = std::max(1, std::min(8, std::atoi(es)));
       if (const char* colon = std::strchr(es, ':')) c->potrf_sb_min = std::max(0, std::atoi(colon + 1));
@@ -1622,6 +1634,10 @@ void gpe_destroy(gpe_ctx* c) {
     if (F->tcnt) hipFree(F->tcnt);
   }
   if (c->tr.tflags) hipFree(c->tr.tflags);
+  if (c->dozp) hipFree(c->dozp);
+  if (c->dozr) hipFree(c->dozr);
+  if (c->dozx) hipFree(c->dozx);
+  if (c->dozl) hipFree(c->dozl);
   if (c->tr.Faug) hipFree(c->tr.Faug);
   if (c->aux.tflags) hipFree(c->aux.tflags);
   if (c->dprobs) hipFree(c->dprobs);
@@ -1954,6 +1970,97 @@ int snb_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_hp
   return GPE_OK;
 }
 
+
+// ---------------------------------------------------------------- A^-1 on the int8 cores
+// (gpemu_ozaki.hpp).  Used by the objective's gradient for OZ_MIN_NP <= n_pad <= OZ_MAX_NP:
+// below, the fp64 LAUUM is a few short launches; above, the planes and residues (each
+// N bytes per lower entry) would take more than ~13 GB per context.
+constexpr int OZ_MIN_NP = 2048, OZ_MAX_NP = 32768;
+bool oz_use(const gpe_ctx* c) { return c->oz_on && c->n_pad >= OZ_MIN_NP && c->n_pad <= OZ_MAX_NP; }
+
+// moduli and reconstruction constants for operand sums of length up to np2
+OzConst oz_consts(int nmod, int np2) {
+  static const int mods[OZ_MAXMOD] = {256, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217, 211, 199, 197, 193, 191};
+  OzConst k{};
+  k.nmod = nmod;
+  double log2M = 0.0, Md = 1.0;
+  for (int l = 0; l < nmod; ++l) {
+    log2M += std::log2((double)mods[l]);
+    Md *= (double)mods[l];
+  }
+  k.Md = Md;
+  // |C'| <= np2 2^(2 beta) < M / 2
+  k.beta = std::min(53, (int)std::floor((log2M - 1.0 - std::log2((double)np2) - 1e-9) / 2.0));
+  for (int l = 0; l < nmod; ++l) {
+    const int m = mods[l];
+    k.m[l] = m;
+    k.c16[l] = 65536 % m;
+    k.inv[l] = 1.0f / (float)m;
+    long long Mm = 1;   // (M / m) mod m
+    for (int j = 0; j < nmod; ++j)
+      if (j != l) Mm = (Mm * (mods[j] % m)) % m;
+    int y = 1;          // its inverse mod m
+    while ((Mm * y) % m != 1) ++y;
+    // y / m = rhi + rlo, rhi on the 2^-41 grid (exact products and sums in k_oz_crt)
+    const long long num = (long long)y << 41;
+    const long long Q = num / m, R = num - Q * m;
+    k.rhi[l] = std::ldexp((double)Q, -41);
+    k.rlo[l] = std::ldexp((double)R / (double)m, -41);
+  }
+  return k;
+}
+
+// planes, residues, exponents and the tile list for this n_pad
+int oz_prepare(gpe_ctx* c) {
+  const int np2 = (int)(((c->n_pad + OZ_T - 1) / OZ_T) * OZ_T);
+  if (np2 == c->oz_np2 && c->oz_c.nmod == c->oz_nmod) return GPE_OK;
+  c->oz_np2 = 0;
+  const int NT2 = np2 / OZ_T;
+  const size_t planes = (size_t)oz_plane_bytes(np2) * c->oz_nmod;
+  const size_t resid = (size_t)NT2 * (NT2 + 1) / 2 * OZ_T * OZ_T * c->oz_nmod;
+  CHK(dalloc(c, &c->dozp, planes));
+  CHK(dalloc(c, &c->dozr, resid));
+  CHK(dalloc(c, &c->dozx, (size_t)np2));
+  // tile rows longest first (K = np2 - 256 ti), greedily binned by work into 8 XCD bins,
+  // interleaved position by position (bin = position % 8); bins padded to one length
+  std::vector<std::vector<unsigned>> bins(8);
+  std::vector<double> load(8, 0.0);
+  for (int ti = 0; ti < NT2; ++ti) {
+    const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    load[x] += (double)(ti + 1) * (np2 - OZ_T * ti);
+    for (int tj = 0; tj <= ti; ++tj) bins[x].push_back(((unsigned)ti << 16) | (unsigned)tj);
+  }
+  size_t longest = 0;
+  for (auto& b : bins) longest = std::max(longest, b.size());
+  std::vector<unsigned> list(8 * longest, 0xffffffffu);
+  for (int x = 0; x < 8; ++x)
+    for (size_t q = 0; q < bins[x].size(); ++q) list[8 * q + x] = bins[x][q];
+  CHK(dalloc(c, &c->dozl, list.size()));
+  HIPCHK(c, hipMemcpy(c->dozl, list.data(), list.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+  c->oz_list_len = (int)list.size();
+  c->oz_c = oz_consts(c->oz_nmod, np2);
+  c->oz_np2 = np2;
+  return GPE_OK;
+}
+
+// A^-1 = X^T X (lower 128-tiles) of the workspace's X = L^-1 (F.B) into F.A
+int lauum_ozaki(gpe_ctx* c, Fact& F) {
+  CHK(oz_prepare(c));
+  const int np = (int)F.n_pad, np2 = c->oz_np2, NT2 = np2 / OZ_T;
+  const OzConst& k = c->oz_c;
+  const long long pb = oz_plane_bytes(np2), rb = (long long)NT2 * (NT2 + 1) / 2 * OZ_T * OZ_T;
+  hipLaunchKernelGGL(k_oz_colexp, dim3((np2 + 3) / 4), dim3(256), 0, c->stream, F.B, (long long)F.n_pad, np, np2,
+                     k.beta, c->dozx);
+  hipLaunchKernelGGL(k_oz_split, dim3(np2, (np2 + 4095) / 4096), dim3(256), 0, c->stream, F.B, (long long)F.n_pad, np,
+                     np2, c->dozx, c->dozp, pb, k);
+  hipLaunchKernelGGL(k_oz_gemm, dim3(k.nmod * c->oz_list_len), dim3(256), OZ_LDS, c->stream, c->dozp, pb, np2,
+                     c->dozl, c->oz_list_len, c->dozr, rb, k);
+  hipLaunchKernelGGL(k_oz_crt, dim3(NT2 * (NT2 + 1) / 2 * 16), dim3(256), 0, c->stream, c->dozr, rb, c->dozx, np, F.A,
+                     (long long)F.n_pad, k);
+  HIPCHK(c, hipGetLastError());
+  return GPE_OK;
+}
+
 int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp, int32_t n_hp,
                   double nu_fixed, int32_t want_grad, double* llh_out, double* grad_out,
                   double* sigma2_out) {
@@ -2001,7 +2108,7 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
   HIPCHK(c, hipMemcpyAsync(c->hpin + P * P + NBt, c->dinfo, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipEventRecord(c->ev_host, c->stream));
   ev_rec(c, 4);
-  if (want_grad) CHK(lauum(c, c->tr));
+  if (want_grad) CHK(oz_use(c) ? lauum_ozaki(c, c->tr) : lauum(c, c->tr));
   ev_rec(c, 5);
   HIPCHK(c, hipEventSynchronize(c->ev_host));
   std::vector<double> G(c->hpin, c->hpin + (size_t)P * P);

@@ -1,0 +1,279 @@
+// gpemu_ozaki.hpp -- A^-1 = X^T X (the LAUUM of the objective's gradient, X = L^-1 lower
+// triangular) on the int8 matrix cores, exact integer products reconstructed to fp64 by the
+// Chinese remainder theorem (the Ozaki scheme II construction: Ozaki, Uchino, Imamura 2024).
+//
+// Why: on gfx950 the 32 x 32 x 32 i8 MFMA does 32768 integer multiply-adds per 32 cycles per
+// SIMD against 2048 flops per 64 cycles for the 16 x 16 x 4 f64 MFMA: 32 x the fp64 rate per
+// clock (measured on random operands, where the chip holds a lower clock: 2.2-2.4 POPS against
+// the fp64 GEMM's 70 TF/s, tools/hip/i8_probe.hip).  With N = 16 moduli the product is exact
+// and the operands carry 53 bits: the result has fp64 accuracy.
+//
+// The arithmetic, per column j of X (the rows of both operands of X^T X):
+//   e_j     = 52 - ilogb(max_k |X(k,j)|), so X'(k,j) = rint(X(k,j) 2^e_j) is an integer with
+//             |X'| <= 2^53 (beta bits: 53, or fewer for n > 16384, see oz_beta on the host);
+//   C'(i,j) = sum_k X'(k,i) X'(k,j), exact, |C'| <= n 2^(2 beta) < M / 2 (M = prod m_l);
+//   for each modulus m_l (pairwise coprime, <= 256): X'_l = X' mod m_l in [-128, 127]
+//             (int8), C'_l = X'_l^T X'_l on the i8 MFMA (int32, exact: |.| <= n 2^14 < 2^31),
+//             c_l = C'_l mod m_l (centred, stored as one byte);
+//   C'/M    = sum_l c_l y_l / m_l  (mod 1), y_l = (M / m_l)^-1 mod m_l: the centred fraction
+//             v of that sum, formed exactly on a 2^-41 grid (hi parts) plus the lo parts,
+//             gives C' = v M and A^-1(i,j) = v M 2^-(e_i + e_j).
+// Kernels: k_oz_colexp (e_j), k_oz_split (X -> N int8 planes, lower 256-column panels),
+// k_oz_gemm (grouped over moduli: 256 x 256 tiles of the lower triangle, K from the tile
+// row's diagonal block), k_oz_crt (N residue bytes per element -> fp64, lower 128-tiles).
+#pragma once
+
+namespace gpe {
+
+constexpr int OZ_T = 256;                  // output tile, and the planes' column panels
+constexpr int OZ_SK = 64;                  // k (bytes) per LDS stage: two 32-deep k-steps
+constexpr int OZ_NBUF = 4;                 // stage ring (loads issued 3 stages ahead)
+constexpr int OZ_OPND = OZ_T * OZ_SK;      // one operand's stage image (16 KB)
+constexpr int OZ_LDS = OZ_NBUF * 2 * OZ_OPND;   // 128 KB: one workgroup per CU
+constexpr int OZ_MAXMOD = 16;
+
+// moduli (pairwise coprime; the odd ones <= 253 so a rounded centred residue stays in int8)
+// and the reconstruction constants (host: oz_consts)
+struct OzConst {
+  int m[OZ_MAXMOD];        // modulus
+  int c16[OZ_MAXMOD];      // 2^16 mod m
+  float inv[OZ_MAXMOD];    // 1 / m
+  double rhi[OZ_MAXMOD];   // y / m rounded to a multiple of 2^-41 (y = (M / m)^-1 mod m)
+  double rlo[OZ_MAXMOD];   // y / m - rhi
+  double Md;               // M = prod m (rounded)
+  int nmod;
+  int beta;                // operand bits
+};
+
+typedef int oz_v4i __attribute__((ext_vector_type(4)));
+typedef int oz_v16i __attribute__((ext_vector_type(16)));
+
+// byte offset of column-panel cb in the planes: panel cb holds columns [256 cb, 256 cb + 256),
+// rows [256 cb, np2), column-major with ld np2 - 256 cb
+__host__ __device__ __forceinline__ long long oz_panel_off(int cb, int np2) {
+  return (long long)OZ_T * ((long long)cb * np2 - (long long)OZ_T * cb * (cb - 1) / 2);
+}
+__host__ __device__ __forceinline__ long long oz_plane_bytes(int np2) { return oz_panel_off(np2 / OZ_T, np2); }
+
+// e_j for every column j < np2 (one wave per column, rows k >= j; columns past np: 0)
+static __global__ void __launch_bounds__(256) k_oz_colexp(const double* __restrict__ X, long long ldx, int np,
+                                                          int np2, int beta, int* __restrict__ ex) {
+  const int lane = threadIdx.x & 63, j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= np2) return;
+  double mx = 0.0;
+  if (j < np)
+    for (int k = j + lane; k < np; k += 64) mx = fmax(mx, fabs(X[k + (long long)j * ldx]));
+  for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off, 64));
+  if (lane == 0) ex[j] = mx > 0.0 ? (beta - 1) - ilogb(mx) : 0;
+}
+
+// X -> the N int8 planes: thread = 16 consecutive rows of one column; entries above the
+// diagonal (and past np) are zero
+static __global__ void __launch_bounds__(256) k_oz_split(const double* __restrict__ X, long long ldx, int np,
+                                                         int np2, const int* __restrict__ ex, int8_t* __restrict__ planes,
+                                                         long long plane_bytes, OzConst cst) {
+  const int j = blockIdx.x;
+  const int cb = j / OZ_T, r0 = cb * OZ_T;
+  const int k0 = r0 + 16 * ((int)blockIdx.y * 256 + (int)threadIdx.x);
+  if (k0 >= np2) return;
+  const int e = ex[j];
+  double xs[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int k = k0 + u;
+    const double v = (k >= j && k < np && j < np) ? X[k + (long long)j * ldx] : 0.0;
+    xs[u] = rint(ldexp(v, e));   // |.| <= 2^beta, exact integer
+  }
+  const long long ld = np2 - r0;
+  int8_t* dst = planes + oz_panel_off(cb, np2) + (long long)(j - r0) * ld + (k0 - r0);
+  for (int l = 0; l < cst.nmod; ++l) {
+    const double m = (double)cst.m[l], im = 1.0 / m;
+    unsigned w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      // centred residue: x - m rint(x / m) is exact (|x| <= 2^53, the product q m an integer
+      // below 2^53), |.| <= m / 2 + 1; the m = 256 one wraps into int8 congruently
+      const double q = rint(xs[u] * im);
+      int r = (int)fma(-q, m, xs[u]);
+      r = r > 127 ? r - cst.m[l] : (r < -128 ? r + cst.m[l] : r);
+      w[u >> 2] |= ((unsigned)r & 0xffu) << (8 * (u & 3));
+    }
+    *reinterpret_cast<oz_v4i*>(dst + (long long)l * plane_bytes) = oz_v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+  }
+}
+
+__device__ __forceinline__ void oz_glds16(const int8_t* src, int8_t* dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+template <int N> __device__ __forceinline__ void oz_vmwait() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); }
+
+// One 256 x 256 tile (ti >= tj) of C'_l = X'_l^T X'_l for modulus l, K from 256 ti to np2.
+// blockIdx.x = l * list_len + position (the list's length a multiple of 8, so position % 8
+// is the XCD under round-robin dispatch; entries 0xffffffff pad the bins).  4 waves of
+// 128 x 128 (4 x 4 blocks of the 32 x 32 x 32 i8 MFMA, operands swapped so lane & 31 runs
+// along the tile's rows); stages of 64 k through a 4-deep LDS ring filled by direct
+// global -> LDS loads.  The stage image of each operand is [row][64 B] with granule g of row
+// r at slot g ^ ((r >> 2) & 3): conflict-free for ds_read_b128's lane groups.  Output: the
+// centred residue of every entry, one byte, in the MFMA's own order (lane l of block b of
+// wave w: 16 bytes at ((w 16 + b) 64 + l) 16 of the tile's 64 KB).
+static __global__ void __launch_bounds__(256, 1) k_oz_gemm(const int8_t* __restrict__ planes, long long plane_bytes,
+                                                           int np2, const unsigned* __restrict__ list, int list_len,
+                                                           int8_t* __restrict__ res, long long res_bytes, OzConst cst) {
+  extern __shared__ __attribute__((aligned(16))) double lds_d[];
+  int8_t* lds = reinterpret_cast<int8_t*>(lds_d);
+  const int l = (int)blockIdx.x / list_len;
+  const unsigned ent = list[(int)blockIdx.x - l * list_len];
+  if (ent == 0xffffffffu) return;
+  const int ti = (int)(ent >> 16), tj = (int)(ent & 0xffffu);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = (wave >> 1) * 128, wn = (wave & 1) * 128;
+  const int8_t* P = planes + (long long)l * plane_bytes;
+  // operand rows: columns of X in panels ti (A) and tj (B); k from 256 ti
+  const long long lda = np2 - OZ_T * ti, ldb = np2 - OZ_T * tj;
+  const int kp = (lane & 3) ^ ((lane >> 4) & 3);
+  const int8_t* sa = P + oz_panel_off(ti, np2) + (long long)(16 * wave + (lane >> 2)) * lda + 16 * kp;
+  const int8_t* sb = P + oz_panel_off(tj, np2) + (long long)(16 * wave + (lane >> 2)) * ldb +
+                     (long long)OZ_T * (ti - tj) + 16 * kp;
+  auto stage = [&](int s) {
+    int8_t* As = lds + (s & (OZ_NBUF - 1)) * 2 * OZ_OPND;
+    int8_t* Bs = As + OZ_OPND;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int w = wave + 4 * p;   // wave-instruction index: rows 16 w .. 16 w + 15
+      oz_glds16(sa + (long long)p * 64 * lda + (long long)s * OZ_SK, As + 16 * w * OZ_SK);
+      oz_glds16(sb + (long long)p * 64 * ldb + (long long)s * OZ_SK, Bs + 16 * w * OZ_SK);
+    }
+  };
+  oz_v16i acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = oz_v16i{};
+  const int ns = (np2 - OZ_T * ti) / OZ_SK;
+  const int r32 = lane & 31, h = lane >> 5, sw = (r32 >> 2) & 3;
+  // the 8 fragments (4 of A, 4 of B) of k-step ks of stage s
+  auto frags = [&](int s, int ks, oz_v4i (&af)[4], oz_v4i (&bf)[4]) {
+    const int8_t* As = lds + (s & (OZ_NBUF - 1)) * 2 * OZ_OPND;
+    const int8_t* Bs = As + OZ_OPND;
+    const int slot = ((2 * ks + h) ^ sw) * 16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const oz_v4i*>(As + (wm + 32 * i + r32) * OZ_SK + slot);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const oz_v4i*>(Bs + (wn + 32 * j + r32) * OZ_SK + slot);
+  };
+  auto mfmas = [&](const oz_v4i (&af)[4], const oz_v4i (&bf)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(bf[j], af[i], acc[i][j], 0, 0, 0);
+  };
+  // wait until stage s has landed (this wave's loads; the barrier makes it every wave's):
+  // the stages issued after it, up to s + 3, may stay in flight (loads retire in order)
+  auto wait_stage = [&](int s) {
+    const int later = min(ns - 1, s + 2) - s;
+    if (later >= 2) oz_vmwait<16>();
+    else if (later == 1) oz_vmwait<8>();
+    else oz_vmwait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  // Software pipeline, one barrier per stage: the next k-step's fragments are read while the
+  // current k-step's 16 MFMAs issue.  Stage s + 3 goes into the buffer of stage s - 1, whose
+  // last fragment reads every wave finished before the barrier of stage s.
+  for (int s = 0; s < min(ns, 3); ++s) stage(s);
+  oz_v4i ca[4], cb[4], na[4], nb[4];
+  wait_stage(0);
+  if (ns > 3) stage(3);
+  frags(0, 0, ca, cb);
+  for (int s = 0; s < ns; ++s) {
+    // this k-step's MFMAs with the next k-step's 8 fragment reads between the first 8 (an
+    // MFMA leaves the wave's issue free for most of its 32 cycles; the reads issued ahead
+    // of the MFMAs made the first MFMA wait for all of them: lgkmcnt(0))
+    mfmas(ca, cb);
+    frags(s, 1, na, nb);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one LDS read
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + 1 < ns) {
+      wait_stage(s + 1);
+      if (s + 4 < ns) stage(s + 4);
+      frags(s + 1, 0, ca, cb);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas(na, nb);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // centred residues: t = (acc >> 16) (2^16 mod m) + (acc & 0xffff) is exact in fp32
+  // (|t| < 2^20), q = rint(t / m) to within 3e-4, r = t - q m in [-m/2 - 1, m/2 + 1];
+  // m = 256: the low byte itself
+  const int m = cst.m[l], c16 = cst.c16[l];
+  const float inv = cst.inv[l];
+  int8_t* out = res + (long long)l * res_bytes + ((long long)ti * (ti + 1) / 2 + tj) * (OZ_T * OZ_T) +
+                ((long long)(wave * 16) * 64 + lane) * 16;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      unsigned w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int a = acc[i][j][r];
+        int v = a;
+        if (m != 256) {
+          const int t = __mul24(a >> 16, c16) + (a & 0xffff);
+          const int q = (int)rintf((float)t * inv);
+          v = t - __mul24(q, m);
+        }
+        w[r >> 2] |= ((unsigned)v & 0xffu) << (8 * (r & 3));
+      }
+      *reinterpret_cast<oz_v4i*>(out + (long long)(4 * i + j) * 64 * 16) = oz_v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+    }
+}
+
+// fp64 entries from the residues: thread u of tile t (16 workgroups per tile) = wave
+// u / 1024, block (u / 64) % 16, lane u % 64 of k_oz_gemm's order, 16 entries; lower
+// 128-tiles within np only, into C (ld ldc)
+static __global__ void __launch_bounds__(256) k_oz_crt(const int8_t* __restrict__ res, long long res_bytes,
+                                                       const int* __restrict__ ex, int np, double* __restrict__ C,
+                                                       long long ldc, OzConst cst) {
+  const int t = (int)blockIdx.x >> 4;
+  const int u = ((int)blockIdx.x & 15) * 256 + (int)threadIdx.x;
+  int ti = 0;
+  while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+  const int tj = t - ti * (ti + 1) / 2;
+  const int wave = u >> 10, blk = (u >> 6) & 15, lane = u & 63;
+  const int i = blk >> 2, j = blk & 3;
+  const int gm = OZ_T * ti + (wave >> 1) * 128 + 32 * i + (lane & 31);
+  const int gn0 = OZ_T * tj + (wave & 1) * 128 + 32 * j + 4 * (lane >> 5);
+  if (gm >= np || gn0 >= np) return;
+  double shi[16], slo[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) shi[r] = slo[r] = 0.0;
+  const int8_t* src = res + (long long)t * (OZ_T * OZ_T) + (long long)u * 16;
+  for (int l = 0; l < cst.nmod; ++l) {
+    const oz_v4i w = *reinterpret_cast<const oz_v4i*>(src + (long long)l * res_bytes);
+    const double rh = cst.rhi[l], rl = cst.rlo[l];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const double cv = (double)(int)(int8_t)((unsigned)w[r >> 2] >> (8 * (r & 3)));
+      shi[r] = fma(cv, rh, shi[r]);   // exact: multiples of 2^-41 below 2^11
+      slo[r] = fma(cv, rl, slo[r]);
+    }
+  }
+  const int em = ex[gm];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int gn = gn0 + (r & 3) + 8 * (r >> 2);
+    if (gn >= np || (gm >> 7) < (gn >> 7)) continue;   // lower 128-tiles only
+    const double v = (shi[r] - rint(shi[r])) + slo[r];   // C' / M, centred
+    C[gm + (long long)gn * ldc] = v * ldexp(cst.Md, -(em + ex[gn]));
+  }
+}
+
+}  // namespace gpe
