@@ -2021,15 +2021,29 @@ int oz_prepare(gpe_ctx* c) {
   CHK(dalloc(c, &c->dozp, planes));
   CHK(dalloc(c, &c->dozr, resid));
   CHK(dalloc(c, &c->dozx, (size_t)np2));
-  // tile rows longest first (K = np2 - 256 ti), greedily binned by work into 8 XCD bins,
-  // interleaved position by position (bin = position % 8); bins padded to one length
+  // Blocks of OZ_BR tile rows x OZ_BC tile columns (clipped to the lower triangle), longest K
+  // first, greedily binned by work into 8 XCD bins, interleaved position by position (bin =
+  // position % 8, the XCD under round-robin dispatch), bins padded to one length.  An XCD's
+  // 32 CUs then run one block at a time: its tiles share 4 A panels and 8 B panels (the rows'
+  // K starts differ by at most 3 x 256), where a whole tile row on one XCD shared one A panel
+  // among 32 different B panels (L2 hit rate ~0.5)
+  constexpr int OZ_BR = 4, OZ_BC = 8;
   std::vector<std::vector<unsigned>> bins(8);
   std::vector<double> load(8, 0.0);
-  for (int ti = 0; ti < NT2; ++ti) {
-    const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-    load[x] += (double)(ti + 1) * (np2 - OZ_T * ti);
-    for (int tj = 0; tj <= ti; ++tj) bins[x].push_back(((unsigned)ti << 16) | (unsigned)tj);
-  }
+  for (int r0 = 0; r0 < NT2; r0 += OZ_BR)
+    for (int c0 = 0; c0 <= std::min(NT2 - 1, r0 + OZ_BR - 1); c0 += OZ_BC) {
+      std::vector<unsigned> blk;
+      double w = 0.0;
+      for (int ti = r0; ti < std::min(NT2, r0 + OZ_BR); ++ti)
+        for (int tj = c0; tj < std::min(ti + 1, c0 + OZ_BC); ++tj) {
+          blk.push_back(((unsigned)ti << 16) | (unsigned)tj);
+          w += (double)(np2 - OZ_T * ti);
+        }
+      if (blk.empty()) continue;
+      const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+      load[x] += w;
+      bins[x].insert(bins[x].end(), blk.begin(), blk.end());
+    }
   size_t longest = 0;
   for (auto& b : bins) longest = std::max(longest, b.size());
   std::vector<unsigned> list(8 * longest, 0xffffffffu);
@@ -2051,7 +2065,7 @@ int lauum_ozaki(gpe_ctx* c, Fact& F) {
   const long long pb = oz_plane_bytes(np2), rb = (long long)NT2 * (NT2 + 1) / 2 * OZ_T * OZ_T;
   hipLaunchKernelGGL(k_oz_colexp, dim3((np2 + 3) / 4), dim3(256), 0, c->stream, F.B, (long long)F.n_pad, np, np2,
                      k.beta, c->dozx);
-  hipLaunchKernelGGL(k_oz_split, dim3(np2, (np2 + 4095) / 4096), dim3(256), 0, c->stream, F.B, (long long)F.n_pad, np,
+  hipLaunchKernelGGL(k_oz_split, dim3(np2, (np2 + 256 * OZ_SPLIT_ROWS - 1) / (256 * OZ_SPLIT_ROWS)), dim3(256), 0, c->stream, F.B, (long long)F.n_pad, np,
                      np2, c->dozx, c->dozp, pb, k);
   hipLaunchKernelGGL(k_oz_gemm, dim3(k.nmod * c->oz_list_len), dim3(256), OZ_LDS, c->stream, c->dozp, pb, np2,
                      c->dozl, c->oz_list_len, c->dozr, rb, k);

@@ -67,30 +67,42 @@ static __global__ void __launch_bounds__(256) k_oz_colexp(const double* __restri
   if (lane == 0) ex[j] = mx > 0.0 ? (beta - 1) - ilogb(mx) : 0;
 }
 
-// X -> the N int8 planes: thread = 16 consecutive rows of one column; entries above the
-// diagonal (and past np) are zero
+// X -> the N int8 planes: thread = 8 consecutive rows of one column (a wave reads 4 KB of
+// the column and writes 512 contiguous bytes per plane); entries above the diagonal (and past
+// np) are zero
+constexpr int OZ_SPLIT_ROWS = 8;
 static __global__ void __launch_bounds__(256) k_oz_split(const double* __restrict__ X, long long ldx, int np,
                                                          int np2, const int* __restrict__ ex, int8_t* __restrict__ planes,
                                                          long long plane_bytes, OzConst cst) {
   const int j = blockIdx.x;
   const int cb = j / OZ_T, r0 = cb * OZ_T;
-  const int k0 = r0 + 16 * ((int)blockIdx.y * 256 + (int)threadIdx.x);
+  const int k0 = r0 + OZ_SPLIT_ROWS * ((int)blockIdx.y * 256 + (int)threadIdx.x);
   if (k0 >= np2) return;
   const int e = ex[j];
-  double xs[16];
+  double xs[OZ_SPLIT_ROWS];
+  if (j < np && k0 + OZ_SPLIT_ROWS <= np && k0 >= j) {   // (16-byte loads: k0 is a multiple of 8)
 #pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int k = k0 + u;
-    const double v = (k >= j && k < np && j < np) ? X[k + (long long)j * ldx] : 0.0;
-    xs[u] = rint(ldexp(v, e));   // |.| <= 2^beta, exact integer
+    for (int u = 0; u < OZ_SPLIT_ROWS; u += 2) {
+      const double2 v = *reinterpret_cast<const double2*>(X + k0 + u + (long long)j * ldx);
+      xs[u] = v.x;
+      xs[u + 1] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < OZ_SPLIT_ROWS; ++u) {
+      const int k = k0 + u;
+      xs[u] = (k >= j && k < np && j < np) ? X[k + (long long)j * ldx] : 0.0;
+    }
   }
+#pragma unroll
+  for (int u = 0; u < OZ_SPLIT_ROWS; ++u) xs[u] = rint(ldexp(xs[u], e));   // |.| <= 2^beta, exact integer
   const long long ld = np2 - r0;
   int8_t* dst = planes + oz_panel_off(cb, np2) + (long long)(j - r0) * ld + (k0 - r0);
   for (int l = 0; l < cst.nmod; ++l) {
     const double m = (double)cst.m[l], im = 1.0 / m;
-    unsigned w[4] = {0u, 0u, 0u, 0u};
+    unsigned w[2] = {0u, 0u};
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < OZ_SPLIT_ROWS; ++u) {
       // centred residue: x - m rint(x / m) is exact (|x| <= 2^53, the product q m an integer
       // below 2^53), |.| <= m / 2 + 1; the m = 256 one wraps into int8 congruently
       const double q = rint(xs[u] * im);
@@ -98,7 +110,7 @@ static __global__ void __launch_bounds__(256) k_oz_split(const double* __restric
       r = r > 127 ? r - cst.m[l] : (r < -128 ? r + cst.m[l] : r);
       w[u >> 2] |= ((unsigned)r & 0xffu) << (8 * (u & 3));
     }
-    *reinterpret_cast<oz_v4i*>(dst + (long long)l * plane_bytes) = oz_v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+    *reinterpret_cast<uint2*>(dst + (long long)l * plane_bytes) = make_uint2(w[0], w[1]);
   }
 }
 
