@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <map>
 #include <cmath>
@@ -55,6 +56,8 @@ struct Plan {
   // launches also carrying the augmented row (when the workspace has one)
   std::vector<int> fused, fused_aug;
   std::vector<int> trtri;   // launches in order
+  // per TRTRI level (launches trtri[2 l], trtri[2 l + 1]): its block pairs {t0, h, t1}
+  std::vector<std::vector<std::array<int, 3>>> tri_pairs;
   int lauum = -1;
   bool aug = false;         // fused_aug is built
   // group schedule (the default for a lone evaluation): ONE launch per column group of width >= 2 holding
@@ -72,6 +75,14 @@ struct Plan {
 // diagonal tiles' quadrant counters (G_DQUAD) and the panel tiles' stored-update counters
 // (G_PHALF0)
 constexpr int FACT_FLAG_INTS = 6;
+
+// one TRTRI block pair on the int8 cores (trtri_pair_ozaki): rows of X11 / X22 (Ra / Rb),
+// padded to 256 (Pa / Pb), and its two products' tile lists in dozl
+struct OzTriPair {
+  int t0, h, t1, Ra, Rb, Pa, Pb;
+  long long la_off, lb_off;
+  int la_len, lb_len;
+};
 
 // A factorisation workspace: two n_pad x n_pad buffers and their GEMM schedule.
 struct Fact {
@@ -160,7 +171,10 @@ struct gpe_ctx {
   int8_t* dozp = nullptr;         // the N int8 planes of X (lower 256-column panels)
   int8_t* dozr = nullptr;         // the N residue bytes of every lower 256-tile entry
   int* dozx = nullptr;            // per-column exponents
-  unsigned* dozl = nullptr;       // k_oz_gemm's tile list
+  unsigned* dozl = nullptr;       // k_oz_gemm's tile lists (the LAUUM's, then every TRTRI pair's)
+  double* dozt = nullptr;         // the TRTRI pairs' T = L21 X11
+  std::vector<OzTriPair> oz_tri;  // the TRTRI pairs on the int8 cores
+  int oz_tri_min = 8192;          // rows of a TRTRI level's blocks from which it runs there
   int dbg_skip_wait = -1;         // GPEMU_DEBUG_SKIP_WAIT (tests): a helper gives up its first wait
   size_t small_cap = 0;
 
@@ -1044,12 +1058,14 @@ int build_plan(gpe_ctx* c, Fact& F) {
   // --- triangular inverse X = L^-1 in B (diagonal tiles already hold Dinv)
   for (int s = 2; s / 2 < NB; s *= 2) {
     std::vector<GemmProb> pa, pb;
+    std::vector<std::array<int, 3>> prs;
     double fa = 0.0, fb = 0.0;
     for (int t0 = 0; t0 < NB; t0 += s) {
       const int h = t0 + s / 2;
       if (h >= NB) continue;
       const int t1 = std::min(t0 + s, NB);
       const int a = h - t0, b = t1 - h;
+      prs.push_back({t0, h, t1});
       // T^T (a x b tiles, stored in the upper block rows t0:h, cols h:t1 of B)
       //   = X11^T L21^T ;  opA(m,k) = X11(k,m): K-contiguous, upper -> kbeg = ti*128
       pa.push_back(mkprob(tile(B, t0, t0), ld, tile(A, h, t0), ld, tile(B, t0, h), ld, a, b,
@@ -1061,6 +1077,7 @@ int build_plan(gpe_ctx* c, Fact& F) {
       fb += (double)b * T * b * T * a * T;
     }
     if (pa.empty()) continue;
+    pl.tri_pairs.push_back(prs);
     split_k(pa, F.part, F.tcnt);
     split_k(pb, F.part, F.tcnt);
     pl.trtri.push_back((int)pl.launches.size());
@@ -1234,10 +1251,23 @@ int ensure_xdiag(gpe_ctx* c, Fact& F) {
   return GPE_OK;
 }
 
-int trtri(gpe_ctx* c, Fact& F) {
+int trtri_pair_ozaki(gpe_ctx* c, Fact& F, int t0, int h, int t1);
+bool oz_tri_level(const gpe_ctx* c, const std::vector<std::array<int, 3>>& prs);
+
+// X = L^-1 by levels; with ozaki (the objective's gradient) the levels whose blocks are at
+// least oz_tri_min rows run their two products on the int8 matrix cores (trtri_pair_ozaki)
+int trtri(gpe_ctx* c, Fact& F, bool ozaki = false) {
   CHK(build_plan(c, F));
   CHK(ensure_xdiag(c, F));
-  for (int li : F.plan.trtri) CHK(launch_gemm_range(c, F.plan.launches[li]));
+  const Plan& pl = F.plan;
+  for (size_t lv = 0; lv < pl.tri_pairs.size(); ++lv) {
+    if (ozaki && oz_tri_level(c, pl.tri_pairs[lv])) {
+      for (const auto& pr : pl.tri_pairs[lv]) CHK(trtri_pair_ozaki(c, F, pr[0], pr[1], pr[2]));
+      continue;
+    }
+    CHK(launch_gemm_range(c, pl.launches[pl.trtri[2 * lv]]));
+    CHK(launch_gemm_range(c, pl.launches[pl.trtri[2 * lv + 1]]));
+  }
   return GPE_OK;
 }
 
@@ -1400,7 +1430,7 @@ int factor_and_invert(gpe_ctx* c, int kernel, const double* delta, double nu, do
   CHK(potrf(c, c->tr, c->zaug_valid));
   ev_rec(c, 2);
   if (invert) {
-    CHK(trtri(c, c->tr));
+    CHK(trtri(c, c->tr, true));   // (only the objective's gradient inverts here)
     c->linv_valid = true;
   }
   CHK(z_from_factor(c));
@@ -1445,6 +1475,258 @@ int trsv_lower(gpe_ctx* c, Fact& F, const double* R, long long ldr, int P, doubl
                        R + (long long)c0 * ldr, ldr, Y + (long long)c0 * ldy, ldy, pc, F.tflags, F.tflags + 1,
                        c->dinfo);
     HIPCHK(c, hipGetLastError());
+  }
+  return GPE_OK;
+}
+
+// ---------------------------------------------------------------- A^-1 on the int8 cores
+// (gpemu_ozaki.hpp).  Used by the objective's gradient for OZ_MIN_NP <= n_pad <= OZ_MAX_NP:
+// below, the fp64 LAUUM is a few short launches; above, the planes and residues (each
+// N bytes per lower entry) would take more than ~13 GB per context.
+constexpr int OZ_MIN_NP = 2048, OZ_MAX_NP = 32768;
+bool oz_use(const gpe_ctx* c) { return c->oz_on && c->n_pad >= OZ_MIN_NP && c->n_pad <= OZ_MAX_NP; }
+
+// moduli and reconstruction constants for operand sums of length up to np2
+OzConst oz_consts(int nmod, int np2) {
+  static const int mods[OZ_MAXMOD] = {256, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217, 211, 199, 197, 193, 191};
+  OzConst k{};
+  k.nmod = nmod;
+  double log2M = 0.0, Md = 1.0;
+  for (int l = 0; l < nmod; ++l) {
+    log2M += std::log2((double)mods[l]);
+    Md *= (double)mods[l];
+  }
+  k.Md = Md;
+  // |C'| <= np2 2^(2 beta) < M / 2
+  k.beta = std::min(53, (int)std::floor((log2M - 1.0 - std::log2((double)np2) - 1e-9) / 2.0));
+  for (int l = 0; l < nmod; ++l) {
+    const int m = mods[l];
+    k.m[l] = m;
+    k.c16[l] = 65536 % m;
+    k.inv[l] = 1.0f / (float)m;
+    long long Mm = 1;   // (M / m) mod m
+    for (int j = 0; j < nmod; ++j)
+      if (j != l) Mm = (Mm * (mods[j] % m)) % m;
+    int y = 1;          // its inverse mod m
+    while ((Mm * y) % m != 1) ++y;
+    // y / m = rhi + rlo, rhi on the 2^-41 grid (exact products and sums in k_oz_crt)
+    const long long num = (long long)y << 41;
+    const long long Q = num / m, R = num - Q * m;
+    k.rhi[l] = std::ldexp((double)Q, -41);
+    k.rlo[l] = std::ldexp((double)R / (double)m, -41);
+  }
+  return k;
+}
+
+// A product's tile list: blocks of OZ_BR tile rows x OZ_BC tile columns (clipped to the lower
+// triangle when lower), heaviest first, greedily binned by work into 8 XCD bins, interleaved
+// position by position (bin = position % 8, the XCD under round-robin dispatch), bins padded
+// to one length with 0xffffffff.  An XCD's 32 CUs then run one block at a time: its tiles
+// share 4 A panels and 8 B panels (a whole tile row on one XCD shared one A panel among 32
+// different B panels: L2 hit rate ~0.5)
+template <class W>
+std::vector<unsigned> oz_list(int nti, int ntj, bool lower, W work) {
+  constexpr int OZ_BR = 4, OZ_BC = 8;
+  struct Blk { double w; std::vector<unsigned> t; };
+  std::vector<Blk> blks;
+  for (int r0 = 0; r0 < nti; r0 += OZ_BR)
+    for (int c0 = 0; c0 < ntj && (!lower || c0 <= r0 + OZ_BR - 1); c0 += OZ_BC) {
+      Blk b{0.0, {}};
+      for (int ti = r0; ti < std::min(nti, r0 + OZ_BR); ++ti)
+        for (int tj = c0; tj < std::min(lower ? ti + 1 : ntj, c0 + OZ_BC); ++tj) {
+          b.t.push_back(((unsigned)ti << 16) | (unsigned)tj);
+          b.w += work(ti, tj);
+        }
+      if (!b.t.empty()) blks.push_back(std::move(b));
+    }
+  std::stable_sort(blks.begin(), blks.end(), [](const Blk& x, const Blk& y) { return x.w / x.t.size() > y.w / y.t.size(); });
+  std::vector<std::vector<unsigned>> bins(8);
+  std::vector<double> load(8, 0.0);
+  for (const Blk& b : blks) {
+    const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    load[x] += b.w;
+    bins[x].insert(bins[x].end(), b.t.begin(), b.t.end());
+  }
+  size_t longest = 0;
+  for (auto& b : bins) longest = std::max(longest, b.size());
+  std::vector<unsigned> list(8 * longest, 0xffffffffu);
+  for (int x = 0; x < 8; ++x)
+    for (size_t q = 0; q < bins[x].size(); ++q) list[8 * q + x] = bins[x][q];
+  return list;
+}
+
+// the TRTRI levels on the int8 cores: every pair of a level whose blocks have at least
+// oz_tri_min rows (GPEMU_OZAKI_TRI_MIN; the levels below stay fp64: their products are a
+// few short tiles)
+bool oz_tri_level(const gpe_ctx* c, const std::vector<std::array<int, 3>>& prs) {
+  return oz_use(c) && !prs.empty() && (prs[0][1] - prs[0][0]) * TILE >= c->oz_tri_min;
+}
+
+// planes, residues, exponents, scratch and the tile lists (the LAUUM's and every Ozaki
+// TRTRI pair's) for this n_pad
+int oz_prepare(gpe_ctx* c, Fact& F) {
+  const int np2 = (int)(((c->n_pad + OZ_T - 1) / OZ_T) * OZ_T);
+  if (np2 == c->oz_np2 && c->oz_c.nmod == c->oz_nmod) return GPE_OK;
+  c->oz_np2 = 0;
+  CHK(build_plan(c, F));
+  const int NT2 = np2 / OZ_T, N = c->oz_nmod;
+  size_t planes = (size_t)oz_plane_bytes(np2) * N;
+  size_t resid = (size_t)NT2 * (NT2 + 1) / 2 * OZ_T * OZ_T * N;
+  size_t scratch = 0, nex = (size_t)np2;
+  std::vector<unsigned> all = oz_list(NT2, NT2, true, [&](int ti, int) { return (double)(np2 - OZ_T * ti); });
+  c->oz_list_len = (int)all.size();
+  c->oz_tri.clear();
+  for (const auto& prs : F.plan.tri_pairs) {
+    if (!oz_tri_level(c, prs)) continue;
+    for (const auto& pr : prs) {
+      OzTriPair q;
+      q.t0 = pr[0]; q.h = pr[1]; q.t1 = pr[2];
+      q.Ra = (q.h - q.t0) * TILE;
+      q.Rb = (q.t1 - q.h) * TILE;
+      q.Pa = (q.Ra + OZ_T - 1) / OZ_T * OZ_T;
+      q.Pb = (q.Rb + OZ_T - 1) / OZ_T * OZ_T;
+      const int nti = q.Pb / OZ_T, ntj = q.Pa / OZ_T;
+      const std::vector<unsigned> la = oz_list(nti, ntj, false, [&](int, int tj) { return (double)(q.Pa - OZ_T * tj); });
+      const std::vector<unsigned> lb = oz_list(nti, ntj, false, [&](int ti, int) { return (double)(OZ_T * (ti + 1)); });
+      q.la_off = (long long)all.size();
+      q.la_len = (int)la.size();
+      all.insert(all.end(), la.begin(), la.end());
+      q.lb_off = (long long)all.size();
+      q.lb_len = (int)lb.size();
+      all.insert(all.end(), lb.begin(), lb.end());
+      planes = std::max(planes, (size_t)N * q.Pa * (q.Pa + q.Pb));
+      resid = std::max(resid, (size_t)N * q.Pa * q.Pb);
+      scratch = std::max(scratch, (size_t)q.Pa * q.Pb);
+      nex = std::max(nex, (size_t)(q.Pa + q.Pb));
+      c->oz_tri.push_back(q);
+    }
+  }
+  CHK(dalloc(c, &c->dozp, planes));
+  CHK(dalloc(c, &c->dozr, resid));
+  CHK(dalloc(c, &c->dozx, nex));
+  CHK(dalloc(c, &c->dozt, scratch));
+  CHK(dalloc(c, &c->dozl, all.size()));
+  HIPCHK(c, hipMemcpy(c->dozl, all.data(), all.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+  c->oz_c = oz_consts(N, np2);   // (beta for sums of length np2: valid for every product here)
+  c->oz_np2 = np2;
+  return GPE_OK;
+}
+
+int oz_gemm_crt(gpe_ctx* c, const OzGemm& g, const OzCrt& r, int nti) {
+  const OzConst& k = c->oz_c;
+  hipLaunchKernelGGL(k_oz_gemm, dim3(k.nmod * g.list_len), dim3(256), OZ_LDS, c->stream, g, k);
+  hipLaunchKernelGGL(k_oz_crt, dim3((g.tri ? nti * (nti + 1) / 2 : nti * g.ntj) * 16), dim3(256), 0, c->stream, r, k);
+  HIPCHK(c, hipGetLastError());
+  return GPE_OK;
+}
+
+// A^-1 = X^T X (lower 128-tiles) of the workspace's X = L^-1 (F.B) into F.A
+int lauum_ozaki(gpe_ctx* c, Fact& F) {
+  CHK(oz_prepare(c, F));
+  const int np = (int)F.n_pad, np2 = c->oz_np2, NT2 = np2 / OZ_T;
+  const OzConst& k = c->oz_c;
+  const long long pb = oz_plane_bytes(np2), rb = (long long)NT2 * (NT2 + 1) / 2 * OZ_T * OZ_T;
+  hipLaunchKernelGGL(k_oz_colexp, dim3((np2 + 3) / 4), dim3(256), 0, c->stream, F.B, (long long)F.n_pad, np, np2,
+                     k.beta, c->dozx);
+  hipLaunchKernelGGL(k_oz_split, dim3(np2, (np2 + 256 * OZ_SPLIT_ROWS - 1) / (256 * OZ_SPLIT_ROWS)), dim3(256), 0,
+                     c->stream, F.B, (long long)F.n_pad, np, np2, c->dozx, c->dozp, pb, k);
+  OzGemm g;
+  g.a = g.b = OzOpnd{c->dozp, pb, 0, np2};
+  g.list = c->dozl;
+  g.list_len = c->oz_list_len;
+  g.K = np2;
+  g.kbeg = 1;
+  g.kend = 0;
+  g.tri = 1;
+  g.ntj = 0;
+  g.res = c->dozr;
+  g.res_bytes = rb;
+  OzCrt r{c->dozr, rb, 1, 0, c->dozx, c->dozx, F.A, (long long)F.n_pad, np, np, 1, 1.0};
+  return oz_gemm_crt(c, g, r, NT2);
+}
+
+// One pair (t0, h, t1) of a TRTRI level on the int8 cores (plan: the blocks X11 = X(t0:h,
+// t0:h), X22 = X(h:t1, h:t1) already inverted, L21 = L(h:t1, t0:h)):
+//   T   = L21 X11      (rows of L21 against columns of X11, k >= the column: kbeg = 256 tj)
+//   X21 = -X22 T       (rows of X22, k <= the row: kend = 256 (ti + 1), against columns of T)
+// T goes to a scratch block (column-major, so its columns are the second product's rows);
+// X21 over B's tile block (h, t0), as the fp64 launches' pb
+int trtri_pair_ozaki(gpe_ctx* c, Fact& F, int t0, int h, int t1) {
+  CHK(oz_prepare(c, F));
+  const OzTriPair* qp = nullptr;
+  for (const OzTriPair& q : c->oz_tri)
+    if (q.t0 == t0 && q.h == h && q.t1 == t1) qp = &q;
+  if (!qp) return fail(c, GPE_ERR_STATE, "internal error: TRTRI pair without an int8 plan");
+  const OzTriPair& q = *qp;
+  const OzConst& k = c->oz_c;
+  const long long ld = F.n_pad;
+  auto tile = [&](double* M, int i, int j) { return M + (long long)i * TILE + (long long)j * TILE * ld; };
+  const double* L21 = tile(F.A, h, t0);
+  const double* X11 = tile(F.B, t0, t0);
+  const double* X22 = tile(F.B, h, h);
+  double* X21 = tile(F.B, h, t0);
+  int* exA = c->dozx;
+  int* exB = c->dozx + q.Pb;
+  const int nti = q.Pb / OZ_T, ntj = q.Pa / OZ_T;
+  const long long rb = (long long)nti * ntj * OZ_T * OZ_T;
+  // --- T = L21 X11
+  {
+    const long long pA = (long long)q.Pb * q.Pa, pB = (long long)q.Pa * q.Pa;
+    int8_t* PA = c->dozp;
+    int8_t* PB = c->dozp + (size_t)k.nmod * pA;
+    HIPCHK(c, hipMemsetAsync(exA, 0, q.Pb * sizeof(int), c->stream));
+    hipLaunchKernelGGL(k_oz_rowexp<true>, dim3(q.Pb / 64, (q.Ra + 255) / 256), dim3(256), 0, c->stream, L21, ld, q.Rb, q.Pb,
+                       q.Ra, 0, k.beta, exA);
+    hipLaunchKernelGGL(k_oz_il_to_ex, dim3((q.Pb + 255) / 256), dim3(256), 0, c->stream, exA, q.Pb, k.beta);
+    hipLaunchKernelGGL(k_oz_rowexp<false>, dim3(q.Pa / 4), dim3(256), 0, c->stream, X11, ld, q.Ra, q.Pa, q.Ra, 1, k.beta, exB);
+    hipLaunchKernelGGL(k_oz_split_rect<true>, dim3(q.Pb / 64, q.Pa / 64), dim3(256), 0, c->stream, L21, ld, q.Rb, q.Ra, 0,
+                       exA, PA, pA, (long long)q.Pa, q.Pa, k);
+    hipLaunchKernelGGL(k_oz_split_rect<false>, dim3(q.Pa, (q.Pa + 2047) / 2048), dim3(256), 0, c->stream, X11, ld, q.Ra, q.Ra,
+                       1, exB, PB, pB, (long long)q.Pa, q.Pa, k);
+    OzGemm g;
+    g.a = OzOpnd{PA, pA, q.Pa, 0};
+    g.b = OzOpnd{PB, pB, q.Pa, 0};
+    g.list = c->dozl + q.la_off;
+    g.list_len = q.la_len;
+    g.K = q.Pa;
+    g.kbeg = 2;
+    g.kend = 0;
+    g.tri = 0;
+    g.ntj = ntj;
+    g.res = c->dozr;
+    g.res_bytes = rb;
+    OzCrt r{c->dozr, rb, 0, ntj, exA, exB, c->dozt, (long long)q.Pb, q.Rb, q.Ra, 0, 1.0};
+    CHK(oz_gemm_crt(c, g, r, nti));
+  }
+  // --- X21 = -X22 T
+  {
+    const long long pA = (long long)q.Pb * q.Pb, pB = (long long)q.Pa * q.Pb;
+    int8_t* PA = c->dozp;
+    int8_t* PB = c->dozp + (size_t)k.nmod * pA;
+    HIPCHK(c, hipMemsetAsync(exA, 0, q.Pb * sizeof(int), c->stream));
+    hipLaunchKernelGGL(k_oz_rowexp<true>, dim3(q.Pb / 64, (q.Rb + 255) / 256), dim3(256), 0, c->stream, X22, ld, q.Rb, q.Pb,
+                       q.Rb, 2, k.beta, exA);
+    hipLaunchKernelGGL(k_oz_il_to_ex, dim3((q.Pb + 255) / 256), dim3(256), 0, c->stream, exA, q.Pb, k.beta);
+    hipLaunchKernelGGL(k_oz_rowexp<false>, dim3(q.Pa / 4), dim3(256), 0, c->stream, c->dozt, (long long)q.Pb, q.Ra, q.Pa,
+                       q.Rb, 0, k.beta, exB);
+    hipLaunchKernelGGL(k_oz_split_rect<true>, dim3(q.Pb / 64, q.Pb / 64), dim3(256), 0, c->stream, X22, ld, q.Rb, q.Rb, 2,
+                       exA, PA, pA, (long long)q.Pb, q.Pb, k);
+    hipLaunchKernelGGL(k_oz_split_rect<false>, dim3(q.Pa, (q.Pb + 2047) / 2048), dim3(256), 0, c->stream, c->dozt,
+                       (long long)q.Pb, q.Ra, q.Rb, 0, exB, PB, pB, (long long)q.Pb, q.Pb, k);
+    OzGemm g;
+    g.a = OzOpnd{PA, pA, q.Pb, 0};
+    g.b = OzOpnd{PB, pB, q.Pb, 0};
+    g.list = c->dozl + q.lb_off;
+    g.list_len = q.lb_len;
+    g.K = q.Pb;
+    g.kbeg = 0;
+    g.kend = 1;
+    g.tri = 0;
+    g.ntj = ntj;
+    g.res = c->dozr;
+    g.res_bytes = rb;
+    OzCrt r{c->dozr, rb, 0, ntj, exA, exB, X21, ld, q.Rb, q.Ra, 0, -1.0};
+    CHK(oz_gemm_crt(c, g, r, nti));
   }
   return GPE_OK;
 }
@@ -1545,6 +1827,7 @@ gpe_ctx* gpe_create(int32_t device) {
     if (const char* ed = std::getenv("GPEMU_DEBUG_SKIP_WAIT")) c->dbg_skip_wait = std::atoi(ed);
     if (const char* eo = std::getenv("GPEMU_OZAKI")) c->oz_on = std::atoi(eo) != 0;
     if (const char* em = std::getenv("GPEMU_OZAKI_MODULI")) c->oz_nmod = std::max(8, std::min(OZ_MAXMOD, std::atoi(em)));
+    if (const char* et = std::getenv("GPEMU_OZAKI_TRI_MIN")) c->oz_tri_min = std::max(512, std::atoi(et));
     if (const char* es = std::getenv("GPEMU_POTRF_SB")) {
       c->potrf_sb = std::max(1, std::min(8, std::atoi(es)));
       if (const char* colon = std::strchr(es, ':')) c->potrf_sb_min = std::max(0, std::atoi(colon + 1));
@@ -1638,6 +1921,7 @@ void gpe_destroy(gpe_ctx* c) {
   if (c->dozr) hipFree(c->dozr);
   if (c->dozx) hipFree(c->dozx);
   if (c->dozl) hipFree(c->dozl);
+  if (c->dozt) hipFree(c->dozt);
   if (c->tr.Faug) hipFree(c->tr.Faug);
   if (c->aux.tflags) hipFree(c->aux.tflags);
   if (c->dprobs) hipFree(c->dprobs);
@@ -1970,110 +2254,6 @@ int snb_objective(gpe_ctx* c, bool gp4ml, int kernel, const double* hp, int n_hp
   return GPE_OK;
 }
 
-
-// ---------------------------------------------------------------- A^-1 on the int8 cores
-// (gpemu_ozaki.hpp).  Used by the objective's gradient for OZ_MIN_NP <= n_pad <= OZ_MAX_NP:
-// below, the fp64 LAUUM is a few short launches; above, the planes and residues (each
-// N bytes per lower entry) would take more than ~13 GB per context.
-constexpr int OZ_MIN_NP = 2048, OZ_MAX_NP = 32768;
-bool oz_use(const gpe_ctx* c) { return c->oz_on && c->n_pad >= OZ_MIN_NP && c->n_pad <= OZ_MAX_NP; }
-
-// moduli and reconstruction constants for operand sums of length up to np2
-OzConst oz_consts(int nmod, int np2) {
-  static const int mods[OZ_MAXMOD] = {256, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217, 211, 199, 197, 193, 191};
-  OzConst k{};
-  k.nmod = nmod;
-  double log2M = 0.0, Md = 1.0;
-  for (int l = 0; l < nmod; ++l) {
-    log2M += std::log2((double)mods[l]);
-    Md *= (double)mods[l];
-  }
-  k.Md = Md;
-  // |C'| <= np2 2^(2 beta) < M / 2
-  k.beta = std::min(53, (int)std::floor((log2M - 1.0 - std::log2((double)np2) - 1e-9) / 2.0));
-  for (int l = 0; l < nmod; ++l) {
-    const int m = mods[l];
-    k.m[l] = m;
-    k.c16[l] = 65536 % m;
-    k.inv[l] = 1.0f / (float)m;
-    long long Mm = 1;   // (M / m) mod m
-    for (int j = 0; j < nmod; ++j)
-      if (j != l) Mm = (Mm * (mods[j] % m)) % m;
-    int y = 1;          // its inverse mod m
-    while ((Mm * y) % m != 1) ++y;
-    // y / m = rhi + rlo, rhi on the 2^-41 grid (exact products and sums in k_oz_crt)
-    const long long num = (long long)y << 41;
-    const long long Q = num / m, R = num - Q * m;
-    k.rhi[l] = std::ldexp((double)Q, -41);
-    k.rlo[l] = std::ldexp((double)R / (double)m, -41);
-  }
-  return k;
-}
-
-// planes, residues, exponents and the tile list for this n_pad
-int oz_prepare(gpe_ctx* c) {
-  const int np2 = (int)(((c->n_pad + OZ_T - 1) / OZ_T) * OZ_T);
-  if (np2 == c->oz_np2 && c->oz_c.nmod == c->oz_nmod) return GPE_OK;
-  c->oz_np2 = 0;
-  const int NT2 = np2 / OZ_T;
-  const size_t planes = (size_t)oz_plane_bytes(np2) * c->oz_nmod;
-  const size_t resid = (size_t)NT2 * (NT2 + 1) / 2 * OZ_T * OZ_T * c->oz_nmod;
-  CHK(dalloc(c, &c->dozp, planes));
-  CHK(dalloc(c, &c->dozr, resid));
-  CHK(dalloc(c, &c->dozx, (size_t)np2));
-  // Blocks of OZ_BR tile rows x OZ_BC tile columns (clipped to the lower triangle), longest K
-  // first, greedily binned by work into 8 XCD bins, interleaved position by position (bin =
-  // position % 8, the XCD under round-robin dispatch), bins padded to one length.  An XCD's
-  // 32 CUs then run one block at a time: its tiles share 4 A panels and 8 B panels (the rows'
-  // K starts differ by at most 3 x 256), where a whole tile row on one XCD shared one A panel
-  // among 32 different B panels (L2 hit rate ~0.5)
-  constexpr int OZ_BR = 4, OZ_BC = 8;
-  std::vector<std::vector<unsigned>> bins(8);
-  std::vector<double> load(8, 0.0);
-  for (int r0 = 0; r0 < NT2; r0 += OZ_BR)
-    for (int c0 = 0; c0 <= std::min(NT2 - 1, r0 + OZ_BR - 1); c0 += OZ_BC) {
-      std::vector<unsigned> blk;
-      double w = 0.0;
-      for (int ti = r0; ti < std::min(NT2, r0 + OZ_BR); ++ti)
-        for (int tj = c0; tj < std::min(ti + 1, c0 + OZ_BC); ++tj) {
-          blk.push_back(((unsigned)ti << 16) | (unsigned)tj);
-          w += (double)(np2 - OZ_T * ti);
-        }
-      if (blk.empty()) continue;
-      const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-      load[x] += w;
-      bins[x].insert(bins[x].end(), blk.begin(), blk.end());
-    }
-  size_t longest = 0;
-  for (auto& b : bins) longest = std::max(longest, b.size());
-  std::vector<unsigned> list(8 * longest, 0xffffffffu);
-  for (int x = 0; x < 8; ++x)
-    for (size_t q = 0; q < bins[x].size(); ++q) list[8 * q + x] = bins[x][q];
-  CHK(dalloc(c, &c->dozl, list.size()));
-  HIPCHK(c, hipMemcpy(c->dozl, list.data(), list.size() * sizeof(unsigned), hipMemcpyHostToDevice));
-  c->oz_list_len = (int)list.size();
-  c->oz_c = oz_consts(c->oz_nmod, np2);
-  c->oz_np2 = np2;
-  return GPE_OK;
-}
-
-// A^-1 = X^T X (lower 128-tiles) of the workspace's X = L^-1 (F.B) into F.A
-int lauum_ozaki(gpe_ctx* c, Fact& F) {
-  CHK(oz_prepare(c));
-  const int np = (int)F.n_pad, np2 = c->oz_np2, NT2 = np2 / OZ_T;
-  const OzConst& k = c->oz_c;
-  const long long pb = oz_plane_bytes(np2), rb = (long long)NT2 * (NT2 + 1) / 2 * OZ_T * OZ_T;
-  hipLaunchKernelGGL(k_oz_colexp, dim3((np2 + 3) / 4), dim3(256), 0, c->stream, F.B, (long long)F.n_pad, np, np2,
-                     k.beta, c->dozx);
-  hipLaunchKernelGGL(k_oz_split, dim3(np2, (np2 + 256 * OZ_SPLIT_ROWS - 1) / (256 * OZ_SPLIT_ROWS)), dim3(256), 0, c->stream, F.B, (long long)F.n_pad, np,
-                     np2, c->dozx, c->dozp, pb, k);
-  hipLaunchKernelGGL(k_oz_gemm, dim3(k.nmod * c->oz_list_len), dim3(256), OZ_LDS, c->stream, c->dozp, pb, np2,
-                     c->dozl, c->oz_list_len, c->dozr, rb, k);
-  hipLaunchKernelGGL(k_oz_crt, dim3(NT2 * (NT2 + 1) / 2 * 16), dim3(256), 0, c->stream, c->dozr, rb, c->dozx, np, F.A,
-                     (long long)F.n_pad, k);
-  HIPCHK(c, hipGetLastError());
-  return GPE_OK;
-}
 
 int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp, int32_t n_hp,
                   double nu_fixed, int32_t want_grad, double* llh_out, double* grad_out,

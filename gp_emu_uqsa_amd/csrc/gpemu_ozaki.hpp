@@ -120,34 +120,70 @@ __device__ __forceinline__ void oz_glds16(const int8_t* src, int8_t* dst) {
 }
 template <int N> __device__ __forceinline__ void oz_vmwait() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); }
 
-// One 256 x 256 tile (ti >= tj) of C'_l = X'_l^T X'_l for modulus l, K from 256 ti to np2.
-// blockIdx.x = l * list_len + position (the list's length a multiple of 8, so position % 8
-// is the XCD under round-robin dispatch; entries 0xffffffff pad the bins).  4 waves of
-// 128 x 128 (4 x 4 blocks of the 32 x 32 x 32 i8 MFMA, operands swapped so lane & 31 runs
-// along the tile's rows); stages of 64 k through a 4-deep LDS ring filled by direct
+// One operand of a product, as int8 planes (one per modulus, plane_bytes apart): row r of
+// 256-row tile t at depth k is
+//   packed (the LAUUM's lower column panels of X): oz_panel_off(t, np2) + r (np2 - 256 t) + k - 256 t
+//   rectangular: (256 t + r) ld + k
+struct OzOpnd {
+  const int8_t* p;
+  long long plane_bytes;
+  long long ld;    // rectangular row pitch (bytes); 0: packed
+  int np2;         // packed: the padded order
+};
+__device__ __forceinline__ const int8_t* oz_tile_rows(const OzOpnd& o, int t, int k, long long& ld) {
+  if (o.ld == 0) {
+    ld = o.np2 - OZ_T * t;
+    return o.p + oz_panel_off(t, o.np2) + (k - OZ_T * t);
+  }
+  ld = o.ld;
+  return o.p + (long long)OZ_T * t * o.ld + k;
+}
+
+// A product C'_l = A'_l B'_l^T over the 256 x 256 tiles of a list (entries ti << 16 | tj, the
+// list's length a multiple of 8 so position % 8 is the XCD under round-robin dispatch,
+// 0xffffffff padding the bins), blockIdx.x = l * list_len + position.  K range of tile
+// (ti, tj): from 0, 256 ti or 256 tj (kbeg 0 / 1 / 2) to K or 256 (ti + 1) (kend 0 / 1):
+// the triangular operands' nonzero k.
+struct OzGemm {
+  OzOpnd a, b;
+  const unsigned* list;
+  int list_len;
+  int K, kbeg, kend;
+  int tri, ntj;    // residue tile of (ti, tj): ti (ti + 1) / 2 + tj (tri) or ti ntj + tj
+  int8_t* res;
+  long long res_bytes;
+};
+__device__ __forceinline__ long long oz_res_tile(int tri, int ntj, int ti, int tj) {
+  return tri ? (long long)ti * (ti + 1) / 2 + tj : (long long)ti * ntj + tj;
+}
+
+// 4 waves of 128 x 128 (4 x 4 blocks of the 32 x 32 x 32 i8 MFMA, operands swapped so lane &
+// 31 runs along the tile's rows); stages of 64 k through a 4-deep LDS ring filled by direct
 // global -> LDS loads.  The stage image of each operand is [row][64 B] with granule g of row
 // r at slot g ^ ((r >> 2) & 3): conflict-free for ds_read_b128's lane groups.  Output: the
 // centred residue of every entry, one byte, in the MFMA's own order (lane l of block b of
 // wave w: 16 bytes at ((w 16 + b) 64 + l) 16 of the tile's 64 KB).
-static __global__ void __launch_bounds__(256, 1) k_oz_gemm(const int8_t* __restrict__ planes, long long plane_bytes,
-                                                           int np2, const unsigned* __restrict__ list, int list_len,
-                                                           int8_t* __restrict__ res, long long res_bytes, OzConst cst) {
+static __global__ void __launch_bounds__(256, 1) k_oz_gemm(OzGemm g, OzConst cst) {
   extern __shared__ __attribute__((aligned(16))) double lds_d[];
   int8_t* lds = reinterpret_cast<int8_t*>(lds_d);
-  const int l = (int)blockIdx.x / list_len;
-  const unsigned ent = list[(int)blockIdx.x - l * list_len];
+  const int l = (int)blockIdx.x / g.list_len;
+  const unsigned ent = g.list[(int)blockIdx.x - l * g.list_len];
   if (ent == 0xffffffffu) return;
   const int ti = (int)(ent >> 16), tj = (int)(ent & 0xffffu);
+  const int kb = g.kbeg == 1 ? OZ_T * ti : (g.kbeg == 2 ? OZ_T * tj : 0);
+  const int ke = g.kend == 1 ? min(g.K, OZ_T * (ti + 1)) : g.K;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = (wave >> 1) * 128, wn = (wave & 1) * 128;
-  const int8_t* P = planes + (long long)l * plane_bytes;
-  // operand rows: columns of X in panels ti (A) and tj (B); k from 256 ti
-  const long long lda = np2 - OZ_T * ti, ldb = np2 - OZ_T * tj;
+  OzOpnd oa = g.a, ob = g.b;
+  oa.p += (long long)l * oa.plane_bytes;
+  ob.p += (long long)l * ob.plane_bytes;
+  long long lda, ldb;
   const int kp = (lane & 3) ^ ((lane >> 4) & 3);
-  const int8_t* sa = P + oz_panel_off(ti, np2) + (long long)(16 * wave + (lane >> 2)) * lda + 16 * kp;
-  const int8_t* sb = P + oz_panel_off(tj, np2) + (long long)(16 * wave + (lane >> 2)) * ldb +
-                     (long long)OZ_T * (ti - tj) + 16 * kp;
+  const int8_t* sa = oz_tile_rows(oa, ti, kb, lda);
+  const int8_t* sb = oz_tile_rows(ob, tj, kb, ldb);
+  sa += (long long)(16 * wave + (lane >> 2)) * lda + 16 * kp;
+  sb += (long long)(16 * wave + (lane >> 2)) * ldb + 16 * kp;
   auto stage = [&](int s) {
     int8_t* As = lds + (s & (OZ_NBUF - 1)) * 2 * OZ_OPND;
     int8_t* Bs = As + OZ_OPND;
@@ -163,7 +199,7 @@ static __global__ void __launch_bounds__(256, 1) k_oz_gemm(const int8_t* __restr
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = oz_v16i{};
-  const int ns = (np2 - OZ_T * ti) / OZ_SK;
+  const int ns = max(0, ke - kb) / OZ_SK;
   const int r32 = lane & 31, h = lane >> 5, sw = (r32 >> 2) & 3;
   // the 8 fragments (4 of A, 4 of B) of k-step ks of stage s
   auto frags = [&](int s, int ks, oz_v4i (&af)[4], oz_v4i (&bf)[4]) {
@@ -191,42 +227,44 @@ static __global__ void __launch_bounds__(256, 1) k_oz_gemm(const int8_t* __restr
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
-  // Software pipeline, one barrier per stage: the next k-step's fragments are read while the
-  // current k-step's 16 MFMAs issue.  Stage s + 3 goes into the buffer of stage s - 1, whose
-  // last fragment reads every wave finished before the barrier of stage s.
-  for (int s = 0; s < min(ns, 3); ++s) stage(s);
-  oz_v4i ca[4], cb[4], na[4], nb[4];
-  wait_stage(0);
-  if (ns > 3) stage(3);
-  frags(0, 0, ca, cb);
-  for (int s = 0; s < ns; ++s) {
-    // this k-step's MFMAs with the next k-step's 8 fragment reads between the first 8 (an
-    // MFMA leaves the wave's issue free for most of its 32 cycles; the reads issued ahead
-    // of the MFMAs made the first MFMA wait for all of them: lgkmcnt(0))
-    mfmas(ca, cb);
-    frags(s, 1, na, nb);
+  if (ns > 0) {
+    // Software pipeline, one barrier per stage: the next k-step's fragments are read while
+    // the current k-step's 16 MFMAs issue.  Stage s + 4 goes into the buffer of stage s,
+    // whose last fragment reads every wave finished before the barrier of stage s + 1.
+    for (int s = 0; s < min(ns, 3); ++s) stage(s);
+    oz_v4i ca[4], cb[4], na[4], nb[4];
+    wait_stage(0);
+    if (ns > 3) stage(3);
+    frags(0, 0, ca, cb);
+    for (int s = 0; s < ns; ++s) {
+      // this k-step's MFMAs with the next k-step's 8 fragment reads between the first 8 (an
+      // MFMA leaves the wave's issue free for most of its 32 cycles; the reads issued ahead
+      // of the MFMAs made the first MFMA wait for all of them: lgkmcnt(0))
+      mfmas(ca, cb);
+      frags(s, 1, na, nb);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one LDS read
+      for (int u = 0; u < 8; ++u) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one LDS read
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < ns) {
+        wait_stage(s + 1);
+        if (s + 4 < ns) stage(s + 4);
+        frags(s + 1, 0, ca, cb);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(na, nb);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    if (s + 1 < ns) {
-      wait_stage(s + 1);
-      if (s + 4 < ns) stage(s + 4);
-      frags(s + 1, 0, ca, cb);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    mfmas(na, nb);
-    __builtin_amdgcn_sched_barrier(0);
   }
   // centred residues: t = (acc >> 16) (2^16 mod m) + (acc & 0xffff) is exact in fp32
   // (|t| < 2^20), q = rint(t / m) to within 3e-4, r = t - q m in [-m/2 - 1, m/2 + 1];
   // m = 256: the low byte itself
   const int m = cst.m[l], c16 = cst.c16[l];
   const float inv = cst.inv[l];
-  int8_t* out = res + (long long)l * res_bytes + ((long long)ti * (ti + 1) / 2 + tj) * (OZ_T * OZ_T) +
+  int8_t* out = g.res + (long long)l * g.res_bytes + oz_res_tile(g.tri, g.ntj, ti, tj) * (OZ_T * OZ_T) +
                 ((long long)(wave * 16) * 64 + lane) * 16;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -248,28 +286,44 @@ static __global__ void __launch_bounds__(256, 1) k_oz_gemm(const int8_t* __restr
     }
 }
 
-// fp64 entries from the residues: thread u of tile t (16 workgroups per tile) = wave
-// u / 1024, block (u / 64) % 16, lane u % 64 of k_oz_gemm's order, 16 entries; lower
-// 128-tiles within np only, into C (ld ldc)
-static __global__ void __launch_bounds__(256) k_oz_crt(const int8_t* __restrict__ res, long long res_bytes,
-                                                       const int* __restrict__ ex, int np, double* __restrict__ C,
-                                                       long long ldc, OzConst cst) {
+// fp64 entries from the residues: C(r, c) = alpha v M 2^-(exr[r] + exc[c]), v = C'/M the
+// centred fraction of sum_l c_l y_l / m_l.  Thread u of tile t (16 workgroups per tile) =
+// wave u / 1024, block (u / 64) % 16, lane u % 64 of k_oz_gemm's order, 16 entries; rows
+// < rows and columns < cols only, and with lower128 only the lower 128-tiles.
+struct OzCrt {
+  const int8_t* res;
+  long long res_bytes;
+  int tri, ntj;
+  const int* exr;
+  const int* exc;
+  double* C;
+  long long ldc;
+  int rows, cols, lower128;
+  double alpha;
+};
+static __global__ void __launch_bounds__(256) k_oz_crt(OzCrt g, OzConst cst) {
   const int t = (int)blockIdx.x >> 4;
   const int u = ((int)blockIdx.x & 15) * 256 + (int)threadIdx.x;
-  int ti = 0;
-  while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-  const int tj = t - ti * (ti + 1) / 2;
+  int ti, tj;
+  if (g.tri) {
+    ti = 0;
+    while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+    tj = t - ti * (ti + 1) / 2;
+  } else {
+    ti = t / g.ntj;
+    tj = t - ti * g.ntj;
+  }
   const int wave = u >> 10, blk = (u >> 6) & 15, lane = u & 63;
   const int i = blk >> 2, j = blk & 3;
   const int gm = OZ_T * ti + (wave >> 1) * 128 + 32 * i + (lane & 31);
   const int gn0 = OZ_T * tj + (wave & 1) * 128 + 32 * j + 4 * (lane >> 5);
-  if (gm >= np || gn0 >= np) return;
+  if (gm >= g.rows || gn0 >= g.cols) return;
   double shi[16], slo[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) shi[r] = slo[r] = 0.0;
-  const int8_t* src = res + (long long)t * (OZ_T * OZ_T) + (long long)u * 16;
+  const int8_t* src = g.res + (long long)t * (OZ_T * OZ_T) + (long long)u * 16;
   for (int l = 0; l < cst.nmod; ++l) {
-    const oz_v4i w = *reinterpret_cast<const oz_v4i*>(src + (long long)l * res_bytes);
+    const oz_v4i w = *reinterpret_cast<const oz_v4i*>(src + (long long)l * g.res_bytes);
     const double rh = cst.rhi[l], rl = cst.rlo[l];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -278,13 +332,120 @@ static __global__ void __launch_bounds__(256) k_oz_crt(const int8_t* __restrict_
       slo[r] = fma(cv, rl, slo[r]);
     }
   }
-  const int em = ex[gm];
+  const int em = g.exr[gm];
+  const double sc = g.alpha * cst.Md;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int gn = gn0 + (r & 3) + 8 * (r >> 2);
-    if (gn >= np || (gm >> 7) < (gn >> 7)) continue;   // lower 128-tiles only
+    if (gn >= g.cols || (g.lower128 && (gm >> 7) < (gn >> 7))) continue;
     const double v = (shi[r] - rint(shi[r])) + slo[r];   // C' / M, centred
-    C[gm + (long long)gn * ldc] = v * ldexp(cst.Md, -(em + ex[gn]));
+    g.C[gm + (long long)gn * g.ldc] = v * ldexp(sc, -(em + g.exc[gn]));
+  }
+}
+
+// ---- rectangular operands (the TRTRI's products): op(r, k) of an fp64 block src (ld) is
+// src[k + r ld] (TRANS false: the rows are the block's columns) or src[r + k ld] (TRANS
+// true), r < R, k < Kv; zero outside, and (mask) where k < r (1) or k > r (2): the lower
+// triangle's nonzeros seen from a column (1) or a row (2).
+__device__ __forceinline__ bool oz_keep(int mask, int r, int k) {
+  return mask == 1 ? k >= r : (mask == 2 ? k <= r : true);
+}
+
+// per-row exponents e_r = beta - 1 - ilogb(max_k |op(r, k)|), rows r < Rp (0 past R or for a
+// zero row).  TRANS false: one wave per row.  TRANS true: workgroup = 64 rows x 256 k (the
+// lanes along r: coalesced), its maximum's ilogb + 2048 atomically max-ed into il (zeroed
+// before), then k_oz_il_to_ex.
+template <bool TRANS>
+static __global__ void __launch_bounds__(256) k_oz_rowexp(const double* __restrict__ src, long long ld, int R, int Rp,
+                                                          int Kv, int mask, int beta, int* __restrict__ ex) {
+  if constexpr (!TRANS) {
+    const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= Rp) return;
+    double mx = 0.0;
+    if (r < R)
+      for (int k = lane; k < Kv; k += 64)
+        if (oz_keep(mask, r, k)) mx = fmax(mx, fabs(src[k + (long long)r * ld]));
+    for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off, 64));
+    if (lane == 0) ex[r] = mx > 0.0 ? (beta - 1) - ilogb(mx) : 0;
+  } else {
+    __shared__ double red[4][64];
+    const int rl = threadIdx.x & 63, q = threadIdx.x >> 6, r = blockIdx.x * 64 + rl;
+    const int k0 = blockIdx.y * 256;
+    double mx = 0.0;
+    if (r < R)
+#pragma unroll 8
+      for (int u = 0; u < 64; ++u) {
+        const int k = k0 + 4 * u + q;
+        if (k < Kv && oz_keep(mask, r, k)) mx = fmax(mx, fabs(src[r + (long long)k * ld]));
+      }
+    red[q][rl] = mx;
+    __syncthreads();
+    if (q == 0 && r < R) {
+      mx = fmax(fmax(red[0][rl], red[1][rl]), fmax(red[2][rl], red[3][rl]));
+      if (mx > 0.0) atomicMax(ex + r, ilogb(mx) + 2048);
+    }
+  }
+}
+static __global__ void __launch_bounds__(256) k_oz_il_to_ex(int* __restrict__ ex, int Rp, int beta) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r < Rp) ex[r] = ex[r] > 0 ? (beta - 1) - (ex[r] - 2048) : 0;
+}
+
+// op -> the N int8 planes, rectangular (row r at r ldp + k, k < Kp; zero past R / Kv and
+// masked).  TRANS false: thread = 8 consecutive k of one row (contiguous in src).  TRANS true:
+// workgroup = 64 rows x 64 k, thread = 16 consecutive k of one row with the lanes along r
+// (each load coalesced); each plane's 64 x 64 bytes go through LDS so the stores run along
+// k (4 threads per row, 16 bytes each).
+template <bool TRANS>
+static __global__ void __launch_bounds__(256) k_oz_split_rect(const double* __restrict__ src, long long ld, int R,
+                                                              int Kv, int mask, const int* __restrict__ ex,
+                                                              int8_t* __restrict__ planes, long long plane_bytes,
+                                                              long long ldp, int Kp, OzConst cst) {
+  constexpr int NK = TRANS ? 16 : 8;
+  int r, k0;
+  if constexpr (TRANS) {
+    r = blockIdx.x * 64 + (threadIdx.x & 63);
+    k0 = ((int)blockIdx.y * 4 + (threadIdx.x >> 6)) * NK;
+  } else {
+    r = blockIdx.x;
+    k0 = ((int)blockIdx.y * 256 + (int)threadIdx.x) * NK;
+    if (k0 >= Kp) return;
+  }
+  const int e = ex[r];
+  double xs[NK];
+#pragma unroll
+  for (int u = 0; u < NK; ++u) {
+    const int k = k0 + u;
+    double v = 0.0;
+    if (r < R && k < Kv && oz_keep(mask, r, k)) v = TRANS ? src[r + (long long)k * ld] : src[k + (long long)r * ld];
+    xs[u] = rint(ldexp(v, e));
+  }
+  __shared__ oz_v4i tr[64 * 5];   // TRANS: [row][16-byte piece], pitch 5 pieces (bank spread)
+  for (int l = 0; l < cst.nmod; ++l) {
+    const double m = (double)cst.m[l], im = 1.0 / m;
+    unsigned w[NK / 4];
+#pragma unroll
+    for (int c = 0; c < NK / 4; ++c) w[c] = 0u;
+#pragma unroll
+    for (int u = 0; u < NK; ++u) {
+      const double q = rint(xs[u] * im);
+      int rr = (int)fma(-q, m, xs[u]);
+      rr = rr > 127 ? rr - cst.m[l] : (rr < -128 ? rr + cst.m[l] : rr);
+      w[u >> 2] |= ((unsigned)rr & 0xffu) << (8 * (u & 3));
+    }
+    if constexpr (TRANS) {
+      const int rl = threadIdx.x & 63, pc = threadIdx.x >> 6;
+      if (l > 0) __syncthreads();   // (the previous plane's reads done)
+      tr[rl * 5 + pc] = oz_v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+      __syncthreads();
+      const int wr = threadIdx.x >> 2, wp = threadIdx.x & 3;   // row wr, piece wp of the block
+      const long long row = (long long)blockIdx.x * 64 + wr;
+      *reinterpret_cast<oz_v4i*>(planes + (long long)l * plane_bytes + row * ldp + (long long)blockIdx.y * 64 + 16 * wp) =
+          tr[wr * 5 + wp];
+    } else {
+      *reinterpret_cast<uint2*>(planes + (long long)l * plane_bytes + (long long)r * ldp + k0 + (long long)0) =
+          make_uint2(w[0], w[1]);
+    }
   }
 }
 
