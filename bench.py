@@ -49,6 +49,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "log-marginal-likelihood evals/sec at n=16384 d=10 fp64; 1/2/4/8 GPU"
 FP64_MFMA_PEAK_TFLOPS = 78.6       # MI355X dense fp64 matrix peak (spec)
+INT8_MFMA_PEAK_TOPS = 5033.0       # dense i8 matrix peak (spec: 2 x the 2.5 PF dense bf16)
+INT8_RANDOM_CEILING_TOPS = 2449.0  # MFMA-only i8 loop on random operands, 4 waves/SIMD (tools/hip/i8_probe.hip)
 C4 = (65536, 20)                   # BASELINE.json configs[3]
 
 
@@ -439,8 +441,9 @@ def guarded_rowblock(native, synthetic, group, rank, world, local, args, sync_al
     return res
 
 
-def pmc_traffic(n, d):
-    """HBM bytes per GEMM launch from the committed rocprofv3 PMC summary."""
+def pmc_traffic(n, d, which="gemm"):
+    """HBM bytes per launch of k_gemm (which="gemm") or k_oz_gemm ("ozaki") from the committed
+    rocprofv3 PMC summary (tools/pmc_gemm.py)."""
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_gemm_*.json"))):
         try:
@@ -451,7 +454,8 @@ def pmc_traffic(n, d):
             best = (os.path.relpath(path, ROOT), rec)
     if best is None:
         return None, None
-    return best[1].get("bytes_per_gemm_launch"), best[0]
+    key = "bytes_per_gemm_launch" if which == "gemm" else "bytes_per_ozaki_launch"
+    return best[1].get(key), best[0]
 
 
 def main(argv=None):
@@ -522,6 +526,7 @@ def main(argv=None):
 
     run_tries(args.warmup)
     gemm_ms = gemm_fl = gemm_n = 0.0
+    oz_ms = oz_ops = oz_fl = oz_n = 0.0
     phase_acc = {}
     prof_steps = 0
     sync_all()
@@ -539,6 +544,11 @@ def main(argv=None):
             gemm_ms += gs["ms"]
             gemm_fl += gs["flops"]
             gemm_n += gs["launches"]
+            oz = ctxs[k].ozaki_stats()
+            oz_ms += oz["ms"]
+            oz_ops += oz["int8_ops"]
+            oz_fl += oz["fp64_flops"]
+            oz_n += oz["launches"]
             for key, v in ctxs[k].phase_times().items():
                 phase_acc[key] = phase_acc.get(key, 0.0) + v
             prof_steps += 1
@@ -573,6 +583,8 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
+            "dtype_note": "fp64 throughout; the A^-1 and top-TRTRI products are computed exactly (53-bit operands, "
+                          "integer products reconstructed by CRT) on the int8 matrix cores",
             "data": "synthetic (oLHC design, toysim3D-style outputs + 0.01 N(0,1) noise)",
             "config": {"workload": f"gp4ml LLH+grad, n={args.n} d={args.d}, std Gaussian kernel, "
                                    f"nugget fitted ({args.d + 2} hp); a step = one eval of each of "
@@ -593,14 +605,30 @@ def main(argv=None):
                                              "GPU to itself (the tries run one after the other in that step)",
                                "achieved_step_level": step_tflops,
                                "frac_step_level": step_tflops / FP64_MFMA_PEAK_TFLOPS,
-                               "step_level_basis": f"whole-job: n^3 algorithmic flops per evaluation x "
-                                                   f"{K} tries in flight / ms_per_step (the headline regime)",
+                               "step_level_basis": f"whole-job: n^3 algorithmic fp64 flops per evaluation x "
+                                                   f"{K} tries in flight / ms_per_step (the headline regime; the "
+                                                   f"A^-1 and top TRTRI products among them run as exact int8 "
+                                                   f"products, see int8_emulation)",
                                "traffic": traffic,
                                "traffic_source": (f"{tsrc}: rocprofv3 --pmc passes of this bench command "
                                                   f"(committed, not measured in this run)") if tsrc else None,
                                "kernel": "k_gemm (fp64 v_mfma_f64_16x16x4_f64)",
                                "flops_per_launch": gemm_fl / gemm_n,
                                "ms_per_launch": gemm_ms / gemm_n}
+            if oz_n > 0:
+                ach = oz_ops / (oz_ms * 1e-3) / 1e12
+                out["roofline"]["int8_emulation"] = {
+                    "kernel": "k_oz_gemm (v_mfma_i32_32x32x32_i8): A^-1 = L^-T L^-1 and the top TRTRI level's two "
+                              "products as exact integer products of 53-bit operands, 16 moduli, CRT back to fp64 "
+                              "(gpemu_ozaki.hpp)",
+                    "bound": "mfma", "unit": "TOPS (int8)", "achieved": ach, "peak": INT8_MFMA_PEAK_TOPS,
+                    "frac": ach / INT8_MFMA_PEAK_TOPS,
+                    "random_operand_ceiling": INT8_RANDOM_CEILING_TOPS,
+                    "frac_of_random_operand_ceiling": ach / INT8_RANDOM_CEILING_TOPS,
+                    "fp64_equivalent_tflops": oz_fl / (oz_ms * 1e-3) / 1e12,
+                    "ms_per_eval": oz_ms / max(prof_steps, 1), "launches_per_eval": oz_n / max(prof_steps, 1),
+                    "fp64_flops_share": oz_fl / (oz_fl + gemm_fl),
+                    "traffic": pmc_traffic(args.n, args.d, "ozaki")[0]}
             phase_ms = {k: v / max(prof_steps, 1) for k, v in phase_acc.items()}
             third = float(args.n) ** 3 / 3.0   # algorithmic flops of POTRF, TRTRI and LAUUM each
             out["extra"] = {"phase_ms": phase_ms,

@@ -82,6 +82,7 @@ struct OzTriPair {
   int t0, h, t1, Ra, Rb, Pa, Pb;
   long long la_off, lb_off;
   int la_len, lb_len;
+  double ops_a, ops_b;   // int8 ops of its two products (every modulus)
 };
 
 // A factorisation workspace: two n_pad x n_pad buffers and their GEMM schedule.
@@ -175,6 +176,11 @@ struct gpe_ctx {
   double* dozt = nullptr;         // the TRTRI pairs' T = L21 X11
   std::vector<OzTriPair> oz_tri;  // the TRTRI pairs on the int8 cores
   int oz_tri_min = 8192;          // rows of a TRTRI level's blocks from which it runs there
+  double oz_lauum_ops = 0.0;      // int8 ops of the LAUUM product (every modulus)
+  // profiling (gpe_ozaki_stats): events around the k_oz_gemm launches of the last objective
+  std::vector<hipEvent_t> oev;
+  size_t oev_used = 0;
+  double oz_ms = 0.0, oz_launches = 0.0, oz_ops = 0.0, oz_flops64 = 0.0;
   int dbg_skip_wait = -1;         // GPEMU_DEBUG_SKIP_WAIT (tests): a helper gives up its first wait
   size_t small_cap = 0;
 
@@ -1575,6 +1581,8 @@ int oz_prepare(gpe_ctx* c, Fact& F) {
   size_t scratch = 0, nex = (size_t)np2;
   std::vector<unsigned> all = oz_list(NT2, NT2, true, [&](int ti, int) { return (double)(np2 - OZ_T * ti); });
   c->oz_list_len = (int)all.size();
+  c->oz_lauum_ops = 0.0;
+  for (int ti = 0; ti < NT2; ++ti) c->oz_lauum_ops += 2.0 * OZ_T * OZ_T * (ti + 1) * (double)(np2 - OZ_T * ti) * N;
   c->oz_tri.clear();
   for (const auto& prs : F.plan.tri_pairs) {
     if (!oz_tri_level(c, prs)) continue;
@@ -1588,6 +1596,9 @@ int oz_prepare(gpe_ctx* c, Fact& F) {
       const int nti = q.Pb / OZ_T, ntj = q.Pa / OZ_T;
       const std::vector<unsigned> la = oz_list(nti, ntj, false, [&](int, int tj) { return (double)(q.Pa - OZ_T * tj); });
       const std::vector<unsigned> lb = oz_list(nti, ntj, false, [&](int ti, int) { return (double)(OZ_T * (ti + 1)); });
+      q.ops_a = q.ops_b = 0.0;
+      for (int tj = 0; tj < ntj; ++tj) q.ops_a += 2.0 * OZ_T * OZ_T * nti * (double)(q.Pa - OZ_T * tj) * N;
+      for (int ti = 0; ti < nti; ++ti) q.ops_b += 2.0 * OZ_T * OZ_T * ntj * (double)(OZ_T * (ti + 1)) * N;
       q.la_off = (long long)all.size();
       q.la_len = (int)la.size();
       all.insert(all.end(), la.begin(), la.end());
@@ -1612,9 +1623,24 @@ int oz_prepare(gpe_ctx* c, Fact& F) {
   return GPE_OK;
 }
 
-int oz_gemm_crt(gpe_ctx* c, const OzGemm& g, const OzCrt& r, int nti) {
+int oz_gemm_crt(gpe_ctx* c, const OzGemm& g, const OzCrt& r, int nti, double ops, double flops64) {
   const OzConst& k = c->oz_c;
+  if (c->prof) {
+    while (c->oev_used + 2 > c->oev.size()) {
+      hipEvent_t e;
+      HIPCHK(c, hipEventCreate(&e));
+      c->oev.push_back(e);
+    }
+    HIPCHK(c, hipEventRecord(c->oev[c->oev_used], c->stream));
+  }
   hipLaunchKernelGGL(k_oz_gemm, dim3(k.nmod * g.list_len), dim3(256), OZ_LDS, c->stream, g, k);
+  if (c->prof) {
+    HIPCHK(c, hipEventRecord(c->oev[c->oev_used + 1], c->stream));
+    c->oev_used += 2;
+    c->oz_launches += 1.0;
+    c->oz_ops += ops;
+    c->oz_flops64 += flops64;
+  }
   hipLaunchKernelGGL(k_oz_crt, dim3((g.tri ? nti * (nti + 1) / 2 : nti * g.ntj) * 16), dim3(256), 0, c->stream, r, k);
   HIPCHK(c, hipGetLastError());
   return GPE_OK;
@@ -1642,7 +1668,7 @@ int lauum_ozaki(gpe_ctx* c, Fact& F) {
   g.res = c->dozr;
   g.res_bytes = rb;
   OzCrt r{c->dozr, rb, 1, 0, c->dozx, c->dozx, F.A, (long long)F.n_pad, np, np, 1, 1.0};
-  return oz_gemm_crt(c, g, r, NT2);
+  return oz_gemm_crt(c, g, r, NT2, c->oz_lauum_ops, (double)np * np * np / 3.0);
 }
 
 // One pair (t0, h, t1) of a TRTRI level on the int8 cores (plan: the blocks X11 = X(t0:h,
@@ -1696,7 +1722,7 @@ int trtri_pair_ozaki(gpe_ctx* c, Fact& F, int t0, int h, int t1) {
     g.res = c->dozr;
     g.res_bytes = rb;
     OzCrt r{c->dozr, rb, 0, ntj, exA, exB, c->dozt, (long long)q.Pb, q.Rb, q.Ra, 0, 1.0};
-    CHK(oz_gemm_crt(c, g, r, nti));
+    CHK(oz_gemm_crt(c, g, r, nti, q.ops_a, (double)q.Ra * q.Ra * q.Rb));
   }
   // --- X21 = -X22 T
   {
@@ -1726,7 +1752,7 @@ int trtri_pair_ozaki(gpe_ctx* c, Fact& F, int t0, int h, int t1) {
     g.res = c->dozr;
     g.res_bytes = rb;
     OzCrt r{c->dozr, rb, 0, ntj, exA, exB, X21, ld, q.Rb, q.Ra, 0, -1.0};
-    CHK(oz_gemm_crt(c, g, r, nti));
+    CHK(oz_gemm_crt(c, g, r, nti, q.ops_b, (double)q.Rb * q.Rb * q.Ra));
   }
   return GPE_OK;
 }
@@ -1922,6 +1948,7 @@ void gpe_destroy(gpe_ctx* c) {
   if (c->dozx) hipFree(c->dozx);
   if (c->dozl) hipFree(c->dozl);
   if (c->dozt) hipFree(c->dozt);
+  for (hipEvent_t e : c->oev) hipEventDestroy(e);
   if (c->tr.Faug) hipFree(c->tr.Faug);
   if (c->aux.tflags) hipFree(c->aux.tflags);
   if (c->dprobs) hipFree(c->dprobs);
@@ -2004,6 +2031,15 @@ int gpe_set_profiling(gpe_ctx* c, int32_t on) {
 int gpe_phase_times(gpe_ctx* c, double* ms_out, int32_t n) {
   if (!c || !ms_out) return GPE_ERR_ARG;
   for (int i = 0; i < n && i < 8; ++i) ms_out[i] = c->phase_ms[i];
+  return GPE_OK;
+}
+
+int gpe_ozaki_stats(gpe_ctx* c, double* ms_out, double* launches_out, double* int8_ops_out, double* fp64_flops_out) {
+  if (!c) return GPE_ERR_ARG;
+  if (ms_out) *ms_out = c->oz_ms;
+  if (launches_out) *launches_out = c->oz_launches;
+  if (int8_ops_out) *int8_ops_out = c->oz_ops;
+  if (fp64_flops_out) *fp64_flops_out = c->oz_flops64;
   return GPE_OK;
 }
 
@@ -2279,6 +2315,8 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
   if (c->prof) {
     c->gev_used = 0;
     c->gemm_launches = c->gemm_flops = c->gemm_ms = 0.0;
+    c->oev_used = 0;
+    c->oz_ms = c->oz_launches = c->oz_ops = c->oz_flops64 = 0.0;
   }
   if (c->tiny && c->NB == 1 && d <= TINY_DM && q + 1 <= TINY_DM)
     return tiny_objective(c, gp4ml, kernel, hp, n_hp, fitnug, nu, s2, rscale, want_grad != 0, llh_out, grad_out,
@@ -2400,6 +2438,13 @@ done:
       g += ms;
     }
     c->gemm_ms = g;
+    g = 0.0;
+    for (size_t i = 0; i + 1 < c->oev_used; i += 2) {
+      ms = 0.f;
+      (void)hipEventElapsedTime(&ms, c->oev[i], c->oev[i + 1]);
+      g += ms;
+    }
+    c->oz_ms = g;
   }
   return GPE_OK;
 }

@@ -65,6 +65,7 @@ SIGNATURES = {
     "gpe_set_profiling": (_ct.c_int, [_VP, _ct.c_int32]),
     "gpe_phase_times": (_ct.c_int, [_VP, _D, _ct.c_int32]),
     "gpe_gemm_stats": (_ct.c_int, [_VP, _D, _D, _D]),
+    "gpe_ozaki_stats": (_ct.c_int, [_VP, _D, _D, _D, _D]),
     # include/gpemu_dist.h: row-block distributed value objective (RCCL / loopback)
     "gpe_dist_unique_id": (_ct.c_int, [_ct.c_char_p, _ct.c_int32]),
     "gpe_dist_create": (_VP, [_ct.c_int32, _ct.c_int32, _ct.c_int32, _ct.c_char_p]),
@@ -427,6 +428,14 @@ class Context:
         self._check(self.lib.gpe_gemm_stats(self._h, _ct.byref(ms), _ct.byref(nl), _ct.byref(fl)),
                     "gpe_gemm_stats")
         return {"ms": ms.value, "launches": nl.value, "flops": fl.value}
+
+    def ozaki_stats(self):
+        """k_oz_gemm launches of the most recent objective (profiling on): ms, launches,
+        int8 ops and the fp64 flops of the products they emulate."""
+        ms, nl, ops, fl = _ct.c_double(), _ct.c_double(), _ct.c_double(), _ct.c_double()
+        self._check(self.lib.gpe_ozaki_stats(self._h, _ct.byref(ms), _ct.byref(nl), _ct.byref(ops), _ct.byref(fl)),
+                    "gpe_ozaki_stats")
+        return {"ms": ms.value, "launches": nl.value, "int8_ops": ops.value, "fp64_flops": fl.value}
 
 
 _default_ctx = None

@@ -30,11 +30,12 @@
 extern "C" {
 #endif
 
-#define GPE_ABI_VERSION 9   /* 3: gpe_dist_objective gained want_grad / grad_out; 4: sensitivity;
+#define GPE_ABI_VERSION 10  /* 3: gpe_dist_objective gained want_grad / grad_out; 4: sensitivity;
                                 5: gpe_noise_sample (noise_fit); 6: gpe_kernel_grad;
                                 7: gpe_lhc_maximin; 8: gpe_dist_rank_bytes,
                                 gpe_device_synchronize, gpe_build_id;
-                                9: gpe_dist_local_rows takes the basis width q */
+                                9: gpe_dist_local_rows takes the basis width q;
+                                10: gpe_ozaki_stats */
 
 enum gpe_status {
     GPE_OK = 0,
@@ -227,6 +228,14 @@ int gpe_phase_times(gpe_ctx* ctx, double* ms_out, int32_t n);
  * recent objective (profiling on), and their algorithmic flop count. */
 int gpe_gemm_stats(gpe_ctx* ctx, double* ms_out, double* launches_out,
                    double* flops_out);
+
+/* The same for the int8 products of the objective's A^-1 and of the top TRTRI level
+ * (gpemu_ozaki.hpp: the fp64 products emulated exactly on the i8 MFMA, N moduli): their
+ * device time (ms), launch count, int8 multiply-add ops (2 per multiply-add, every modulus)
+ * and the fp64 flops of the products they replace.  Internal instrumentation for bench.py;
+ * the reference has no counterpart. */
+int gpe_ozaki_stats(gpe_ctx* ctx, double* ms_out, double* launches_out, double* int8_ops_out,
+                    double* fp64_flops_out);
 
 #ifdef __cplusplus
 }

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_no_device_fails_loudly():
     lib = native.load_library()
-    assert lib.gpe_abi_version() == 9
+    assert lib.gpe_abi_version() == 10
     if lib.gpe_device_count() == 0:
         with pytest.raises(native.NativeUnavailable):
             native.Context(0)
