@@ -174,6 +174,7 @@ struct gpe_ctx {
   int* dozx = nullptr;            // per-column exponents
   unsigned* dozl = nullptr;       // k_oz_gemm's tile lists (the LAUUM's, then every TRTRI pair's)
   double* dozt = nullptr;         // the TRTRI pairs' T = L21 X11
+  hipEvent_t ev_oz = nullptr;     // the first int8 TRTRI pair's L21 planes are ready (stream2)
   std::vector<OzTriPair> oz_tri;  // the TRTRI pairs on the int8 cores
   int oz_tri_min = 8192;          // rows of a TRTRI level's blocks from which it runs there
   double oz_lauum_ops = 0.0;      // int8 ops of the LAUUM product (every modulus)
@@ -1257,7 +1258,8 @@ int ensure_xdiag(gpe_ctx* c, Fact& F) {
   return GPE_OK;
 }
 
-int trtri_pair_ozaki(gpe_ctx* c, Fact& F, int t0, int h, int t1);
+int trtri_pair_ozaki(gpe_ctx* c, Fact& F, int t0, int h, int t1, bool l21_ready);
+int oz_l21_ahead(gpe_ctx* c, Fact& F, int t0, int h, int t1);
 bool oz_tri_level(const gpe_ctx* c, const std::vector<std::array<int, 3>>& prs);
 
 // X = L^-1 by levels; with ozaki (the objective's gradient) the levels whose blocks are at
@@ -1266,9 +1268,21 @@ int trtri(gpe_ctx* c, Fact& F, bool ozaki = false) {
   CHK(build_plan(c, F));
   CHK(ensure_xdiag(c, F));
   const Plan& pl = F.plan;
+  // the first int8 pair's L21 (final since the Cholesky) is converted on the second stream
+  // while the fp64 levels below it run
+  int first = -1;
+  for (size_t lv = 0; lv < pl.tri_pairs.size() && ozaki && first < 0; ++lv)
+    if (oz_tri_level(c, pl.tri_pairs[lv])) first = (int)lv;
+  if (first >= 0) {
+    const auto& pr = pl.tri_pairs[first][0];
+    CHK(oz_l21_ahead(c, F, pr[0], pr[1], pr[2]));
+  }
   for (size_t lv = 0; lv < pl.tri_pairs.size(); ++lv) {
     if (ozaki && oz_tri_level(c, pl.tri_pairs[lv])) {
-      for (const auto& pr : pl.tri_pairs[lv]) CHK(trtri_pair_ozaki(c, F, pr[0], pr[1], pr[2]));
+      for (size_t i = 0; i < pl.tri_pairs[lv].size(); ++i) {
+        const auto& pr = pl.tri_pairs[lv][i];
+        CHK(trtri_pair_ozaki(c, F, pr[0], pr[1], pr[2], (int)lv == first && i == 0));
+      }
       continue;
     }
     CHK(launch_gemm_range(c, pl.launches[pl.trtri[2 * lv]]));
@@ -1677,17 +1691,56 @@ int lauum_ozaki(gpe_ctx* c, Fact& F) {
 //   X21 = -X22 T       (rows of X22, k <= the row: kend = 256 (ti + 1), against columns of T)
 // T goes to a scratch block (column-major, so its columns are the second product's rows);
 // X21 over B's tile block (h, t0), as the fp64 launches' pb
-int trtri_pair_ozaki(gpe_ctx* c, Fact& F, int t0, int h, int t1) {
-  CHK(oz_prepare(c, F));
-  const OzTriPair* qp = nullptr;
+const OzTriPair* oz_pair(const gpe_ctx* c, int t0, int h, int t1) {
   for (const OzTriPair& q : c->oz_tri)
-    if (q.t0 == t0 && q.h == h && q.t1 == t1) qp = &q;
+    if (q.t0 == t0 && q.h == h && q.t1 == t1) return &q;
+  return nullptr;
+}
+
+// the first product's L21 side: row exponents and int8 planes of the rows of L21, on stream st
+int oz_l21(gpe_ctx* c, Fact& F, const OzTriPair& q, hipStream_t st) {
+  const OzConst& k = c->oz_c;
+  const long long ld = F.n_pad;
+  const double* L21 = F.A + (long long)q.h * TILE + (long long)q.t0 * TILE * ld;
+  int* exA = c->dozx;
+  const long long pA = (long long)q.Pb * q.Pa;
+  HIPCHK(c, hipMemsetAsync(exA, 0, q.Pb * sizeof(int), st));
+  hipLaunchKernelGGL(k_oz_rowexp<true>, dim3(q.Pb / 64, (q.Ra + 255) / 256), dim3(256), 0, st, L21, ld, q.Rb, q.Pb,
+                     q.Ra, 0, k.beta, exA);
+  hipLaunchKernelGGL(k_oz_il_to_ex, dim3((q.Pb + 255) / 256), dim3(256), 0, st, exA, q.Pb, k.beta);
+  hipLaunchKernelGGL(k_oz_split_rect<true>, dim3(q.Pb / 64, q.Pa / 64), dim3(256), 0, st, L21, ld, q.Rb, q.Ra, 0,
+                     exA, c->dozp, pA, (long long)q.Pa, q.Pa, k);
+  HIPCHK(c, hipGetLastError());
+  return GPE_OK;
+}
+
+// oz_l21 of a pair on the second stream, forked from the context stream (L is final there)
+int oz_l21_ahead(gpe_ctx* c, Fact& F, int t0, int h, int t1) {
+  CHK(oz_prepare(c, F));
+  const OzTriPair* q = oz_pair(c, t0, h, t1);
+  if (!q) return fail(c, GPE_ERR_STATE, "internal error: TRTRI pair without an int8 plan");
+  if (!c->ev_oz) HIPCHK(c, hipEventCreateWithFlags(&c->ev_oz, hipEventDisableTiming));
+  HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+  CHK(oz_l21(c, F, *q, c->stream2));
+  HIPCHK(c, hipEventRecord(c->ev_oz, c->stream2));
+  return GPE_OK;
+}
+
+// One pair (t0, h, t1) of a TRTRI level on the int8 cores (plan: the blocks X11 = X(t0:h,
+// t0:h), X22 = X(h:t1, h:t1) already inverted, L21 = L(h:t1, t0:h)):
+//   T   = L21 X11      (rows of L21 against columns of X11, k >= the column: kbeg = 256 tj)
+//   X21 = -X22 T       (rows of X22, k <= the row: kend = 256 (ti + 1), against columns of T)
+// T goes to a scratch block (column-major, so its columns are the second product's rows);
+// X21 over B's tile block (h, t0), as the fp64 launches' pb.  l21_ready: oz_l21_ahead ran.
+int trtri_pair_ozaki(gpe_ctx* c, Fact& F, int t0, int h, int t1, bool l21_ready) {
+  CHK(oz_prepare(c, F));
+  const OzTriPair* qp = oz_pair(c, t0, h, t1);
   if (!qp) return fail(c, GPE_ERR_STATE, "internal error: TRTRI pair without an int8 plan");
   const OzTriPair& q = *qp;
   const OzConst& k = c->oz_c;
   const long long ld = F.n_pad;
   auto tile = [&](double* M, int i, int j) { return M + (long long)i * TILE + (long long)j * TILE * ld; };
-  const double* L21 = tile(F.A, h, t0);
   const double* X11 = tile(F.B, t0, t0);
   const double* X22 = tile(F.B, h, h);
   double* X21 = tile(F.B, h, t0);
@@ -1700,13 +1753,9 @@ int trtri_pair_ozaki(gpe_ctx* c, Fact& F, int t0, int h, int t1) {
     const long long pA = (long long)q.Pb * q.Pa, pB = (long long)q.Pa * q.Pa;
     int8_t* PA = c->dozp;
     int8_t* PB = c->dozp + (size_t)k.nmod * pA;
-    HIPCHK(c, hipMemsetAsync(exA, 0, q.Pb * sizeof(int), c->stream));
-    hipLaunchKernelGGL(k_oz_rowexp<true>, dim3(q.Pb / 64, (q.Ra + 255) / 256), dim3(256), 0, c->stream, L21, ld, q.Rb, q.Pb,
-                       q.Ra, 0, k.beta, exA);
-    hipLaunchKernelGGL(k_oz_il_to_ex, dim3((q.Pb + 255) / 256), dim3(256), 0, c->stream, exA, q.Pb, k.beta);
+    if (l21_ready) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_oz, 0));
+    else CHK(oz_l21(c, F, q, c->stream));
     hipLaunchKernelGGL(k_oz_rowexp<false>, dim3(q.Pa / 4), dim3(256), 0, c->stream, X11, ld, q.Ra, q.Pa, q.Ra, 1, k.beta, exB);
-    hipLaunchKernelGGL(k_oz_split_rect<true>, dim3(q.Pb / 64, q.Pa / 64), dim3(256), 0, c->stream, L21, ld, q.Rb, q.Ra, 0,
-                       exA, PA, pA, (long long)q.Pa, q.Pa, k);
     hipLaunchKernelGGL(k_oz_split_rect<false>, dim3(q.Pa, (q.Pa + 2047) / 2048), dim3(256), 0, c->stream, X11, ld, q.Ra, q.Ra,
                        1, exB, PB, pB, (long long)q.Pa, q.Pa, k);
     OzGemm g;
@@ -1948,6 +1997,7 @@ void gpe_destroy(gpe_ctx* c) {
   if (c->dozx) hipFree(c->dozx);
   if (c->dozl) hipFree(c->dozl);
   if (c->dozt) hipFree(c->dozt);
+  if (c->ev_oz) hipEventDestroy(c->ev_oz);
   for (hipEvent_t e : c->oev) hipEventDestroy(e);
   if (c->tr.Faug) hipFree(c->tr.Faug);
   if (c->aux.tflags) hipFree(c->aux.tflags);
