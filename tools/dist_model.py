@@ -146,6 +146,10 @@ def main():
     ap.add_argument("--alpha-us", type=float, default=25.0)
     ap.add_argument("--beta2", type=float, default=64.0, help="GB/s per rank at P=2")
     ap.add_argument("--beta", type=float, default=300.0, help="GB/s per rank at P>=4")
+    ap.add_argument("--trtri-overlap", choices=("none", "prev-level", "full"), default="none",
+                    help="TRTRI all-gathers hidden behind compute: none (round 5, in series), prev-level "
+                         "(level l's gathers beside level l-1's products: round-6 verdict option 1), full "
+                         "(a ring pass of X row blocks beside the products: option 2, upper bound)")
     args = ap.parse_args()
     widths = [tuple(int(v) for v in e.split(":")) for e in args.widths.split(",")]
     nb = -(-args.points // TILE)
@@ -176,7 +180,30 @@ def main():
             # divide; the bulk does (taken as not overlapping the chain: at P = 1 this is the
             # measurement)
             t_sweep = chain + comm_sweep + bulk / P
-            row["predicted_ms"] = t_sweep + grad / P + comm_tr + comm_rest
+            t_grad = grad / P + comm_tr
+            if P > 1 and args.trtri_overlap != "none":
+                # per level: its products' share of the gradient compute (n S^2 of n^3 / 3 for the
+                # TRTRI's 1 / 2 of it) and its gathers' time
+                lv = trtri_levels(nb, P, cap * 8)
+                tot = sum(s_ * s_ for (s_, *_r) in lv)
+                trtri_ms = (grad / P) * 0.5
+                comp = [trtri_ms * (s_ * s_) / tot for (s_, *_r) in lv]
+                gath = []
+                for (s_, cc, g1, s1, g2, s2, pairs) in lv:
+                    a = s_ // 2
+                    b = 0
+                    for j0 in range(0, a, cc):
+                        cw, rows1 = min(cc, a - j0), a - j0
+                        b += (P - 1) * (sum(-(-rows1 // P) * cw for _ in pairs) +
+                                        sum(cw * -(-(t1 - h) // P) for (_, h, t1) in pairs)) * T2B
+                    gath.append(b / beta * 1e3 + 2 * args.alpha_us * 1e-3 * (-(-a // cc)))
+                if args.trtri_overlap == "prev-level":
+                    hidden = sum(min(gath[i], comp[i - 1]) for i in range(1, len(lv)))
+                else:
+                    hidden = min(sum(gath), grad / P)
+                t_grad = grad / P + comm_tr - hidden
+                row["trtri_comm_hidden_ms"] = hidden
+            row["predicted_ms"] = t_sweep + t_grad + comm_rest
             row["speedup_vs_p1"] = args.p1_ms / row["predicted_ms"]
         rows.append(row)
     for r in rows:

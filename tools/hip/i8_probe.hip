@@ -275,6 +275,140 @@ __global__ void __launch_bounds__(256) k_i8peak32r(const v4i* __restrict__ rnd, 
   out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
+// Variants 4-6: the production loop of k_oz_gemm (gpemu_ozaki.hpp: 256 x 256 tiles, one k-step's
+// MFMAs with the next k-step's fragment reads interleaved, one barrier per 64-k stage) with
+// MODE 0: direct global -> LDS loads (4-stage ring, production); 1: register staging
+// (global_load_dwordx4 into VGPRs three stages ahead, ds_write_b128 into a 3-buffer ring);
+// 2: no global loads at all (the MFMA + LDS-read pipeline alone, on stale LDS)
+template <int MODE>
+__global__ void __launch_bounds__(256, 1) k_i8gemm_p(const int8_t* __restrict__ A, long long lda,
+                                                     const int8_t* __restrict__ B, long long ldb,
+                                                     int* __restrict__ C, long long ldc, int K, int mt) {
+  extern __shared__ __attribute__((aligned(16))) int8_t lds[];
+  constexpr int NB = MODE == 1 ? 3 : 4;
+  const int ti = blockIdx.x % mt, tj = blockIdx.x / mt;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = (wave >> 1) * 128, wn = (wave & 1) * 128;
+  const int kp = (lane & 3) ^ ((lane >> 4) & 3);
+  const int8_t* sa = A + (long long)ti * T3 * lda + (long long)(16 * wave + (lane >> 2)) * lda + 16 * kp;
+  const int8_t* sb = B + (long long)tj * T3 * ldb + (long long)(16 * wave + (lane >> 2)) * ldb + 16 * kp;
+  auto bufp = [&](int s) { return lds + (s % NB) * 2 * OP3; };
+  auto stage = [&](int s) {   // MODE 0
+    int8_t* As = bufp(s);
+    int8_t* Bs = As + OP3;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int w = wave + 4 * p;
+      glds16(sa + (long long)p * 64 * lda + (long long)s * SK3, As + 16 * w * SK3);
+      glds16(sb + (long long)p * 64 * ldb + (long long)s * SK3, Bs + 16 * w * SK3);
+    }
+  };
+  v4i rg[2][8];   // MODE 1: two stages of staging registers
+  auto gload = [&](int s, v4i (&r)[8]) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      r[2 * p] = *reinterpret_cast<const v4i*>(sa + (long long)p * 64 * lda + (long long)s * SK3);
+      r[2 * p + 1] = *reinterpret_cast<const v4i*>(sb + (long long)p * 64 * ldb + (long long)s * SK3);
+    }
+  };
+  auto lwrite = [&](int s, const v4i (&r)[8]) {
+    int8_t* As = bufp(s);
+    int8_t* Bs = As + OP3;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int w = wave + 4 * p;
+      *reinterpret_cast<v4i*>(As + 16 * w * SK3 + 16 * lane) = r[2 * p];
+      *reinterpret_cast<v4i*>(Bs + 16 * w * SK3 + 16 * lane) = r[2 * p + 1];
+    }
+  };
+  v16i acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v16i{};
+  const int ns = K / SK3;
+  const int r32 = lane & 31, h = lane >> 5, sw = (r32 >> 2) & 3;
+  auto frags = [&](int s, int ks, v4i (&af)[4], v4i (&bf)[4]) {
+    const int8_t* As = bufp(s);
+    const int8_t* Bs = As + OP3;
+    const int slot = ((2 * ks + h) ^ sw) * 16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const v4i*>(As + (wm + 32 * i + r32) * SK3 + slot);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const v4i*>(Bs + (wn + 32 * j + r32) * SK3 + slot);
+  };
+  auto mfmas = [&](const v4i (&af)[4], const v4i (&bf)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(bf[j], af[i], acc[i][j], 0, 0, 0);
+  };
+  auto wait_stage = [&](int s) {
+    if constexpr (MODE == 0) {
+      const int later = min(ns - 1, s + 2) - s;
+      if (later >= 2) vmwait<16>();
+      else if (later == 1) vmwait<8>();
+      else vmwait<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  v4i ca[4], cb[4], na[4], nb[4];
+  if constexpr (MODE == 0) {
+    for (int s = 0; s < min(ns, 3); ++s) stage(s);
+    wait_stage(0);
+    if (ns > 3) stage(3);
+  } else if constexpr (MODE == 1) {
+    gload(0, rg[0]);
+    if (ns > 1) gload(1, rg[1]);
+    vmwait<0>();
+    lwrite(0, rg[0]);
+    if (ns > 2) gload(2, rg[0]);
+    wait_stage(0);
+  } else {
+    wait_stage(0);
+  }
+  frags(0, 0, ca, cb);
+  for (int s = 0; s < ns; ++s) {
+    mfmas(ca, cb);
+    frags(s, 1, na, nb);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + 1 < ns) {
+      if constexpr (MODE == 1) {
+        // stage s + 1's registers (loaded two iterations ago) into buffer (s + 1) % 3, whose
+        // last reads (stage s - 2) every wave finished before the previous barrier
+        if (s + 2 < ns) vmwait<8>(); else vmwait<0>();
+        lwrite(s + 1, rg[(s + 1) & 1]);
+        if (s + 3 < ns) gload(s + 3, rg[(s + 1) & 1]);
+      }
+      wait_stage(s + 1);
+      if constexpr (MODE == 0)
+        if (s + 4 < ns) stage(s + 4);
+      frags(s + 1, 0, ca, cb);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas(na, nb);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long long m = (long long)ti * T3 + wm + 32 * i + r32;
+        const long long n = (long long)tj * T3 + wn + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * h;
+        C[m + n * ldc] = acc[i][j][r];
+      }
+}
+
 int main(int argc, char** argv) {
   const int big = argc > 1 ? atoi(argv[1]) : 8192;
   const int var = argc > 2 ? atoi(argv[2]) : 0;
@@ -339,11 +473,15 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dc, (size_t)M * N * 4));
     CK(hipMemcpy(da, ha.data(), ha.size(), hipMemcpyHostToDevice));
     CK(hipMemcpy(db, hb.data(), hb.size(), hipMemcpyHostToDevice));
-    const int TT = var ? TB : T;
+    const int TT = var >= 3 ? T3 : (var ? TB : T);
     const int mt = M / TT, nt = N / TT;
-    const size_t lds = var == 3 ? NBUF3 * 2 * OP3 : (var ? 4 * OPND2 : 4 * OPND);
+    const size_t lds = var >= 3 ? NBUF3 * 2 * OP3 : (var ? 4 * OPND2 : 4 * OPND);
     auto run = [&]() {
-      if (var == 3) hipLaunchKernelGGL(k_i8gemm_c, dim3(mt * nt), dim3(256), lds, 0, da, (long long)K, db, (long long)K, dc, (long long)M, K, mt);
+      if (var == 7) hipLaunchKernelGGL(k_i8gemm_p<0>, dim3(mt * nt), dim3(256), lds, 0, da, 0ll, db, 0ll, dc, (long long)M, K, mt);
+      else if (var == 4) hipLaunchKernelGGL(k_i8gemm_p<0>, dim3(mt * nt), dim3(256), lds, 0, da, (long long)K, db, (long long)K, dc, (long long)M, K, mt);
+      else if (var == 5) hipLaunchKernelGGL(k_i8gemm_p<1>, dim3(mt * nt), dim3(256), lds, 0, da, (long long)K, db, (long long)K, dc, (long long)M, K, mt);
+      else if (var == 6) hipLaunchKernelGGL(k_i8gemm_p<2>, dim3(mt * nt), dim3(256), lds, 0, da, (long long)K, db, (long long)K, dc, (long long)M, K, mt);
+      else if (var == 3) hipLaunchKernelGGL(k_i8gemm_c, dim3(mt * nt), dim3(256), lds, 0, da, (long long)K, db, (long long)K, dc, (long long)M, K, mt);
       else if (var) hipLaunchKernelGGL(k_i8gemm_b, dim3(mt * nt), dim3(256), lds, 0, da, (long long)K, db, (long long)K, dc, (long long)M, K, mt);
       else hipLaunchKernelGGL(k_i8gemm, dim3(mt * nt), dim3(256), lds, 0, da, (long long)K, db, (long long)K, dc, (long long)M, K, mt);
     };
