@@ -78,12 +78,6 @@ constexpr int FACT_FLAG_INTS = 6;
 
 // one TRTRI block pair on the int8 cores (trtri_pair_ozaki): rows of X11 / X22 (Ra / Rb),
 // padded to 256 (Pa / Pb), and its two products' tile lists in dozl
-struct OzTriPair {
-  int t0, h, t1, Ra, Rb, Pa, Pb;
-  long long la_off, lb_off;
-  int la_len, lb_len;
-  double ops_a, ops_b;   // int8 ops of its two products (every modulus)
-};
 
 // A factorisation workspace: two n_pad x n_pad buffers and their GEMM schedule.
 struct Fact {
@@ -1506,75 +1500,6 @@ int trsv_lower(gpe_ctx* c, Fact& F, const double* R, long long ldr, int P, doubl
 constexpr int OZ_MIN_NP = 2048, OZ_MAX_NP = 32768;
 bool oz_use(const gpe_ctx* c) { return c->oz_on && c->n_pad >= OZ_MIN_NP && c->n_pad <= OZ_MAX_NP; }
 
-// moduli and reconstruction constants for operand sums of length up to np2
-OzConst oz_consts(int nmod, int np2) {
-  static const int mods[OZ_MAXMOD] = {256, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217, 211, 199, 197, 193, 191};
-  OzConst k{};
-  k.nmod = nmod;
-  double log2M = 0.0, Md = 1.0;
-  for (int l = 0; l < nmod; ++l) {
-    log2M += std::log2((double)mods[l]);
-    Md *= (double)mods[l];
-  }
-  k.Md = Md;
-  // |C'| <= np2 2^(2 beta) < M / 2
-  k.beta = std::min(53, (int)std::floor((log2M - 1.0 - std::log2((double)np2) - 1e-9) / 2.0));
-  for (int l = 0; l < nmod; ++l) {
-    const int m = mods[l];
-    k.m[l] = m;
-    k.c16[l] = 65536 % m;
-    k.inv[l] = 1.0f / (float)m;
-    long long Mm = 1;   // (M / m) mod m
-    for (int j = 0; j < nmod; ++j)
-      if (j != l) Mm = (Mm * (mods[j] % m)) % m;
-    int y = 1;          // its inverse mod m
-    while ((Mm * y) % m != 1) ++y;
-    // y / m = rhi + rlo, rhi on the 2^-41 grid (exact products and sums in k_oz_crt)
-    const long long num = (long long)y << 41;
-    const long long Q = num / m, R = num - Q * m;
-    k.rhi[l] = std::ldexp((double)Q, -41);
-    k.rlo[l] = std::ldexp((double)R / (double)m, -41);
-  }
-  return k;
-}
-
-// A product's tile list: blocks of OZ_BR tile rows x OZ_BC tile columns (clipped to the lower
-// triangle when lower), heaviest first, greedily binned by work into 8 XCD bins, interleaved
-// position by position (bin = position % 8, the XCD under round-robin dispatch), bins padded
-// to one length with 0xffffffff.  An XCD's 32 CUs then run one block at a time: its tiles
-// share 4 A panels and 8 B panels (a whole tile row on one XCD shared one A panel among 32
-// different B panels: L2 hit rate ~0.5)
-template <class W>
-std::vector<unsigned> oz_list(int nti, int ntj, bool lower, W work) {
-  constexpr int OZ_BR = 4, OZ_BC = 8;
-  struct Blk { double w; std::vector<unsigned> t; };
-  std::vector<Blk> blks;
-  for (int r0 = 0; r0 < nti; r0 += OZ_BR)
-    for (int c0 = 0; c0 < ntj && (!lower || c0 <= r0 + OZ_BR - 1); c0 += OZ_BC) {
-      Blk b{0.0, {}};
-      for (int ti = r0; ti < std::min(nti, r0 + OZ_BR); ++ti)
-        for (int tj = c0; tj < std::min(lower ? ti + 1 : ntj, c0 + OZ_BC); ++tj) {
-          b.t.push_back(((unsigned)ti << 16) | (unsigned)tj);
-          b.w += work(ti, tj);
-        }
-      if (!b.t.empty()) blks.push_back(std::move(b));
-    }
-  std::stable_sort(blks.begin(), blks.end(), [](const Blk& x, const Blk& y) { return x.w / x.t.size() > y.w / y.t.size(); });
-  std::vector<std::vector<unsigned>> bins(8);
-  std::vector<double> load(8, 0.0);
-  for (const Blk& b : blks) {
-    const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-    load[x] += b.w;
-    bins[x].insert(bins[x].end(), b.t.begin(), b.t.end());
-  }
-  size_t longest = 0;
-  for (auto& b : bins) longest = std::max(longest, b.size());
-  std::vector<unsigned> list(8 * longest, 0xffffffffu);
-  for (int x = 0; x < 8; ++x)
-    for (size_t q = 0; q < bins[x].size(); ++q) list[8 * q + x] = bins[x][q];
-  return list;
-}
-
 // the TRTRI levels on the int8 cores: every pair of a level whose blocks have at least
 // oz_tri_min rows (GPEMU_OZAKI_TRI_MIN; the levels below stay fp64: their products are a
 // few short tiles)
@@ -1601,26 +1526,9 @@ int oz_prepare(gpe_ctx* c, Fact& F) {
   for (const auto& prs : F.plan.tri_pairs) {
     if (!oz_tri_level(c, prs)) continue;
     for (const auto& pr : prs) {
-      OzTriPair q;
-      q.t0 = pr[0]; q.h = pr[1]; q.t1 = pr[2];
-      q.Ra = (q.h - q.t0) * TILE;
-      q.Rb = (q.t1 - q.h) * TILE;
-      q.Pa = (q.Ra + OZ_T - 1) / OZ_T * OZ_T;
-      q.Pb = (q.Rb + OZ_T - 1) / OZ_T * OZ_T;
-      const int nti = q.Pb / OZ_T, ntj = q.Pa / OZ_T;
-      const std::vector<unsigned> la = oz_list(nti, ntj, false, [&](int, int tj) { return (double)(q.Pa - OZ_T * tj); });
-      const std::vector<unsigned> lb = oz_list(nti, ntj, false, [&](int ti, int) { return (double)(OZ_T * (ti + 1)); });
-      q.ops_a = q.ops_b = 0.0;
-      for (int tj = 0; tj < ntj; ++tj) q.ops_a += 2.0 * OZ_T * OZ_T * nti * (double)(q.Pa - OZ_T * tj) * N;
-      for (int ti = 0; ti < nti; ++ti) q.ops_b += 2.0 * OZ_T * OZ_T * ntj * (double)(OZ_T * (ti + 1)) * N;
-      q.la_off = (long long)all.size();
-      q.la_len = (int)la.size();
-      all.insert(all.end(), la.begin(), la.end());
-      q.lb_off = (long long)all.size();
-      q.lb_len = (int)lb.size();
-      all.insert(all.end(), lb.begin(), lb.end());
-      planes = std::max(planes, (size_t)N * q.Pa * (q.Pa + q.Pb));
-      resid = std::max(resid, (size_t)N * q.Pa * q.Pb);
+      const OzTriPair q = oz_tri_pair_plan(pr[0], pr[1], pr[2], N, all);
+      planes = std::max(planes, q.planes_bytes(N));
+      resid = std::max(resid, q.resid_bytes(N));
       scratch = std::max(scratch, (size_t)q.Pa * q.Pb);
       nex = std::max(nex, (size_t)(q.Pa + q.Pb));
       c->oz_tri.push_back(q);
@@ -1685,31 +1593,16 @@ int lauum_ozaki(gpe_ctx* c, Fact& F) {
   return oz_gemm_crt(c, g, r, NT2, c->oz_lauum_ops, (double)np * np * np / 3.0);
 }
 
-// One pair (t0, h, t1) of a TRTRI level on the int8 cores (plan: the blocks X11 = X(t0:h,
-// t0:h), X22 = X(h:t1, h:t1) already inverted, L21 = L(h:t1, t0:h)):
-//   T   = L21 X11      (rows of L21 against columns of X11, k >= the column: kbeg = 256 tj)
-//   X21 = -X22 T       (rows of X22, k <= the row: kend = 256 (ti + 1), against columns of T)
-// T goes to a scratch block (column-major, so its columns are the second product's rows);
-// X21 over B's tile block (h, t0), as the fp64 launches' pb
+// the int8 plan of TRTRI pair (t0, h, t1) (oz_prepare)
 const OzTriPair* oz_pair(const gpe_ctx* c, int t0, int h, int t1) {
   for (const OzTriPair& q : c->oz_tri)
     if (q.t0 == t0 && q.h == h && q.t1 == t1) return &q;
   return nullptr;
 }
 
-// the first product's L21 side: row exponents and int8 planes of the rows of L21, on stream st
+// the first product's L21 side (oz_l21_launch) on stream st
 int oz_l21(gpe_ctx* c, Fact& F, const OzTriPair& q, hipStream_t st) {
-  const OzConst& k = c->oz_c;
-  const long long ld = F.n_pad;
-  const double* L21 = F.A + (long long)q.h * TILE + (long long)q.t0 * TILE * ld;
-  int* exA = c->dozx;
-  const long long pA = (long long)q.Pb * q.Pa;
-  HIPCHK(c, hipMemsetAsync(exA, 0, q.Pb * sizeof(int), st));
-  hipLaunchKernelGGL(k_oz_rowexp<true>, dim3(q.Pb / 64, (q.Ra + 255) / 256), dim3(256), 0, st, L21, ld, q.Rb, q.Pb,
-                     q.Ra, 0, k.beta, exA);
-  hipLaunchKernelGGL(k_oz_il_to_ex, dim3((q.Pb + 255) / 256), dim3(256), 0, st, exA, q.Pb, k.beta);
-  hipLaunchKernelGGL(k_oz_split_rect<true>, dim3(q.Pb / 64, q.Pa / 64), dim3(256), 0, st, L21, ld, q.Rb, q.Ra, 0,
-                     exA, c->dozp, pA, (long long)q.Pa, q.Pa, k);
+  oz_l21_launch(st, c->oz_c, q, F.A + (long long)q.h * TILE + (long long)q.t0 * TILE * F.n_pad, F.n_pad, c->dozp, c->dozx);
   HIPCHK(c, hipGetLastError());
   return GPE_OK;
 }
@@ -1727,82 +1620,23 @@ int oz_l21_ahead(gpe_ctx* c, Fact& F, int t0, int h, int t1) {
   return GPE_OK;
 }
 
-// One pair (t0, h, t1) of a TRTRI level on the int8 cores (plan: the blocks X11 = X(t0:h,
-// t0:h), X22 = X(h:t1, h:t1) already inverted, L21 = L(h:t1, t0:h)):
-//   T   = L21 X11      (rows of L21 against columns of X11, k >= the column: kbeg = 256 tj)
-//   X21 = -X22 T       (rows of X22, k <= the row: kend = 256 (ti + 1), against columns of T)
-// T goes to a scratch block (column-major, so its columns are the second product's rows);
-// X21 over B's tile block (h, t0), as the fp64 launches' pb.  l21_ready: oz_l21_ahead ran.
+// One pair (t0, h, t1) of a TRTRI level on the int8 cores (oz_tri_pair_launches): L21 from
+// A, X11 / X22 / X21 in B, T in the scratch block.  l21_ready: oz_l21_ahead ran.
 int trtri_pair_ozaki(gpe_ctx* c, Fact& F, int t0, int h, int t1, bool l21_ready) {
   CHK(oz_prepare(c, F));
   const OzTriPair* qp = oz_pair(c, t0, h, t1);
   if (!qp) return fail(c, GPE_ERR_STATE, "internal error: TRTRI pair without an int8 plan");
-  const OzTriPair& q = *qp;
-  const OzConst& k = c->oz_c;
   const long long ld = F.n_pad;
   auto tile = [&](double* M, int i, int j) { return M + (long long)i * TILE + (long long)j * TILE * ld; };
-  const double* X11 = tile(F.B, t0, t0);
-  const double* X22 = tile(F.B, h, h);
-  double* X21 = tile(F.B, h, t0);
-  int* exA = c->dozx;
-  int* exB = c->dozx + q.Pb;
-  const int nti = q.Pb / OZ_T, ntj = q.Pa / OZ_T;
-  const long long rb = (long long)nti * ntj * OZ_T * OZ_T;
-  // --- T = L21 X11
-  {
-    const long long pA = (long long)q.Pb * q.Pa, pB = (long long)q.Pa * q.Pa;
-    int8_t* PA = c->dozp;
-    int8_t* PB = c->dozp + (size_t)k.nmod * pA;
-    if (l21_ready) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_oz, 0));
-    else CHK(oz_l21(c, F, q, c->stream));
-    hipLaunchKernelGGL(k_oz_rowexp<false>, dim3(q.Pa / 4), dim3(256), 0, c->stream, X11, ld, q.Ra, q.Pa, q.Ra, 1, k.beta, exB);
-    hipLaunchKernelGGL(k_oz_split_rect<false>, dim3(q.Pa, (q.Pa + 2047) / 2048), dim3(256), 0, c->stream, X11, ld, q.Ra, q.Ra,
-                       1, exB, PB, pB, (long long)q.Pa, q.Pa, k);
-    OzGemm g;
-    g.a = OzOpnd{PA, pA, q.Pa, 0};
-    g.b = OzOpnd{PB, pB, q.Pa, 0};
-    g.list = c->dozl + q.la_off;
-    g.list_len = q.la_len;
-    g.K = q.Pa;
-    g.kbeg = 2;
-    g.kend = 0;
-    g.tri = 0;
-    g.ntj = ntj;
-    g.res = c->dozr;
-    g.res_bytes = rb;
-    OzCrt r{c->dozr, rb, 0, ntj, exA, exB, c->dozt, (long long)q.Pb, q.Rb, q.Ra, 0, 1.0};
-    CHK(oz_gemm_crt(c, g, r, nti, q.ops_a, (double)q.Ra * q.Ra * q.Rb));
-  }
-  // --- X21 = -X22 T
-  {
-    const long long pA = (long long)q.Pb * q.Pb, pB = (long long)q.Pa * q.Pb;
-    int8_t* PA = c->dozp;
-    int8_t* PB = c->dozp + (size_t)k.nmod * pA;
-    HIPCHK(c, hipMemsetAsync(exA, 0, q.Pb * sizeof(int), c->stream));
-    hipLaunchKernelGGL(k_oz_rowexp<true>, dim3(q.Pb / 64, (q.Rb + 255) / 256), dim3(256), 0, c->stream, X22, ld, q.Rb, q.Pb,
-                       q.Rb, 2, k.beta, exA);
-    hipLaunchKernelGGL(k_oz_il_to_ex, dim3((q.Pb + 255) / 256), dim3(256), 0, c->stream, exA, q.Pb, k.beta);
-    hipLaunchKernelGGL(k_oz_rowexp<false>, dim3(q.Pa / 4), dim3(256), 0, c->stream, c->dozt, (long long)q.Pb, q.Ra, q.Pa,
-                       q.Rb, 0, k.beta, exB);
-    hipLaunchKernelGGL(k_oz_split_rect<true>, dim3(q.Pb / 64, q.Pb / 64), dim3(256), 0, c->stream, X22, ld, q.Rb, q.Rb, 2,
-                       exA, PA, pA, (long long)q.Pb, q.Pb, k);
-    hipLaunchKernelGGL(k_oz_split_rect<false>, dim3(q.Pa, (q.Pb + 2047) / 2048), dim3(256), 0, c->stream, c->dozt,
-                       (long long)q.Pb, q.Ra, q.Rb, 0, exB, PB, pB, (long long)q.Pb, q.Pb, k);
-    OzGemm g;
-    g.a = OzOpnd{PA, pA, q.Pb, 0};
-    g.b = OzOpnd{PB, pB, q.Pb, 0};
-    g.list = c->dozl + q.lb_off;
-    g.list_len = q.lb_len;
-    g.K = q.Pb;
-    g.kbeg = 0;
-    g.kend = 1;
-    g.tri = 0;
-    g.ntj = ntj;
-    g.res = c->dozr;
-    g.res_bytes = rb;
-    OzCrt r{c->dozr, rb, 0, ntj, exA, exB, X21, ld, q.Rb, q.Ra, 0, -1.0};
-    CHK(oz_gemm_crt(c, g, r, nti, q.ops_b, (double)q.Rb * q.Rb * q.Ra));
-  }
+  if (l21_ready) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_oz, 0));
+  int rc = GPE_OK;
+  oz_tri_pair_launches(c->stream, c->oz_c, *qp, c->dozl, tile(F.A, h, t0), tile(F.B, t0, t0), tile(F.B, h, h),
+                       tile(F.B, h, t0), ld, c->dozt, c->dozp, c->dozr, c->dozx, l21_ready,
+                       [&](const OzGemm& g, const OzCrt& r, int nti, double ops, double fl) {
+                         if (rc == GPE_OK) rc = oz_gemm_crt(c, g, r, nti, ops, fl);
+                       });
+  CHK(rc);
+  HIPCHK(c, hipGetLastError());
   return GPE_OK;
 }
 

@@ -56,6 +56,7 @@
 #include "../../include/gpemu_dist.h"
 #include "gpemu_kernels.hpp"
 #include "gpemu_small.hpp"
+#include "gpemu_ozaki.hpp"
 
 using namespace gpe;
 
@@ -195,13 +196,24 @@ __global__ void __launch_bounds__(256) k_dist_pack(const double* Aloc, long long
 
 // one 128 x 128 tile src (ld lds) -> dst (ld ldd): 16 workgroups of 8 columns, 16-byte
 // accesses (a hipMemcpy2DAsync of the same tile: 16 us per step on the chain)
-__global__ void __launch_bounds__(256) k_dist_tile(const double* src, long long lds, double* dst, long long ldd) {
+__device__ __forceinline__ void k_dist_tile_body(const double* src, long long lds, double* dst, long long ldd) {
   const int c = blockIdx.x * 8 + (threadIdx.x >> 5), i = (threadIdx.x & 31) * 4;
   const double2* s = reinterpret_cast<const double2*>(src + i + c * lds);
   double2* o = reinterpret_cast<double2*>(dst + i + c * ldd);
   const double2 a = s[0], b = s[1];
   o[0] = a;
   o[1] = b;
+}
+__global__ void __launch_bounds__(256) k_dist_tile(const double* src, long long lds, double* dst, long long ldd) {
+  k_dist_tile_body(src, lds, dst, ldd);
+}
+
+// P = 1: the factors' leaf-inverse tiles (one per step, ld 128) -> X's diagonal tiles, all
+// NB at once after the sweep (per step on the chain, k_dist_tile averaged 20 us: its 16
+// workgroups waited for slots behind the trailing updates)
+__global__ void __launch_bounds__(256) k_dist_leaves(const double* src, double* X, long long ld) {
+  const long long t = blockIdx.y;
+  k_dist_tile_body(src + t * TILE * TILE, (long long)TILE, X + t * TILE + t * TILE * ld, ld);
 }
 
 // gathered segment of rank r (blockIdx.y), tile t -> panel rows of global tile (li0_r + t) P + r
@@ -307,6 +319,7 @@ struct Rank {              // one rank's buffers (one per process over RCCL, P i
   double* dR2 = nullptr;   // n_pad x Pc
   double* r2loc = nullptr; // local rows of R2, 128 columns (zero beyond Pc)
   double* wpart = nullptr; // n_pad x 128: [sqrt(c) alpha, W] (all-reduced)
+  long long slab_doubles = 0;
   double* slab = nullptr;  // slab*128 x n_pad: tile rows of this rank's partial X_r^T X_r
                            // (first, the TRTRI chunks' M^T blocks)
   double* csum = nullptr;  // d+3 contraction sums (all-reduced)
@@ -330,6 +343,8 @@ struct TriChunk {
   int unp1 = 0, nunp1 = 0, unp1_tiles = 0;
   int unp2 = 0, nunp2 = 0, unp2_tiles = 0;
   size_t seg1 = 0, seg2 = 0;                  // all-gather segments (doubles)
+  int s = 0, cw = 0;                          // its level (pairs of s tile columns), chunk width
+  std::vector<OzTriPair> oz;                  // P = 1: the level's pairs on the int8 cores
 };
 
 struct SlabLaunch {        // one slab of a rank's partial of A^-1: GEMM + contraction
@@ -366,9 +381,10 @@ struct gpe_dist {
   double* dr = nullptr;
   double* dinvdelta = nullptr;
   int* dinfo = nullptr;    // abort flag / failed pivot (all-reduced with max over RCCL)
-  int* dq = nullptr;       // 4 x NB counters: the diagonal tiles' pending-update blocks (G_DQUAD);
+  int* dq = nullptr;       // 6 x NB counters: the diagonal tiles' pending-update blocks (G_DQUAD);
                            // P = 1: the diagonal flags and the panel halves' stored updates;
-                           // the diagonal launches' tickets
+                           // the diagonal launches' tickets; P = 1: the fused update launches'
+                           // tickets and their first columns' stored tiles (fuse_next_factor)
   double* cpart = nullptr; // contraction partials (scratch, stream-ordered)
   std::vector<Rank> ranks;   // local ranks (all P in loopback, one otherwise)
 
@@ -387,6 +403,9 @@ struct gpe_dist {
   std::vector<hipEvent_t> ev_near, ev_far;     // per group: the sweep's near / far updates done
   hipEvent_t ev_join = nullptr, ev_end = nullptr;
   bool next_on_chain = true;                   // GPEMU_DIST_NEXT_ON_CHAIN=0: round-5 schedule
+  bool fuse_next = false;                      // P = 1: a group's first factor inside the update
+                                               // before it (GPEMU_DIST_FUSE_NEXT=1; measured no
+                                               // faster)
   int* dli0 = nullptr;       // [NB][P] first local row with global row > k
   int* dcnt = nullptr;       // [NB][P] panel tiles of rank r at step k
   GemmProb* dprobs = nullptr;
@@ -414,6 +433,23 @@ struct gpe_dist {
   std::vector<TriChunk> tri;                   // the recursive TRTRI, level by level
   MoveDesc* dmoves = nullptr;
   std::vector<std::vector<SlabLaunch>> slabs;  // per local rank
+  // the A^-1 partial X_r^T X_r on the int8 cores (gpemu_ozaki.hpp, as the single-GPU LAUUM;
+  // GPEMU_OZAKI=0: fp64 k_gemm slabs).  The buffers serve one rank at a time (the loopback
+  // ranks' partials run one after another on the compute stream)
+  bool oz_on = true;
+  int oz_nmod = OZ_MAXMOD;
+  bool oz_now = false;                         // this data's partial on the int8 cores
+  long long oz_cap_mb = 16384;                 // at most this many MiB of planes per rank
+  int oz_tri_min = 8192;                       // P = 1: TRTRI levels of blocks this tall on the
+                                               // int8 cores (GPEMU_OZAKI_TRI_MIN, as gpemu.hip)
+  int oz_np2 = 0, oz_kp = 0;                   // planes: oz_np2 rows (columns of X_r) x oz_kp k
+  OzConst oz_c{};
+  int8_t* ozp = nullptr;                       // N planes of X_r^T
+  int8_t* ozr = nullptr;                       // N residue images of one slab's 256-tiles
+  long long oz_res_bytes = 0;
+  int* ozx = nullptr;                          // column exponents of X_r
+  unsigned* ozl = nullptr;                     // the slabs' tile lists
+  std::vector<std::pair<long long, int>> oz_lists;   // per slab: offset, length
 };
 
 namespace {
@@ -691,6 +727,83 @@ void list_launch(DLaunch& L, const std::vector<GemmProb>& probs, std::vector<uns
   tiles.insert(tiles.end(), ord.begin(), ord.end());
 }
 
+// P = 1 (round-6 verdict item 4): the first step of each group after the first is started
+// inside the update launch before it (the previous group's update of the group's columns, A),
+// on tile counts, as the single-GPU fused sweep does: that launch's tiles of column ge count
+// themselves when stored, the factor of tile (ge, ge) and the panel tiles' first halves wait
+// for all of them, and the rest of the update runs beside the factorisation.  The group's
+// first step has no pending columns (no G_DQUAD blocks), and its launch drops out of the chain
+// (one dependent launch and its idle gap fewer per group).  List order: column ge's tiles,
+// the factor, the other columns' tiles, the panel halves; every wait points to an earlier
+// list position (checked), and positions are claimed by ticket.
+int fuse_next_factor(gpe_dist* h, std::vector<GemmProb>& probs, std::vector<unsigned>& tiles) {
+  const int NB = h->NB;
+  for (int k = 0; k + 1 < NB; ++k) {
+    const int ge = k + 1;
+    if (group_end(h, k) != ge) continue;
+    DLaunch& ul = h->upd_next[k];
+    DLaunch& dl = h->diag[ge];
+    if (ul.count != 1 || ul.tiles == 0 || ul.list < 0 || dl.count == 0 || dl.list >= 0) continue;
+    int* cnt = h->dq + 5 * NB + ge;
+    DLaunch f;
+    f.kind = 0;
+    f.first = (int)probs.size();
+    GemmProb pc = probs[ul.first], pr = probs[ul.first];
+    pc.post = cnt;
+    std::vector<unsigned> col, rest;
+    for (int i = 0; i < ul.tiles; ++i) {
+      const unsigned code = tiles[(size_t)ul.list + i], tj = code & 0xfffu;
+      (tj == (unsigned)ge ? col : rest).push_back((tj == (unsigned)ge ? 0u : 1u << 24) | (code & 0xffffffu));
+    }
+    if (col.empty()) continue;
+    probs.push_back(pc);
+    probs.push_back(pr);
+    std::vector<unsigned> fac, halves;
+    for (int p = 0; p < dl.count; ++p) {
+      GemmProb q = probs[dl.first + p];
+      if (q.flags & G_DQUAD) return dfail(h, GPE_ERR_STATE, "internal error: a group's first step with pending columns");
+      if (q.flags & (G_DIAG | G_PHALF0)) {
+        q.pre0 = cnt;
+        q.pre0_n = (int)col.size();
+      }
+      const unsigned pi = (unsigned)(2 + p);
+      for (int ti = 0; ti < q.mt; ++ti)
+        ((q.flags & G_DIAG) ? fac : halves).push_back((pi << 24) | ((unsigned)ti << 12));
+      f.cdef = f.cdef || gemm_cdef(q);
+      probs.push_back(q);
+    }
+    f.count = 2 + dl.count;
+    f.cdef = f.cdef || gemm_cdef(pc);
+    std::vector<unsigned> order = col;
+    order.insert(order.end(), fac.begin(), fac.end());
+    order.insert(order.end(), rest.begin(), rest.end());
+    order.insert(order.end(), halves.begin(), halves.end());
+    {   // every wait on an earlier position (counts complete before the waiter's slot)
+      std::map<const int*, size_t> last_post;
+      size_t diag_at = order.size();
+      for (size_t i = 0; i < order.size(); ++i) {
+        const GemmProb& q = probs[f.first + (order[i] >> 24)];
+        if (q.post) last_post[q.post] = i;
+        if (q.cpost) last_post[q.cpost] = i;
+        if (q.flags & G_DIAG) diag_at = i;
+      }
+      for (size_t i = 0; i < order.size(); ++i) {
+        const GemmProb& q = probs[f.first + (order[i] >> 24)];
+        const bool ok = (!q.pre0 || (last_post.count(q.pre0) && last_post[q.pre0] < i)) &&
+                        (!(q.flags & G_PANEL) || diag_at < i);
+        if (!ok) return dfail(h, GPE_ERR_STATE, "internal error: fused launch waits on a later tile");
+      }
+    }
+    f.list = (long long)tiles.size();
+    tiles.insert(tiles.end(), order.begin(), order.end());
+    f.tiles = (int)order.size();
+    f.ticket = h->dq + 4 * NB + k;
+    ul = f;
+    dl = DLaunch();   // (step ge launches nothing for its factor)
+  }
+  return GPE_OK;
+}
+
 // every per-step GEMM descriptor and tile list, for the current n and partition
 int build_schedule(gpe_dist* h) {
   const int NB = h->NB, P = h->P, NT = NB + h->NA;
@@ -739,7 +852,7 @@ int build_schedule(gpe_dist* h) {
         p.pre0 = h->dq + k;
         p.pre0_n = DQ_N;
       }
-      p.X = R->dinv + (long long)Kp * TILE;
+      p.X = gath ? R->dinv + (long long)Kp * TILE : R->dinv + (long long)k * TILE * TILE;
       p.ldx = TILE;
       p.logdet = R->logdet + k;
       p.diag_col0 = k * TILE;
@@ -770,7 +883,7 @@ int build_schedule(gpe_dist* h) {
                            R.A + (long long)a * TILE + (long long)k * TILE * R.ld, R.ld, c, 1, Kp,
                            G_PANEL | G_PHALF0, Kp ? -1.0 : 1.0, 1.0);
         q.cpost = h->dq + 2 * NB + k;
-        q.X = R.dinv + (long long)Kp * TILE;
+        q.X = R.dinv + (long long)k * TILE * TILE;
         q.ldx = TILE;
         q.flag = h->dq + NB + k;
         q.diag_col0 = -TILE;   // (no GEMM_TRACE slot)
@@ -877,6 +990,7 @@ int build_schedule(gpe_dist* h) {
       (part == 0 ? h->upd_next : (part == 1 ? h->upd_near : h->upd_far))[k] = ul;
     }
   }
+  if (!gather_panels(h) && h->next_on_chain && h->fuse_next) DCHK(fuse_next_factor(h, probs, tiles));
   if ((int)probs.size() > DIST_DESC_MAX) return dfail(h, GPE_ERR_UNSUPPORTED, "distributed schedule too large");
   DCHK(dalloc(h, &h->dprobs, probs.size()));
   DCHK_HIP(h, hipMemcpy(h->dprobs, probs.data(), probs.size() * sizeof(GemmProb), hipMemcpyHostToDevice));
@@ -924,6 +1038,99 @@ int launch(gpe_dist* h, const DLaunch& L, bool grad = false) {
 // first local tile row of rank r whose global row is >= a
 int lstart_of(int a, int P, int r) { return a <= r ? 0 : (a - r + P - 1) / P; }
 
+// ---- the A^-1 partial on the int8 cores.  Rank r's partial X_r^T X_r is the product of
+// op = X_r^T with itself: op's rows are the columns of X_r (np2 of them, 256-row tiles),
+// its k the rank's rows (oz_kp = rank 0's, the most).  Column c of X_r is zero on the local
+// rows whose global tile row is below c's, so the tiles of op-row tile ti start at local
+// row 128 floor(2 ti / P) (OzGemm kbeg 3).  One launch pair (k_oz_gemm, k_oz_crt) per slab
+// of tile rows [a0, a1) writes the slab's lower tiles, in place of the fp64 slab launch.
+int oz_prepare(gpe_dist* h) {
+  const int NB = h->NB, P = h->P, N = h->oz_nmod;
+  const int np2 = (int)((h->n_pad + OZ_T - 1) / OZ_T * OZ_T), Kp = ((NB - 1) / P + 1) * TILE;
+  h->oz_np2 = np2;
+  h->oz_kp = Kp;
+  h->oz_c = oz_consts(N, Kp);
+  std::vector<unsigned> all;
+  h->oz_lists.clear();
+  long long maxt = 0;
+  for (const SlabLaunch& sl : h->slabs[0]) {   // (the same slab bounds on every rank)
+    const int ti0 = sl.a0 / 2, ti1 = (sl.a1 + 1) / 2;
+    const std::vector<unsigned> l = oz_list(ti1 - ti0, ti1, true, [&](int ti, int) {
+      return (double)std::max(0, Kp - 128 * ((2 * ti) / P));
+    }, ti0);
+    h->oz_lists.push_back({(long long)all.size(), (int)l.size()});
+    all.insert(all.end(), l.begin(), l.end());
+    maxt = std::max(maxt, (long long)ti1 * (ti1 + 1) / 2 - (long long)ti0 * (ti0 + 1) / 2);
+  }
+  h->oz_res_bytes = maxt * OZ_T * OZ_T;
+  // P = 1: the TRTRI levels whose blocks have at least oz_tri_min rows, each in one chunk,
+  // as the single-GPU path's int8 pairs (oz_tri_pair_launches: T in the slab, in place of
+  // the M^T blocks); the partial's buffers are the larger
+  const size_t slab_doubles = (size_t)h->ranks[0].slab_doubles;
+  for (TriChunk& tc : h->tri) {
+    tc.oz.clear();
+    const int a = tc.s / 2;
+    if (P != 1 || tc.cw != a || (long long)a * TILE < h->oz_tri_min) continue;
+    std::vector<unsigned> lists = all;
+    std::vector<OzTriPair> prs;
+    bool fits = true;
+    for (int t0 = 0; t0 + a < NB; t0 += tc.s) {
+      const OzTriPair q = oz_tri_pair_plan(t0, t0 + a, std::min(t0 + tc.s, NB), N, lists);
+      fits = fits && q.planes_bytes(N) <= (size_t)N * np2 * Kp && q.resid_bytes(N) <= (size_t)N * h->oz_res_bytes &&
+             (size_t)q.Pa * q.Pb <= slab_doubles && q.Pa + q.Pb <= np2;
+      prs.push_back(q);
+    }
+    if (!fits) continue;
+    all = lists;
+    tc.oz = prs;
+  }
+  DCHK(dalloc(h, &h->ozp, (size_t)N * np2 * Kp, &h->shared_bytes));
+  DCHK(dalloc(h, &h->ozr, (size_t)N * h->oz_res_bytes, &h->shared_bytes));
+  DCHK(dalloc(h, &h->ozx, (size_t)np2, &h->shared_bytes));
+  DCHK(dalloc(h, &h->ozl, all.size(), &h->shared_bytes));
+  DCHK_HIP(h, hipMemcpy(h->ozl, all.data(), all.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+  return GPE_OK;
+}
+
+// rank R's column exponents and planes of X_r^T (rows past n_pad and k past its rows: zero)
+int oz_split_rank(gpe_dist* h, const Rank& R) {
+  const int np2 = h->oz_np2, Kp = h->oz_kp, Kv = R.nlx * TILE;
+  const OzConst& k = h->oz_c;
+  hipLaunchKernelGGL(k_oz_rowexp<false>, dim3(np2 / 4), dim3(256), 0, h->stream, R.X, R.ld, (int)h->n_pad, np2, Kv,
+                     0, k.beta, h->ozx);
+  hipLaunchKernelGGL(k_oz_split_rect<false>, dim3(np2, (Kp + 2047) / 2048), dim3(256), 0, h->stream, R.X, R.ld,
+                     (int)h->n_pad, Kv, 0, h->ozx, h->ozp, (long long)np2 * Kp, (long long)Kp, Kp, k);
+  DCHK_HIP(h, hipGetLastError());
+  return GPE_OK;
+}
+
+// slab si of rank R's partial: tile rows [a0, a1) (a0 even), their lower tiles into R.slab
+int oz_slab(gpe_dist* h, const Rank& R, const SlabLaunch& sl, size_t si) {
+  const int np2 = h->oz_np2, Kp = h->oz_kp;
+  const int ti0 = sl.a0 / 2, ti1 = (sl.a1 + 1) / 2;
+  const OzConst& k = h->oz_c;
+  OzGemm g;
+  g.a = g.b = OzOpnd{h->ozp, (long long)np2 * Kp, (long long)Kp, 0};
+  g.list = h->ozl + h->oz_lists[si].first;
+  g.list_len = h->oz_lists[si].second;
+  g.K = Kp;
+  g.kbeg = 3;
+  g.kdiv = h->P;
+  g.kend = 0;
+  g.tri = 1;
+  g.ntj = 0;
+  g.res = h->ozr;
+  g.res_bytes = h->oz_res_bytes;
+  g.ti0 = ti0;
+  hipLaunchKernelGGL(k_oz_gemm, dim3(k.nmod * g.list_len), dim3(256), OZ_LDS, h->stream, g, k);
+  const int rows = sl.a1 * TILE;
+  OzCrt r{h->ozr, h->oz_res_bytes, 1, 0, h->ozx, h->ozx, R.slab, (long long)h->slab_rows * TILE, rows, rows, 1, 1.0, ti0};
+  const long long nt = (long long)ti1 * (ti1 + 1) / 2 - (long long)ti0 * (ti0 + 1) / 2;
+  hipLaunchKernelGGL(k_oz_crt, dim3((unsigned)(nt * 16)), dim3(256), 0, h->stream, r, k);
+  DCHK_HIP(h, hipGetLastError());
+  return GPE_OK;
+}
+
 // gradient buffers and GEMM descriptors (TRTRI steps, W partial, A^-1 slabs)
 int ensure_grad(gpe_dist* h) {
   if (h->grad_ready) return GPE_OK;
@@ -939,6 +1146,16 @@ int ensure_grad(gpe_dist* h) {
   if (whole <= 4 * (long long)SLAB_DOUBLES) slab_doubles = std::max(slab_doubles, whole / P);
   if (const char* e = std::getenv("GPEMU_DIST_SLAB_MB")) slab_doubles = std::max(1ll, std::atoll(e)) << 17;
   h->slab_rows = (int)std::max<long long>(1, std::min<long long>(NB, slab_doubles / (TILE * np)));
+  const int tri_rows = h->slab_rows;   // the TRTRI's gathered blocks fit tri_rows tile rows
+  // the int8 partial (oz_slab): products of sums over a rank's rows, oz_kp <= 2^17 keeps the
+  // int32 accumulators exact; its 256-row tiles need every slab but the last to start at an
+  // even tile row.  Its planes take 2 x the bytes of the rank's rows of L^-1: on only while
+  // they fit oz_cap_mb (16 GiB; GPEMU_DIST_OZAKI_MB), so a rank of C4 takes them from P = 8
+  const int nlx0 = (NB - 1) / P + 1;
+  const double oz_planes = (double)h->oz_nmod * ((np + OZ_T - 1) / OZ_T * OZ_T) * nlx0 * TILE;
+  h->oz_now = h->oz_on && np >= 2048 && (long long)nlx0 * TILE < (1 << 17) &&
+              oz_planes <= (double)h->oz_cap_mb * (1 << 20);
+  if (h->oz_now && h->slab_rows < NB && (h->slab_rows & 1)) h->slab_rows = std::max(2, h->slab_rows - 1);
   const long long lds = (long long)h->slab_rows * TILE;
   for (Rank& R : h->ranks) {
     R.nlx = R.rank <= NB - 1 ? (NB - 1 - R.rank) / P + 1 : 0;
@@ -948,7 +1165,8 @@ int ensure_grad(gpe_dist* h) {
     DCHK(dalloc(h, &R.r2loc, (size_t)R.ld * h->NA * TILE, &R.bytes));
     DCHK_HIP(h, hipMemset(R.r2loc, 0, (size_t)R.ld * h->NA * TILE * sizeof(double)));
     DCHK(dalloc(h, &R.wpart, (size_t)np * h->NA * TILE, &R.bytes));
-    DCHK(dalloc(h, &R.slab, (size_t)lds * np, &R.bytes));
+    R.slab_doubles = (long long)std::max(h->slab_rows, tri_rows) * TILE * np;
+    DCHK(dalloc(h, &R.slab, (size_t)R.slab_doubles, &R.bytes));
     DCHK(dalloc(h, &R.csum, (size_t)d + 3, &R.bytes));
   }
   DCHK(dalloc(h, &h->dT2, (size_t)Pc * Pc, &h->shared_bytes));
@@ -967,7 +1185,7 @@ int ensure_grad(gpe_dist* h) {
   std::vector<GemmProb> probs;
   std::vector<MoveDesc> moves;
   h->tri.clear();
-  const long long cap = lds * np, T2 = (long long)TILE * TILE;
+  const long long cap = (long long)tri_rows * TILE * np, T2 = (long long)TILE * TILE;
   struct Pair { int t0, h, t1; };
   std::vector<std::pair<int, int>> lev;   // per level: {s, chunk width}
   long long g1_need = 0, rv_need = 0;
@@ -1012,6 +1230,8 @@ int ensure_grad(gpe_dist* h) {
     for (int j0 = 0; j0 < a; j0 += cc) {
       const int cw = std::min(cc, a - j0), rows1 = a - j0, mx1 = (rows1 + P - 1) / P;
       TriChunk tc;
+      tc.s = s;
+      tc.cw = cw;
       // per pair: offsets in the all-gather segments (o1, o2) and the gathered blocks (og1, og2)
       std::vector<long long> o1, og1, o2, og2;
       long long s1 = 0, gg1 = 0, s2 = 0, gg2 = 0;
@@ -1174,6 +1394,7 @@ int ensure_grad(gpe_dist* h) {
   for (auto& v : h->slabs)
     for (SlabLaunch& sl : v) list_launch(sl.gemm, probs, gt);
   if ((int)probs.size() > DIST_DESC_MAX) return dfail(h, GPE_ERR_UNSUPPORTED, "distributed gradient schedule too large");
+  if (h->oz_now) DCHK(oz_prepare(h));
   DCHK(dalloc(h, &h->gtiles, std::max<size_t>(gt.size(), 1), &h->shared_bytes));
   if (!gt.empty())
     DCHK_HIP(h, hipMemcpy(h->gtiles, gt.data(), gt.size() * sizeof(unsigned), hipMemcpyHostToDevice));
@@ -1194,6 +1415,21 @@ int move_launch(gpe_dist* h, int first, int count, int tiles) {
 int trtri_all(gpe_dist* h) {
   h->cs = h->stream;
   for (const TriChunk& tc : h->tri) {
+    if (!tc.oz.empty()) {   // P = 1, int8 pairs (oz_prepare)
+      Rank& R = h->ranks[0];
+      auto tile = [&](double* M, int i, int j) { return M + (long long)i * TILE + (long long)j * TILE * R.ld; };
+      const OzConst& k = h->oz_c;
+      for (const OzTriPair& q : tc.oz)
+        oz_tri_pair_launches(h->stream, k, q, h->ozl, tile(R.A, q.h, q.t0), tile(R.X, q.t0, q.t0), tile(R.X, q.h, q.h),
+                             tile(R.X, q.h, q.t0), R.ld, R.slab, h->ozp, h->ozr, h->ozx, false,
+                             [&](const OzGemm& g, const OzCrt& r, int nti, double, double) {
+                               hipLaunchKernelGGL(k_oz_gemm, dim3(k.nmod * g.list_len), dim3(256), OZ_LDS, h->stream, g, k);
+                               hipLaunchKernelGGL(k_oz_crt, dim3((unsigned)(nti * g.ntj * 16)), dim3(256), 0, h->stream,
+                                                  r, k);
+                             });
+      DCHK_HIP(h, hipGetLastError());
+      continue;
+    }
     if (h->P > 1) {
       DCHK(move_launch(h, tc.pack0, tc.npack, tc.pack_tiles));
       DCHK(coll_allgather(h, &Rank::trecv, tc.seg1));
@@ -1246,7 +1482,7 @@ int step(gpe_dist* h, int k) {
   DCHK(launch(h, h->diag[k]));
   DCHK(launch(h, h->mrow[k]));
   if (gather_panels(h)) DCHK(coll_bcast(h, &Rank::dinv, 0, (size_t)TILE * (Kp + TILE), owner));
-  if (h->grad_now) {
+  if (h->grad_now && gather_panels(h)) {
     if (Rank* O = rank_slot(h, owner)) {   // the diagonal tile of X = L^-1 (Dinv)
       hipLaunchKernelGGL(k_dist_tile, dim3(TILE / 8), dim3(256), 0, h->cs, O->dinv + Kp * TILE, (long long)TILE,
                          O->X + (long long)(k / P) * TILE + (long long)k * TILE * O->ld, (long long)O->ld);
@@ -1413,6 +1649,11 @@ gpe_dist* gpe_dist_create(int32_t device, int32_t nranks, int32_t rank, const ui
   h->rank = unique_id ? rank : 0;
   h->loop = unique_id == nullptr;
   if (const char* e = std::getenv("GPEMU_DIST_NEXT_ON_CHAIN")) h->next_on_chain = std::atoi(e) != 0;
+  if (const char* e = std::getenv("GPEMU_DIST_FUSE_NEXT")) h->fuse_next = std::atoi(e) != 0;
+  if (const char* e = std::getenv("GPEMU_OZAKI")) h->oz_on = std::atoi(e) != 0;
+  if (const char* e = std::getenv("GPEMU_DIST_OZAKI_MB")) h->oz_cap_mb = std::max(0ll, std::atoll(e));
+  if (const char* e = std::getenv("GPEMU_OZAKI_TRI_MIN")) h->oz_tri_min = std::max(512, std::atoi(e));
+  if (const char* e = std::getenv("GPEMU_OZAKI_MODULI")) h->oz_nmod = std::max(8, std::min(OZ_MAXMOD, std::atoi(e)));
   if (const char* e = std::getenv("GPEMU_DIST_W")) {   // "4:80,2:40": {width, min remaining}
     h->groups.clear();
     std::string spec(e);
@@ -1468,6 +1709,10 @@ void gpe_dist_destroy(gpe_dist* h) {
   dfree(&h->dmoves);
   dfree(&h->wsplit);
   dfree(&h->wcnt);
+  dfree(&h->ozp);
+  dfree(&h->ozr);
+  dfree(&h->ozx);
+  dfree(&h->ozl);
   if (h->hpin) (void)hipHostFree(h->hpin);
   for (hipEvent_t e : h->cev) (void)hipEventDestroy(e);
   if (h->e0) (void)hipEventDestroy(h->e0);
@@ -1514,6 +1759,10 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
   dfree(&h->dmoves);
   dfree(&h->wsplit);
   dfree(&h->wcnt);
+  dfree(&h->ozp);
+  dfree(&h->ozr);
+  dfree(&h->ozx);
+  dfree(&h->ozl);
   DCHK(pinned(h, (size_t)np * std::max(d, Pc) + 16));
   // X (row-major, zero padded)
   DCHK(dalloc(h, &h->dX, (size_t)np * d, &h->shared_bytes));
@@ -1540,7 +1789,7 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
   DCHK(dalloc(h, &h->dinvdelta, (size_t)d, &h->shared_bytes));
   // local ranks and their sweep buffers
   build_groups(h);
-  DCHK(dalloc(h, &h->dq, 4 * (size_t)h->NB, &h->shared_bytes));
+  DCHK(dalloc(h, &h->dq, 6 * (size_t)h->NB, &h->shared_bytes));
   const int NT = h->NB + h->NA;
   h->panel_sz = (size_t)NT * TILE * TILE * h->wmax;
   // the group all-gather's segment: W column blocks of the most tile rows below the group
@@ -1562,7 +1811,9 @@ int gpe_dist_set_data(gpe_dist* h, int64_t n, int32_t d, int32_t q, const double
     Rank& B = h->ranks.back();
     DCHK(dalloc(h, &B.A, (size_t)B.ld * (size_t)NT * TILE, &B.bytes));
     DCHK(dalloc(h, &B.logdet, (size_t)h->NB + 1, &B.bytes));
-    DCHK(dalloc(h, &B.dinv, (size_t)TILE * TILE * h->wmax, &B.bytes));
+    // P = 1: one leaf-inverse tile per step (the factors write them there; k_dist_leaves
+    // moves all of them into X after the sweep, off the chain)
+    DCHK(dalloc(h, &B.dinv, (size_t)TILE * TILE * (gather_panels(h) ? h->wmax : h->NB), &B.bytes));
     if (gather_panels(h)) {
       DCHK(dalloc(h, &B.panel, 2 * h->panel_sz, &B.bytes));
       DCHK(dalloc(h, &B.recv, (size_t)h->P * h->recv_tiles * TILE * TILE, &B.bytes));
@@ -1623,13 +1874,14 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
       DCHK_HIP(h, hipMemsetAsync(R.X, 0, (size_t)R.ld * NB * TILE * sizeof(double), h->stream));
   }
   DCHK(kbuild(h, kernel, nu, s2, rscale));
-  DCHK_HIP(h, hipMemsetAsync(h->dq, 0, 4 * (size_t)NB * sizeof(int), h->stream));
+  DCHK_HIP(h, hipMemsetAsync(h->dq, 0, 6 * (size_t)NB * sizeof(int), h->stream));
   DCHK(group_sweep(h));
   // P = 1: the sweep's factors stored L and the leaf inverses only (flag mode): the
   // TRTRI's leaves X(t, t) are assembled here for every diagonal tile at once
   if (h->grad_now && !gather_panels(h))
     for (Rank& R : h->ranks) {
       if (R.nlx == 0) continue;
+      hipLaunchKernelGGL(k_dist_leaves, dim3(TILE / 8, NB), dim3(256), 0, h->stream, R.dinv, R.X, R.ld);
       hipLaunchKernelGGL(k_xasm, dim3(NB), dim3(256), DB_LDS_DOUBLES * sizeof(double), h->stream, R.A, R.X, R.ld);
       DCHK_HIP(h, hipGetLastError());
     }
@@ -1741,8 +1993,11 @@ int gpe_dist_objective(gpe_dist* h, int32_t variant, int32_t kernel, const doubl
       DCHK_HIP(h, hipMemsetAsync(R.csum, 0, (size_t)(d + 3) * sizeof(double), h->stream));
       if (R.nlx == 0) continue;
       const int q1 = R.rank == 0 ? Pc : 0;   // the -W W^T term once
-      for (const SlabLaunch& sl : h->slabs[s]) {
-        DCHK(launch(h, sl.gemm, true));
+      if (h->oz_now) DCHK(oz_split_rank(h, R));
+      for (size_t si = 0; si < h->slabs[s].size(); ++si) {
+        const SlabLaunch& sl = h->slabs[s][si];
+        if (h->oz_now) DCHK(oz_slab(h, R, sl, si));
+        else DCHK(launch(h, sl.gemm, true));
         const int b0 = sl.a0 * (sl.a0 + 1) / 2, b1 = sl.a1 * (sl.a1 + 1) / 2;
         contract_launch(h, R.slab, lds, (long long)sl.a0 * TILE, b0, b1 - b0, R.wpart, q1, rdiag);
         DCHK_HIP(h, hipGetLastError());

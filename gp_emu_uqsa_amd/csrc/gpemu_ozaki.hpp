@@ -142,8 +142,10 @@ __device__ __forceinline__ const int8_t* oz_tile_rows(const OzOpnd& o, int t, in
 // A product C'_l = A'_l B'_l^T over the 256 x 256 tiles of a list (entries ti << 16 | tj, the
 // list's length a multiple of 8 so position % 8 is the XCD under round-robin dispatch,
 // 0xffffffff padding the bins), blockIdx.x = l * list_len + position.  K range of tile
-// (ti, tj): from 0, 256 ti or 256 tj (kbeg 0 / 1 / 2) to K or 256 (ti + 1) (kend 0 / 1):
-// the triangular operands' nonzero k.
+// (ti, tj): from 0, 256 ti, 256 tj or 128 floor(2 ti / kdiv) (kbeg 0 / 1 / 2 / 3) to K or
+// 256 (ti + 1) (kend 0 / 1): the triangular operands' nonzero k (kbeg 3: the rows of a
+// lower-triangular X dealt cyclically by 128-row tiles over kdiv ranks, seen from one rank).
+// Tile rows from ti0 (the residues of tile (ti, tj) at its index less that of (ti0, 0)).
 struct OzGemm {
   OzOpnd a, b;
   const unsigned* list;
@@ -152,6 +154,8 @@ struct OzGemm {
   int tri, ntj;    // residue tile of (ti, tj): ti (ti + 1) / 2 + tj (tri) or ti ntj + tj
   int8_t* res;
   long long res_bytes;
+  int kdiv = 1;
+  int ti0 = 0;
 };
 __device__ __forceinline__ long long oz_res_tile(int tri, int ntj, int ti, int tj) {
   return tri ? (long long)ti * (ti + 1) / 2 + tj : (long long)ti * ntj + tj;
@@ -170,7 +174,7 @@ static __global__ void __launch_bounds__(256, 1) k_oz_gemm(OzGemm g, OzConst cst
   const unsigned ent = g.list[(int)blockIdx.x - l * g.list_len];
   if (ent == 0xffffffffu) return;
   const int ti = (int)(ent >> 16), tj = (int)(ent & 0xffffu);
-  const int kb = g.kbeg == 1 ? OZ_T * ti : (g.kbeg == 2 ? OZ_T * tj : 0);
+  const int kb = g.kbeg == 1 ? OZ_T * ti : (g.kbeg == 2 ? OZ_T * tj : (g.kbeg == 3 ? 128 * ((2 * ti) / g.kdiv) : 0));
   const int ke = g.kend == 1 ? min(g.K, OZ_T * (ti + 1)) : g.K;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -264,7 +268,8 @@ static __global__ void __launch_bounds__(256, 1) k_oz_gemm(OzGemm g, OzConst cst
   // m = 256: the low byte itself
   const int m = cst.m[l], c16 = cst.c16[l];
   const float inv = cst.inv[l];
-  int8_t* out = g.res + (long long)l * g.res_bytes + oz_res_tile(g.tri, g.ntj, ti, tj) * (OZ_T * OZ_T) +
+  int8_t* out = g.res + (long long)l * g.res_bytes +
+                (oz_res_tile(g.tri, g.ntj, ti, tj) - oz_res_tile(g.tri, g.ntj, g.ti0, 0)) * (OZ_T * OZ_T) +
                 ((long long)(wave * 16) * 64 + lane) * 16;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -289,7 +294,8 @@ static __global__ void __launch_bounds__(256, 1) k_oz_gemm(OzGemm g, OzConst cst
 // fp64 entries from the residues: C(r, c) = alpha v M 2^-(exr[r] + exc[c]), v = C'/M the
 // centred fraction of sum_l c_l y_l / m_l.  Thread u of tile t (16 workgroups per tile) =
 // wave u / 1024, block (u / 64) % 16, lane u % 64 of k_oz_gemm's order, 16 entries; rows
-// < rows and columns < cols only, and with lower128 only the lower 128-tiles.
+// < rows and columns < cols only, and with lower128 only the lower 128-tiles.  Tile rows
+// from ti0 (as OzGemm); row gm of the product goes to row gm - 256 ti0 of C.
 struct OzCrt {
   const int8_t* res;
   long long res_bytes;
@@ -300,18 +306,20 @@ struct OzCrt {
   long long ldc;
   int rows, cols, lower128;
   double alpha;
+  int ti0 = 0;
 };
 static __global__ void __launch_bounds__(256) k_oz_crt(OzCrt g, OzConst cst) {
   const int t = (int)blockIdx.x >> 4;
   const int u = ((int)blockIdx.x & 15) * 256 + (int)threadIdx.x;
   int ti, tj;
   if (g.tri) {
-    ti = 0;
-    while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-    tj = t - ti * (ti + 1) / 2;
+    const int ta = t + g.ti0 * (g.ti0 + 1) / 2;
+    ti = g.ti0;
+    while ((ti + 1) * (ti + 2) / 2 <= ta) ++ti;
+    tj = ta - ti * (ti + 1) / 2;
   } else {
-    ti = t / g.ntj;
-    tj = t - ti * g.ntj;
+    ti = g.ti0 + t / g.ntj;
+    tj = t % g.ntj;
   }
   const int wave = u >> 10, blk = (u >> 6) & 15, lane = u & 63;
   const int i = blk >> 2, j = blk & 3;
@@ -339,7 +347,7 @@ static __global__ void __launch_bounds__(256) k_oz_crt(OzCrt g, OzConst cst) {
     const int gn = gn0 + (r & 3) + 8 * (r >> 2);
     if (gn >= g.cols || (g.lower128 && (gm >> 7) < (gn >> 7))) continue;
     const double v = (shi[r] - rint(shi[r])) + slo[r];   // C' / M, centred
-    g.C[gm + (long long)gn * g.ldc] = v * ldexp(sc, -(em + g.exc[gn]));
+    g.C[gm - OZ_T * g.ti0 + (long long)gn * g.ldc] = v * ldexp(sc, -(em + g.exc[gn]));
   }
 }
 
@@ -446,6 +454,194 @@ static __global__ void __launch_bounds__(256) k_oz_split_rect(const double* __re
       *reinterpret_cast<uint2*>(planes + (long long)l * plane_bytes + (long long)r * ldp + k0 + (long long)0) =
           make_uint2(w[0], w[1]);
     }
+  }
+}
+
+// ---- host side (gpemu.hip, gpemu_dist.hip)
+
+// moduli and reconstruction constants for operand sums of length up to np2
+inline OzConst oz_consts(int nmod, int np2) {
+  static const int mods[OZ_MAXMOD] = {256, 253, 251, 247, 241, 239, 233, 229, 227, 223, 217, 211, 199, 197, 193, 191};
+  OzConst k{};
+  k.nmod = nmod;
+  double log2M = 0.0, Md = 1.0;
+  for (int l = 0; l < nmod; ++l) {
+    log2M += std::log2((double)mods[l]);
+    Md *= (double)mods[l];
+  }
+  k.Md = Md;
+  // |C'| <= np2 2^(2 beta) < M / 2
+  k.beta = std::min(53, (int)std::floor((log2M - 1.0 - std::log2((double)np2) - 1e-9) / 2.0));
+  for (int l = 0; l < nmod; ++l) {
+    const int m = mods[l];
+    k.m[l] = m;
+    k.c16[l] = 65536 % m;
+    k.inv[l] = 1.0f / (float)m;
+    long long Mm = 1;   // (M / m) mod m
+    for (int j = 0; j < nmod; ++j)
+      if (j != l) Mm = (Mm * (mods[j] % m)) % m;
+    int y = 1;          // its inverse mod m
+    while ((Mm * y) % m != 1) ++y;
+    // y / m = rhi + rlo, rhi on the 2^-41 grid (exact products and sums in k_oz_crt)
+    const long long num = (long long)y << 41;
+    const long long Q = num / m, R = num - Q * m;
+    k.rhi[l] = std::ldexp((double)Q, -41);
+    k.rlo[l] = std::ldexp((double)R / (double)m, -41);
+  }
+  return k;
+}
+
+// A product's tile list: blocks of OZ_BR tile rows x OZ_BC tile columns (clipped to the lower
+// triangle when lower), heaviest first, greedily binned by work into 8 XCD bins, interleaved
+// position by position (bin = position % 8, the XCD under round-robin dispatch), bins padded
+// to one length with 0xffffffff; tile rows ti0 .. ti0 + nti - 1.  An XCD's 32 CUs then run one
+// block at a time: its tiles share 4 A panels and 8 B panels (a whole tile row on one XCD
+// shared one A panel among 32 different B panels: L2 hit rate ~0.5)
+template <class W>
+std::vector<unsigned> oz_list(int nti, int ntj, bool lower, W work, int ti0 = 0) {
+  constexpr int OZ_BR = 4, OZ_BC = 8;
+  struct Blk { double w; std::vector<unsigned> t; };
+  std::vector<Blk> blks;
+  for (int r0 = ti0; r0 < ti0 + nti; r0 += OZ_BR)
+    for (int c0 = 0; c0 < ntj && (!lower || c0 <= r0 + OZ_BR - 1); c0 += OZ_BC) {
+      Blk b{0.0, {}};
+      for (int ti = r0; ti < std::min(ti0 + nti, r0 + OZ_BR); ++ti)
+        for (int tj = c0; tj < std::min(lower ? ti + 1 : ntj, c0 + OZ_BC); ++tj) {
+          b.t.push_back(((unsigned)ti << 16) | (unsigned)tj);
+          b.w += work(ti, tj);
+        }
+      if (!b.t.empty()) blks.push_back(std::move(b));
+    }
+  std::stable_sort(blks.begin(), blks.end(), [](const Blk& x, const Blk& y) { return x.w / x.t.size() > y.w / y.t.size(); });
+  std::vector<std::vector<unsigned>> bins(8);
+  std::vector<double> load(8, 0.0);
+  for (const Blk& b : blks) {
+    const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    load[x] += b.w;
+    bins[x].insert(bins[x].end(), b.t.begin(), b.t.end());
+  }
+  size_t longest = 0;
+  for (auto& b : bins) longest = std::max(longest, b.size());
+  std::vector<unsigned> list(8 * longest, 0xffffffffu);
+  for (int x = 0; x < 8; ++x)
+    for (size_t q = 0; q < bins[x].size(); ++q) list[8 * q + x] = bins[x][q];
+  return list;
+}
+
+// ---- one block pair (t0, h, t1) of a TRTRI level (tile units of 128) on the int8 cores:
+// the blocks X11 = X(t0:h, t0:h) and X22 = X(h:t1, h:t1) already inverted, L21 = L(h:t1,
+// t0:h):
+//   T   = L21 X11      (rows of L21 against columns of X11, k >= the column: kbeg = 256 tj)
+//   X21 = -X22 T       (rows of X22, k <= the row: kend = 256 (ti + 1), against columns of T)
+// T goes to a scratch block (column-major, ld Pb, so its columns are the second product's
+// rows).  Plan (host): the rows of each block (Ra, Rb), padded to 256 (Pa, Pb), the two tile
+// lists' offsets in a list array, and the products' int8 operations (every modulus).
+struct OzTriPair {
+  int t0, h, t1, Ra, Rb, Pa, Pb;
+  long long la_off, lb_off;
+  int la_len, lb_len;
+  double ops_a, ops_b;
+  size_t planes_bytes(int N) const { return (size_t)N * Pa * (Pa + Pb); }
+  size_t resid_bytes(int N) const { return (size_t)N * Pa * Pb; }
+};
+inline OzTriPair oz_tri_pair_plan(int t0, int h, int t1, int N, std::vector<unsigned>& lists) {
+  OzTriPair q;
+  q.t0 = t0; q.h = h; q.t1 = t1;
+  q.Ra = (h - t0) * TILE;
+  q.Rb = (t1 - h) * TILE;
+  q.Pa = (q.Ra + OZ_T - 1) / OZ_T * OZ_T;
+  q.Pb = (q.Rb + OZ_T - 1) / OZ_T * OZ_T;
+  const int nti = q.Pb / OZ_T, ntj = q.Pa / OZ_T;
+  const std::vector<unsigned> la = oz_list(nti, ntj, false, [&](int, int tj) { return (double)(q.Pa - OZ_T * tj); });
+  const std::vector<unsigned> lb = oz_list(nti, ntj, false, [&](int ti, int) { return (double)(OZ_T * (ti + 1)); });
+  q.ops_a = q.ops_b = 0.0;
+  for (int tj = 0; tj < ntj; ++tj) q.ops_a += 2.0 * OZ_T * OZ_T * nti * (double)(q.Pa - OZ_T * tj) * N;
+  for (int ti = 0; ti < nti; ++ti) q.ops_b += 2.0 * OZ_T * OZ_T * ntj * (double)(OZ_T * (ti + 1)) * N;
+  q.la_off = (long long)lists.size();
+  q.la_len = (int)la.size();
+  lists.insert(lists.end(), la.begin(), la.end());
+  q.lb_off = (long long)lists.size();
+  q.lb_len = (int)lb.size();
+  lists.insert(lists.end(), lb.begin(), lb.end());
+  return q;
+}
+
+// the first product's L21 side: row exponents (into ex[0, Pb)) and planes of L21's rows
+inline void oz_l21_launch(hipStream_t st, const OzConst& k, const OzTriPair& q, const double* L21, long long ld,
+                          int8_t* planes, int* ex) {
+  const long long pA = (long long)q.Pb * q.Pa;
+  (void)hipMemsetAsync(ex, 0, q.Pb * sizeof(int), st);
+  hipLaunchKernelGGL(k_oz_rowexp<true>, dim3(q.Pb / 64, (q.Ra + 255) / 256), dim3(256), 0, st, L21, ld, q.Rb, q.Pb,
+                     q.Ra, 0, k.beta, ex);
+  hipLaunchKernelGGL(k_oz_il_to_ex, dim3((q.Pb + 255) / 256), dim3(256), 0, st, ex, q.Pb, k.beta);
+  hipLaunchKernelGGL(k_oz_split_rect<true>, dim3(q.Pb / 64, q.Pa / 64), dim3(256), 0, st, L21, ld, q.Rb, q.Ra, 0,
+                     ex, planes, pA, (long long)q.Pa, q.Pa, k);
+}
+
+// both products of the pair on stream st (X blocks and L21 with leading dimension ld; T:
+// Pb x Pa doubles; planes: q.planes_bytes(N); res: q.resid_bytes(N); ex: Pa + Pb ints;
+// lists: the list array of oz_tri_pair_plan, on the device).  l21_done: oz_l21_launch already
+// ran (ordered before st's work by the caller).  gc(g, r, nti, ops, flops64) launches one
+// k_oz_gemm + k_oz_crt pair.
+template <class GC>
+void oz_tri_pair_launches(hipStream_t st, const OzConst& k, const OzTriPair& q, const unsigned* lists, const double* L21,
+                          const double* X11, const double* X22, double* X21, long long ld, double* T, int8_t* planes,
+                          int8_t* res, int* ex, bool l21_done, GC gc) {
+  int* exA = ex;
+  int* exB = ex + q.Pb;
+  const int nti = q.Pb / OZ_T, ntj = q.Pa / OZ_T;
+  const long long rb = (long long)nti * ntj * OZ_T * OZ_T;
+  {   // T = L21 X11
+    const long long pA = (long long)q.Pb * q.Pa, pB = (long long)q.Pa * q.Pa;
+    int8_t* PA = planes;
+    int8_t* PB = planes + (size_t)k.nmod * pA;
+    if (!l21_done) oz_l21_launch(st, k, q, L21, ld, PA, exA);
+    hipLaunchKernelGGL(k_oz_rowexp<false>, dim3(q.Pa / 4), dim3(256), 0, st, X11, ld, q.Ra, q.Pa, q.Ra, 1, k.beta, exB);
+    hipLaunchKernelGGL(k_oz_split_rect<false>, dim3(q.Pa, (q.Pa + 2047) / 2048), dim3(256), 0, st, X11, ld, q.Ra, q.Ra,
+                       1, exB, PB, pB, (long long)q.Pa, q.Pa, k);
+    OzGemm g;
+    g.a = OzOpnd{PA, pA, q.Pa, 0};
+    g.b = OzOpnd{PB, pB, q.Pa, 0};
+    g.list = lists + q.la_off;
+    g.list_len = q.la_len;
+    g.K = q.Pa;
+    g.kbeg = 2;
+    g.kend = 0;
+    g.tri = 0;
+    g.ntj = ntj;
+    g.res = res;
+    g.res_bytes = rb;
+    OzCrt r{res, rb, 0, ntj, exA, exB, T, (long long)q.Pb, q.Rb, q.Ra, 0, 1.0};
+    gc(g, r, nti, q.ops_a, (double)q.Ra * q.Ra * q.Rb);
+  }
+  {   // X21 = -X22 T
+    const long long pA = (long long)q.Pb * q.Pb, pB = (long long)q.Pa * q.Pb;
+    int8_t* PA = planes;
+    int8_t* PB = planes + (size_t)k.nmod * pA;
+    (void)hipMemsetAsync(exA, 0, q.Pb * sizeof(int), st);
+    hipLaunchKernelGGL(k_oz_rowexp<true>, dim3(q.Pb / 64, (q.Rb + 255) / 256), dim3(256), 0, st, X22, ld, q.Rb, q.Pb,
+                       q.Rb, 2, k.beta, exA);
+    hipLaunchKernelGGL(k_oz_il_to_ex, dim3((q.Pb + 255) / 256), dim3(256), 0, st, exA, q.Pb, k.beta);
+    hipLaunchKernelGGL(k_oz_rowexp<false>, dim3(q.Pa / 4), dim3(256), 0, st, T, (long long)q.Pb, q.Ra, q.Pa, q.Rb, 0,
+                       k.beta, exB);
+    hipLaunchKernelGGL(k_oz_split_rect<true>, dim3(q.Pb / 64, q.Pb / 64), dim3(256), 0, st, X22, ld, q.Rb, q.Rb, 2,
+                       exA, PA, pA, (long long)q.Pb, q.Pb, k);
+    hipLaunchKernelGGL(k_oz_split_rect<false>, dim3(q.Pa, (q.Pb + 2047) / 2048), dim3(256), 0, st, T, (long long)q.Pb,
+                       q.Ra, q.Rb, 0, exB, PB, pB, (long long)q.Pb, q.Pb, k);
+    OzGemm g;
+    g.a = OzOpnd{PA, pA, q.Pb, 0};
+    g.b = OzOpnd{PB, pB, q.Pb, 0};
+    g.list = lists + q.lb_off;
+    g.list_len = q.lb_len;
+    g.K = q.Pb;
+    g.kbeg = 0;
+    g.kend = 1;
+    g.tri = 0;
+    g.ntj = ntj;
+    g.res = res;
+    g.res_bytes = rb;
+    OzCrt r{res, rb, 0, ntj, exA, exB, X21, ld, q.Rb, q.Ra, 0, -1.0};
+    gc(g, r, nti, q.ops_b, (double)q.Rb * q.Rb * q.Ra);
   }
 }
 

@@ -174,6 +174,25 @@ def test_loopback_gradient_chunked_trtri(ctx, monkeypatch, P):
     assert ok, (g, gref, err)
 
 
+def _oz_bytes(nb, P, nmod=16):
+    """The int8 A^-1 partial's buffers (gpemu_dist.hip oz_prepare, shared by the loopback
+    ranks): nmod planes of X_r^T (np2 x rank 0's rows) and nmod residue images of the largest
+    slab's 256-tiles (slabs of an even number of tile rows)."""
+    np_ = nb * 128
+    np2 = -(-np_ // 256) * 256
+    kp = ((nb - 1) // P + 1) * 128
+    whole = nb * 128 * np_
+    sd = 1 << 26
+    if whole <= 4 * sd:
+        sd = max(sd, whole // P)
+    sr = max(1, min(nb, sd // (128 * np_)))
+    if sr < nb and sr % 2:
+        sr = max(2, sr - 1)
+    tri = lambda t: t * (t + 1) // 2
+    maxt = max(tri((min(nb, a0 + sr) + 1) // 2) - tri(a0 // 2) for a0 in range(0, nb, sr))
+    return nmod * np2 * kp + nmod * maxt * 256 * 256 + 4 * np2 + (1 << 20)
+
+
 @pytest.mark.parametrize("n,P", [(4000, 2), (4000, 3), (10240, 4)])
 def test_loopback_rank_memory(n, P):
     """Each logical rank holds its own tile rows (of A and, after a gradient call, of
@@ -181,7 +200,8 @@ def test_loopback_rank_memory(n, P):
     gradient: its rows of L^-1 plus at most three slab-sized buffers (the A^-1 partial's
     slab, the TRTRI's gathered X11 and all-gather buffer), the slab being the whole
     triangle's tile rows / P (at least 512 MiB, at most the whole) -- at n = 10240, P = 4
-    one n x n partial per rank (the round-4 slab) would exceed it."""
+    one n x n partial per rank (the round-4 slab) would exceed it; plus the int8 partial's
+    planes and residues (_oz_bytes)."""
     d = 3
     X, f, H = orc.synthetic_problem(n, d, seed=1)
     dc = native.DistContext(0, P)
@@ -204,7 +224,59 @@ def test_loopback_rank_memory(n, P):
         rows = native.dist_local_rows(n, P, r, d + 1)
         xrows = rows * 128 * nb * 128 * 8
         assert grad[r] - val[r] >= xrows                            # its rows of L^-1
-        assert grad[r] - val[r] <= xrows + 3 * slab + (64 << 20), (grad[r] - val[r], xrows, slab)
+        assert grad[r] - val[r] <= xrows + 3 * slab + _oz_bytes(nb, P) + (64 << 20), (grad[r] - val[r], xrows, slab)
     with pytest.raises(RuntimeError):
         dc.rank_bytes(P)
     dc.close()
+
+
+@pytest.mark.parametrize("P,slab_mb", [(1, None), (2, None), (3, 16), (5, 1)])
+def test_loopback_int8_partial_matches_fp64(monkeypatch, P, slab_mb):
+    """The rank partials of A^-1 on the int8 cores (gpemu_dist.hip oz_slab: each rank's
+    X_r^T X_r from its own rows, K from the first nonzero local row of each 256-column block)
+    against the same context type with GPEMU_OZAKI=0 (fp64 k_gemm slabs): the LLH equal (it
+    does not depend on A^-1), the gradient to 1e-10 of scale.  n = 3000 / 2900 pad to 24 / 23
+    tile rows (the last 256-tile half past n_pad); slabs of 16 and 1 MiB (5 tile rows, rounded to 4; 1 row, raised to 2)
+    split the partial into 6 and 12 slabs; against the oracle to the suite's 1e-7.  At P = 1
+    the top TRTRI levels run on the int8 cores too (GPEMU_OZAKI_TRI_MIN lowered)."""
+    n, d = (2900 if P == 3 else 3000), 5   # 23 / 24 tile rows
+    X, f, H = orc.synthetic_problem(n, d, seed=17)
+    r = np.random.RandomState(3).uniform(1e-4, 1e-3, size=n)
+    hp = _hp(d)
+    if slab_mb:
+        monkeypatch.setenv("GPEMU_DIST_SLAB_MB", str(slab_mb))
+    # P = 1: the TRTRI levels of blocks >= 1024 rows on the int8 cores as well (pairs
+    # (0, 8, 16) and (0, 16, 24) at 24 tile rows: a ragged second block)
+    monkeypatch.setenv("GPEMU_OZAKI_TRI_MIN", "1024")
+    out = {}
+    for oz in ("0", "1"):
+        monkeypatch.setenv("GPEMU_OZAKI", oz)
+        dc = native.DistContext(0, P)
+        dc.set_data(X, f, H, r)
+        out[oz] = dc.objective(native.GP4ML, native.KERNEL_ALT_NUG, hp, want_grad=True)
+        dc.close()
+    (l0, g0, _), (l1, g1, _) = out["0"], out["1"]
+    assert l1 == l0
+    scale = np.abs(g0) + np.max(np.abs(g0))
+    assert np.max(np.abs(g1 - g0) / scale) <= 1e-10, (g1, g0)
+    ref = orc.objective_fast(X, f, H, hp, orc.GP4ML, orc.ALT, True, r=r)
+    ok, err = _grad_ok(g1, ref[1])
+    assert ok, err
+
+
+def test_loopback_fused_next_factor_bit_identical(monkeypatch):
+    """GPEMU_DIST_FUSE_NEXT=1 (P = 1: each group's first factor inside the update launch
+    before it, on tile counts) changes the launches, not the arithmetic: LLH and gradient
+    bit-identical to the default schedule, for a ragged n with 4-wide groups to the end."""
+    n, d = 2500, 4
+    X, f, H = orc.synthetic_problem(n, d, seed=23)
+    hp = _hp(d)
+    out = []
+    for fz in ("0", "1"):
+        monkeypatch.setenv("GPEMU_DIST_FUSE_NEXT", fz)
+        dc = native.DistContext(0, 1)
+        dc.set_data(X, f, H)
+        out.append(dc.objective(native.GP4ML, native.KERNEL_STD, hp, want_grad=True))
+        dc.close()
+    assert out[0][0] == out[1][0]
+    assert np.array_equal(out[0][1], out[1][1])
