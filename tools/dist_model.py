@@ -107,7 +107,7 @@ def trtri_collectives(nb, P, cap):
     return cnt, rb
 
 
-def rank_memory_gb(nb, na, P, d, pc, widths, grad=True):
+def rank_memory_gb(nb, na, P, d, pc, widths, grad=True, int8=True):
     """Device bytes of rank 0 (the largest share), in GB."""
     nt, n_pad = nb + na, nb * TILE
     gs = groups(nb, widths)
@@ -131,6 +131,17 @@ def rank_memory_gb(nb, na, P, d, pc, widths, grad=True):
                 g1n = max(g1n, g1 * cc * TILE * TILE)
                 rvn = max(rvn, P * s1 * cc * TILE * TILE, P * s2 * cc * TILE * TILE)
             b += g1n + (0 if rvn <= recv else rvn)
+        # the int8 partial's planes and residues (gpemu_dist.hip oz_prepare; bytes), while the
+        # planes fit 16 GiB
+        np2 = -(-n_pad // 256) * 256
+        kp = ((nb - 1) // P + 1) * TILE
+        if int8 and 16 * np2 * kp <= 16 << 30:
+            sr = max(1, min(nb, sd // (TILE * n_pad)))
+            if sr < nb and sr % 2:
+                sr = max(2, sr - 1)
+            tri = lambda t: t * (t + 1) // 2
+            maxt = max(tri((min(nb, a0 + sr) + 1) // 2) - tri(a0 // 2) for a0 in range(0, nb, sr))
+            b += (16 * np2 * kp + 16 * maxt * 256 * 256) / 8
     return (b + shared) * 8 / 1e9
 
 
@@ -146,6 +157,8 @@ def main():
     ap.add_argument("--alpha-us", type=float, default=25.0)
     ap.add_argument("--beta2", type=float, default=64.0, help="GB/s per rank at P=2")
     ap.add_argument("--beta", type=float, default=300.0, help="GB/s per rank at P>=4")
+    ap.add_argument("--single-ms", type=float, default=None, help="the single-GPU path's LLH+gradient ms")
+    ap.add_argument("--no-int8", action="store_true", help="memory without the int8 partial's buffers")
     ap.add_argument("--trtri-overlap", choices=("none", "prev-level", "full"), default="none",
                     help="TRTRI all-gathers hidden behind compute: none (round 5, in series), prev-level "
                          "(level l's gathers beside level l-1's products: round-6 verdict option 1), full "
@@ -170,7 +183,7 @@ def main():
                "trtri_collectives": c_tr, "trtri_recv_GB": b_tr / 1e9,
                "comm_ms": comm_sweep + comm_tr + comm_rest,
                "comm_sweep_ms": comm_sweep, "comm_trtri_ms": comm_tr,
-               "rank_memory_GB": rank_memory_gb(nb, na, P, args.dims, args.basis, widths)}
+               "rank_memory_GB": rank_memory_gb(nb, na, P, args.dims, args.basis, widths, int8=not args.no_int8)}
         if args.p1_ms and args.p1_value_ms:
             chain = nb * args.chain_us * 1e-3
             sweep = args.p1_value_ms
@@ -205,6 +218,8 @@ def main():
                 row["trtri_comm_hidden_ms"] = hidden
             row["predicted_ms"] = t_sweep + t_grad + comm_rest
             row["speedup_vs_p1"] = args.p1_ms / row["predicted_ms"]
+            if args.single_ms:
+                row["speedup_vs_single_gpu"] = args.single_ms / row["predicted_ms"]
         rows.append(row)
     for r in rows:
         print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}))
