@@ -189,6 +189,18 @@ struct gpe_ctx {
   bool x32_valid = false;
   float* dK32 = nullptr;
   size_t k32_cap = 0;
+  // posterior V = L^-1 K* on the int8 cores (posterior_oz): planes of L^-1's rows and their
+  // exponents (formed once per factor and moduli count), each chunk's K* planes, exponents
+  // and residues, the tile list
+  int8_t* dpxp = nullptr;
+  int* dpxe = nullptr;
+  int8_t* dpkp = nullptr;
+  int* dpke = nullptr;
+  int8_t* dpres = nullptr;
+  unsigned* dpl = nullptr;
+  size_t pxp_cap = 0, pxe_cap = 0, pkp_cap = 0, pke_cap = 0, pres_cap = 0, pl_cap = 0;
+  int px_nmod = 0, pl_nti = 0, pl_ntj = 0, pl_len = 0;
+  bool px_valid = false;
 
   // sensitivity workspace (gpe_sense_pairs / gpe_gauss_transform)
   double* dSU = nullptr;     // J x n_pad per-point factors
@@ -1475,6 +1487,7 @@ int ensure_linv(gpe_ctx* c) {
   CHK(trtri(c, c->tr));
   c->linv_valid = true;
   c->x32_valid = false;
+  c->px_valid = false;
   return GPE_OK;
 }
 
@@ -1819,6 +1832,8 @@ void gpe_destroy(gpe_ctx* c) {
   if (c->dinfo) hipFree(c->dinfo);
   if (c->dX32) hipFree(c->dX32);
   if (c->dK32) hipFree(c->dK32);
+  for (void* b : {(void*)c->dpxp, (void*)c->dpxe, (void*)c->dpkp, (void*)c->dpke, (void*)c->dpres, (void*)c->dpl})
+    if (b) hipFree(b);
   if (c->tr.flags) hipFree(c->tr.flags);
   if (c->aux.flags) hipFree(c->aux.flags);
   for (Fact* F : {&c->tr, &c->aux}) {
@@ -1871,6 +1886,7 @@ int gpe_set_data(gpe_ctx* c, int64_t n, int32_t d, int32_t q, const double* X, c
   c->factor_valid = false;
   c->ainv_valid = false;
   c->x32_valid = false;
+  c->px_valid = false;
   c->zaug_valid = false;
   c->linv_valid = false;
   if (resize) {
@@ -2196,6 +2212,7 @@ int gpe_objective(gpe_ctx* c, int32_t variant, int32_t kernel, const double* hp,
   c->factor_valid = false;
   c->ainv_valid = false;
   c->x32_valid = false;
+  c->px_valid = false;
   if (c->prof) {
     c->gev_used = 0;
     c->gemm_launches = c->gemm_flops = c->gemm_ms = 0.0;
@@ -2340,6 +2357,7 @@ int gpe_factor(gpe_ctx* c, int32_t kernel, const double* delta, double nu, doubl
   c->factor_valid = false;
   c->ainv_valid = false;
   c->x32_valid = false;
+  c->px_valid = false;
   CHK(factor_and_invert(c, kernel, delta, nu, s2, r_scale, false));   // L^-1 on demand
   int info = 0;
   double logdet = 0.0;
@@ -2350,6 +2368,7 @@ int gpe_factor(gpe_ctx* c, int32_t kernel, const double* delta, double nu, doubl
   }
   c->factor_valid = true;
   c->x32_valid = false;
+  c->px_valid = false;
   c->f_kernel = kernel;
   c->f_delta.assign(delta, delta + c->d);
   c->f_nu = nu;
@@ -2363,6 +2382,89 @@ static int grow(gpe_ctx* c, double** p, size_t* cap, size_t need) {
   *cap = 0;
   CHK(dalloc(c, p, need));
   *cap = need;
+  return GPE_OK;
+}
+
+extern "C++" {   // (inside the C-ABI block: a template needs C++ linkage)
+template <class T>
+static int growt(gpe_ctx* c, T** p, size_t* cap, size_t need) {
+  if (need <= *cap) return GPE_OK;
+  *cap = 0;
+  CHK(dalloc(c, p, need));
+  *cap = need;
+  return GPE_OK;
+}
+}
+
+// moduli of the posterior's int8 product: 16 for precision 64 (53-bit operands at n_pad <=
+// 16384, as the objective's), for precision 32 the fewest whose operands keep >= 24 bits (the
+// fp32 significand: 8 at n_pad <= 16384) -- exact products of operands as precise as fp32's
+static int posterior_nmod(int np2, bool f32) {
+  if (!f32) return OZ_MAXMOD;
+  int bits = 24;
+  if (const char* e = std::getenv("GPEMU_OZAKI_POST32_BITS")) bits = std::max(16, std::min(53, std::atoi(e)));
+  for (int N = 6; N < OZ_MAXMOD; ++N)
+    if (oz_consts(N, np2).beta >= bits) return N;
+  return OZ_MAXMOD;
+}
+
+// V = L^-1 K* (n_pad x mp, fp64, ld n_pad) on the int8 cores (gpemu_ozaki.hpp): op(A) = the
+// rows of L^-1 (k <= the row: kend = 256 (ti + 1)), op(B) = the chunk's points (columns of K*,
+// contiguous in k), N moduli, CRT straight into V.  Replaces the fp64 k_gemm product
+// (precision 64, 62 TF/s) and the fp32 one (precision 32, 129 TF/s); the column norms and the
+// full-covariance blocks read V as before.
+static int posterior_oz(gpe_ctx* c, bool f32, const double* Ks, long long mp, double* V) {
+  const int np = (int)c->n_pad, np2 = (np + OZ_T - 1) / OZ_T * OZ_T;
+  const int mp2 = (int)((mp + OZ_T - 1) / OZ_T * OZ_T);
+  const int N = posterior_nmod(np2, f32), nti = np2 / OZ_T, ntj = mp2 / OZ_T;
+  const OzConst k = oz_consts(N, np2);
+  hipStream_t st = c->stream;
+  if (!c->px_valid || c->px_nmod != N) {
+    CHK(growt(c, &c->dpxp, &c->pxp_cap, (size_t)N * np2 * np2));
+    CHK(growt(c, &c->dpxe, &c->pxe_cap, (size_t)np2));
+    HIPCHK(c, hipMemsetAsync(c->dpxe, 0, (size_t)np2 * sizeof(int), st));
+    hipLaunchKernelGGL(k_oz_rowexp<true>, dim3(np2 / 64, (np + 255) / 256), dim3(256), 0, st, c->tr.B, (long long)np,
+                       np, np2, np, 2, k.beta, c->dpxe);
+    hipLaunchKernelGGL(k_oz_il_to_ex, dim3((np2 + 255) / 256), dim3(256), 0, st, c->dpxe, np2, k.beta);
+    hipLaunchKernelGGL(k_oz_split_rect<true>, dim3(np2 / 64, np2 / 64), dim3(256), 0, st, c->tr.B, (long long)np, np,
+                       np, 2, c->dpxe, c->dpxp, (long long)np2 * np2, (long long)np2, np2, k);
+    HIPCHK(c, hipGetLastError());
+    c->px_valid = true;
+    c->px_nmod = N;
+  }
+  if (c->pl_nti != nti || c->pl_ntj != ntj) {
+    const std::vector<unsigned> l = oz_list(nti, ntj, false, [&](int ti, int) { return (double)(OZ_T * (ti + 1)); });
+    c->pl_nti = c->pl_ntj = 0;
+    CHK(growt(c, &c->dpl, &c->pl_cap, l.size()));
+    HIPCHK(c, hipMemcpy(c->dpl, l.data(), l.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+    c->pl_len = (int)l.size();
+    c->pl_nti = nti;
+    c->pl_ntj = ntj;
+  }
+  const long long pB = (long long)mp2 * np2, rb = (long long)nti * ntj * OZ_T * OZ_T;
+  CHK(growt(c, &c->dpkp, &c->pkp_cap, (size_t)N * pB));
+  CHK(growt(c, &c->dpke, &c->pke_cap, (size_t)mp2));
+  CHK(growt(c, &c->dpres, &c->pres_cap, (size_t)N * rb));
+  hipLaunchKernelGGL(k_oz_rowexp<false>, dim3(mp2 / 4), dim3(256), 0, st, Ks, (long long)np, (int)mp, mp2, np, 0, k.beta,
+                     c->dpke);
+  hipLaunchKernelGGL(k_oz_split_rect<false>, dim3(mp2, (np2 + 2047) / 2048), dim3(256), 0, st, Ks, (long long)np,
+                     (int)mp, np, 0, c->dpke, c->dpkp, pB, (long long)np2, np2, k);
+  OzGemm g;
+  g.a = OzOpnd{c->dpxp, (long long)np2 * np2, np2, 0};
+  g.b = OzOpnd{c->dpkp, pB, np2, 0};
+  g.list = c->dpl;
+  g.list_len = c->pl_len;
+  g.K = np2;
+  g.kbeg = 0;
+  g.kend = 1;
+  g.tri = 0;
+  g.ntj = ntj;
+  g.res = c->dpres;
+  g.res_bytes = rb;
+  hipLaunchKernelGGL(k_oz_gemm, dim3(N * g.list_len), dim3(256), OZ_LDS, st, g, k);
+  OzCrt r{c->dpres, rb, 0, ntj, c->dpxe, c->dpke, V, (long long)np, np, (int)mp, 0, 1.0};
+  hipLaunchKernelGGL(k_oz_crt, dim3((unsigned)(nti * ntj * 16)), dim3(256), 0, st, r, k);
+  HIPCHK(c, hipGetLastError());
   return GPE_OK;
 }
 
@@ -2534,10 +2636,11 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
   if (precision == 32 && full_var) return fail(c, GPE_ERR_UNSUPPORTED, "precision 32 is for the diagonal variance");
   CHK(ensure_linv(c));
   const bool f32 = precision == 32;
+  const bool ozp = oz_use(c);   // V on the int8 cores (posterior_oz), either precision
   const int d = c->d, q = c->q, P = q + 1;
   const long long np = c->n_pad;
   const long long CHUNK = full_var ? 16384 : 8192;
-  if (f32 && !c->x32_valid) {
+  if (f32 && !ozp && !c->x32_valid) {
     // fp32 copy of L^-1 (the full square: the GEMM reads only k <= its row tile)
     const size_t need = (size_t)np * np;
     if (need > c->x32_cap) {
@@ -2662,7 +2765,9 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
       HIPCHK(c, hipGetLastError());
     }
     // V = L^-1 K*   (np x mp), X lower-triangular -> kend = (ti+1)*128
-    if (f32) {
+    if (ozp) {
+      CHK(posterior_oz(c, f32, c->dW1, mp, big ? c->dVall + s0 * np : c->dW2));
+    } else if (f32) {
       const size_t need32 = 2 * (size_t)np * mp;
       if (need32 > c->k32_cap) {
         if (c->dK32) (void)hipFree(c->dK32);
@@ -2717,7 +2822,7 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
     if (!full_var) {
       CHK(ensure_small(c, (size_t)mp * P + mp + 64));
       double* dn = c->dsmall + (size_t)mp * P;
-      if (f32)
+      if (f32 && !ozp)
         hipLaunchKernelGGL(k_colnorm2_f32, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, c->stream,
                            c->dK32 + (size_t)np * mp, np, (int)np, (int)mp, dn);
       else

@@ -60,11 +60,15 @@ def test_posterior_large_m_chunked(ctx):
     assert np.max(np.abs(var[sel] - np.diag(v_ref))) < 1e-8
 
 
-def test_posterior_precision32_diagonal(ctx):
-    """precision 32 (config C5): L^-1 K* on fp32 MFMA.  The mean is fp64 and must
-    equal the fp64 path; the diagonal variance sigma^2 (1 - |L^-1 k*|^2 + ...)
-    loses ~fp32 eps * |L^-1 k*|^2 to cancellation, tolerance 2e-5 * sigma^2."""
+@pytest.mark.parametrize("oz", ["1", "0"])
+def test_posterior_precision32_diagonal(monkeypatch, oz):
+    """precision 32 (config C5): L^-1 K* as exact int8 products of 24-bit operands (8 moduli,
+    posterior_oz), or with GPEMU_OZAKI=0 on fp32 MFMA.  The mean is fp64 and must equal the
+    fp64 path; the diagonal variance sigma^2 (1 - |L^-1 k*|^2 + ...) loses ~fp32 eps *
+    |L^-1 k*|^2 to cancellation, tolerance 2e-5 * sigma^2."""
     from gp_emu_uqsa_amd import native, synthetic
+    monkeypatch.setenv("GPEMU_OZAKI", oz)
+    ctx = native.Context(0)
     X, f, H = synthetic.problem(2000, 6, seed=3)
     ctx.set_data(X, f, H)
     delta = np.full(6, 0.8)
@@ -78,6 +82,44 @@ def test_posterior_precision32_diagonal(ctx):
     assert np.max(np.abs(v32 - v64)) < 2e-5 * 0.81, np.max(np.abs(v32 - v64))
     with pytest.raises(RuntimeError):
         ctx.posterior(xs[:10], hs[:10], beta, 0.9, full_var=True, precision=32)
+    ctx.close()
+
+
+def test_posterior_int8_matches_fp64(monkeypatch):
+    """V = L^-1 K* on the int8 cores (posterior_oz, n_pad >= 2048) against the fp64 k_gemm
+    product (GPEMU_OZAKI=0) and the oracle: precision 64 (16 moduli, 53-bit operands) to
+    1e-11 sigma^2 in the diagonal and in the full covariance, precision 32 (8 moduli, 24-bit
+    operands) to 4e-6 sigma^2, below the fp32 GEMM's own error on these inputs; ragged n (2200: 9 tiles of 256) and chunks (9000 points: a full
+    8192-point chunk and a ragged one)."""
+    from gp_emu_uqsa_amd import native, synthetic
+    n, d, s2 = 2200, 5, 0.9 ** 2
+    X, f, H = synthetic.problem(n, d, seed=5)
+    delta = np.full(d, 0.7)
+    xs = synthetic.design(9000, d, seed=8)
+    hs = synthetic.linear_basis(xs)
+    out = {}
+    for oz in ("0", "1"):
+        monkeypatch.setenv("GPEMU_OZAKI", oz)
+        c = native.Context(0)
+        c.set_data(X, f, H)
+        c.factor(native.KERNEL_STD, delta, 1e-3, 1.0, 0.0)
+        beta = c.beta()
+        out[oz] = (c.posterior(xs, hs, beta, 0.9, full_var=False, precision=64),
+                   c.posterior(xs, hs, beta, 0.9, full_var=False, precision=32),
+                   c.posterior(xs[:300], hs[:300], beta, 0.9, full_var=True, precision=64), beta)
+        c.close()
+    (m0, v0), _, (mf0, vf0), beta = out["0"]
+    (m1, v1), (m132, v132), (mf1, vf1), _ = out["1"]
+    assert np.array_equal(m1, m0) and np.array_equal(m132, m0)
+    assert np.max(np.abs(v1 - v0)) < 1e-11 * s2, np.max(np.abs(v1 - v0))
+    # (the fp32 GEMM, GPEMU_OZAKI=0, is 7.9e-6 off on these inputs: tools/post_err_r06.py)
+    assert np.max(np.abs(v132 - v0)) < 4e-6 * s2, np.max(np.abs(v132 - v0))
+    assert np.max(np.abs(vf1 - vf0)) < 1e-11 * s2, np.max(np.abs(vf1 - vf0))
+    A, _ = orc.kernel_var_ref(X, delta, 1e-3, orc.STD, True)
+    sel = np.arange(0, 9000, 450)
+    m_ref, v_ref = orc.posterior_ref(X, f, H, A, xs[sel], hs[sel], beta, 0.9, delta, 1e-3, orc.STD)
+    assert np.max(np.abs(m1[sel] - m_ref)) < 1e-8
+    assert np.max(np.abs(v1[sel] - np.diag(v_ref))) < 1e-8
 
 
 @pytest.mark.parametrize("kind", [orc.STD, orc.ALT])
