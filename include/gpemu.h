@@ -115,9 +115,11 @@ int gpe_beta(gpe_ctx* ctx, double* beta_out);
  * mean_out m; var_out m x m (row-major) when full_var != 0, else its diagonal
  * (m values); any m, in chunks of 16384 points (full: blocks of the m x m result
  * formed on the device and written to the host).  sigma is par.sigma.
- * precision 64: everything in fp64.  precision 32 (diagonal only; SURVEY 8b/8d,
- * BASELINE config C5): the dominant product L^-1 K* (n^2 m flops) runs on fp32
- * MFMA from fp32 copies of L^-1 and K*; the mean and the q x q terms stay fp64. */
+ * precision 64: fp64 accuracy; for 2048 <= n_pad <= 32768 the dominant product
+ * L^-1 K* (n^2 m flops) runs as exact int8 products of 53-bit operands (16 moduli).
+ * precision 32 (diagonal only; SURVEY 8b/8d, BASELINE config C5): that product from
+ * 24-bit operands (8 moduli; GPEMU_OZAKI=0 or n_pad outside that range: fp32 MFMA on
+ * fp32 copies of L^-1 and K*); the mean and the q x q terms stay fp64. */
 int gpe_posterior(gpe_ctx* ctx, int64_t m, const double* Xs, const double* Hs,
                   const double* beta, double sigma, int32_t full_var, int32_t precision,
                   double* mean_out, double* var_out);
