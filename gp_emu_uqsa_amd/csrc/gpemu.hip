@@ -1208,6 +1208,16 @@ int kbuild(gpe_ctx* c, int kernel, double nu, double s2, double rscale) {
 // Every launcher of a workspace's schedule first makes sure it is built: growing the
 // tile-list array for one workspace's plan resets the other's (build_plan), e.g. the
 // aux plan of gpe_noise_sample between gpe_factor and a later on-demand TRTRI / LAUUM.
+// grow a device buffer to at least need elements (contents not kept)
+template <class T>
+int grow_buf(gpe_ctx* c, T** p, size_t* cap, size_t need) {
+  if (need <= *cap) return GPE_OK;
+  *cap = 0;
+  CHK(dalloc(c, p, need));
+  *cap = need;
+  return GPE_OK;
+}
+
 int potrf(gpe_ctx* c, Fact& F, bool with_aug = false) {
   CHK(build_plan(c, F));
   const Plan& pl = F.plan;
@@ -2385,16 +2395,6 @@ static int grow(gpe_ctx* c, double** p, size_t* cap, size_t need) {
   return GPE_OK;
 }
 
-extern "C++" {   // (inside the C-ABI block: a template needs C++ linkage)
-template <class T>
-static int growt(gpe_ctx* c, T** p, size_t* cap, size_t need) {
-  if (need <= *cap) return GPE_OK;
-  *cap = 0;
-  CHK(dalloc(c, p, need));
-  *cap = need;
-  return GPE_OK;
-}
-}
 
 // moduli of the posterior's int8 product: 16 for precision 64 (53-bit operands at n_pad <=
 // 16384, as the objective's), for precision 32 the fewest whose operands keep >= 24 bits (the
@@ -2420,8 +2420,8 @@ static int posterior_oz(gpe_ctx* c, bool f32, const double* Ks, long long mp, do
   const OzConst k = oz_consts(N, np2);
   hipStream_t st = c->stream;
   if (!c->px_valid || c->px_nmod != N) {
-    CHK(growt(c, &c->dpxp, &c->pxp_cap, (size_t)N * np2 * np2));
-    CHK(growt(c, &c->dpxe, &c->pxe_cap, (size_t)np2));
+    CHK(grow_buf(c, &c->dpxp, &c->pxp_cap, (size_t)N * np2 * np2));
+    CHK(grow_buf(c, &c->dpxe, &c->pxe_cap, (size_t)np2));
     HIPCHK(c, hipMemsetAsync(c->dpxe, 0, (size_t)np2 * sizeof(int), st));
     hipLaunchKernelGGL(k_oz_rowexp<true>, dim3(np2 / 64, (np + 255) / 256), dim3(256), 0, st, c->tr.B, (long long)np,
                        np, np2, np, 2, k.beta, c->dpxe);
@@ -2435,16 +2435,16 @@ static int posterior_oz(gpe_ctx* c, bool f32, const double* Ks, long long mp, do
   if (c->pl_nti != nti || c->pl_ntj != ntj) {
     const std::vector<unsigned> l = oz_list(nti, ntj, false, [&](int ti, int) { return (double)(OZ_T * (ti + 1)); });
     c->pl_nti = c->pl_ntj = 0;
-    CHK(growt(c, &c->dpl, &c->pl_cap, l.size()));
+    CHK(grow_buf(c, &c->dpl, &c->pl_cap, l.size()));
     HIPCHK(c, hipMemcpy(c->dpl, l.data(), l.size() * sizeof(unsigned), hipMemcpyHostToDevice));
     c->pl_len = (int)l.size();
     c->pl_nti = nti;
     c->pl_ntj = ntj;
   }
   const long long pB = (long long)mp2 * np2, rb = (long long)nti * ntj * OZ_T * OZ_T;
-  CHK(growt(c, &c->dpkp, &c->pkp_cap, (size_t)N * pB));
-  CHK(growt(c, &c->dpke, &c->pke_cap, (size_t)mp2));
-  CHK(growt(c, &c->dpres, &c->pres_cap, (size_t)N * rb));
+  CHK(grow_buf(c, &c->dpkp, &c->pkp_cap, (size_t)N * pB));
+  CHK(grow_buf(c, &c->dpke, &c->pke_cap, (size_t)mp2));
+  CHK(grow_buf(c, &c->dpres, &c->pres_cap, (size_t)N * rb));
   hipLaunchKernelGGL(k_oz_rowexp<false>, dim3(mp2 / 4), dim3(256), 0, st, Ks, (long long)np, (int)mp, mp2, np, 0, k.beta,
                      c->dpke);
   hipLaunchKernelGGL(k_oz_split_rect<false>, dim3(mp2, (np2 + 2047) / 2048), dim3(256), 0, st, Ks, (long long)np,
