@@ -399,60 +399,112 @@ static __global__ void __launch_bounds__(256) k_oz_il_to_ex(int* __restrict__ ex
   if (r < Rp) ex[r] = ex[r] > 0 ? (beta - 1) - (ex[r] - 2048) : 0;
 }
 
+// x (an integer-valued double, |x| <= 2^53) -> its centred residue mod m as one byte
+__device__ __forceinline__ unsigned oz_res8(double x, double m, double im, int mi) {
+  // x - m rint(x / m) is exact (the product q m an integer below 2^53), |.| <= m / 2 + 1;
+  // the m = 256 one wraps into int8 congruently
+  const double q = rint(x * im);
+  int r = (int)fma(-q, m, x);
+  r = r > 127 ? r - mi : (r < -128 ? r + mi : r);
+  return (unsigned)r & 0xffu;
+}
+
 // op -> the N int8 planes, rectangular (row r at r ldp + k, k < Kp; zero past R / Kv and
-// masked).  TRANS false: thread = 8 consecutive k of one row (contiguous in src).  TRANS true:
-// workgroup = 64 rows x 64 k, thread = 16 consecutive k of one row with the lanes along r
-// (each load coalesced); each plane's 64 x 64 bytes go through LDS so the stores run along
-// k (4 threads per row, 16 bytes each).
+// masked).  TRANS false: thread = 8 consecutive k of one row (contiguous in src: four 16-byte
+// loads when the 8 are in range and on one side of the mask's diagonal).  TRANS true:
+// workgroup = 64 rows x 64 k, thread = 2 adjacent rows x 8 consecutive k (each load 16 bytes,
+// the lanes along r); each plane's 64 x 64 bytes go through LDS so the stores run along k
+// (4 threads per row, 16 bytes each).
 template <bool TRANS>
 static __global__ void __launch_bounds__(256) k_oz_split_rect(const double* __restrict__ src, long long ld, int R,
                                                               int Kv, int mask, const int* __restrict__ ex,
                                                               int8_t* __restrict__ planes, long long plane_bytes,
                                                               long long ldp, int Kp, OzConst cst) {
-  constexpr int NK = TRANS ? 16 : 8;
-  int r, k0;
-  if constexpr (TRANS) {
-    r = blockIdx.x * 64 + (threadIdx.x & 63);
-    k0 = ((int)blockIdx.y * 4 + (threadIdx.x >> 6)) * NK;
-  } else {
-    r = blockIdx.x;
-    k0 = ((int)blockIdx.y * 256 + (int)threadIdx.x) * NK;
+  if constexpr (!TRANS) {
+    const int r = blockIdx.x;
+    const int k0 = ((int)blockIdx.y * 256 + (int)threadIdx.x) * 8;
     if (k0 >= Kp) return;
-  }
-  const int e = ex[r];
-  double xs[NK];
+    const int e = ex[r];
+    double xs[8];
+    const double* p = src + k0 + (long long)r * ld;
+    // the mask's diagonal k = r: all 8 kept (1), all dropped (0), or mixed (2)
+    const int side = mask == 1 ? (k0 >= r ? 1 : (k0 + 7 < r ? 0 : 2))
+                   : (mask == 2 ? (k0 + 7 <= r ? 1 : (k0 > r ? 0 : 2)) : 1);
+    if (r < R && k0 + 8 <= Kv && side == 1 && ((reinterpret_cast<uintptr_t>(p) & 15) == 0)) {
 #pragma unroll
-  for (int u = 0; u < NK; ++u) {
-    const int k = k0 + u;
-    double v = 0.0;
-    if (r < R && k < Kv && oz_keep(mask, r, k)) v = TRANS ? src[r + (long long)k * ld] : src[k + (long long)r * ld];
-    xs[u] = rint(ldexp(v, e));
-  }
-  __shared__ oz_v4i tr[64 * 5];   // TRANS: [row][16-byte piece], pitch 5 pieces (bank spread)
-  for (int l = 0; l < cst.nmod; ++l) {
-    const double m = (double)cst.m[l], im = 1.0 / m;
-    unsigned w[NK / 4];
-#pragma unroll
-    for (int c = 0; c < NK / 4; ++c) w[c] = 0u;
-#pragma unroll
-    for (int u = 0; u < NK; ++u) {
-      const double q = rint(xs[u] * im);
-      int rr = (int)fma(-q, m, xs[u]);
-      rr = rr > 127 ? rr - cst.m[l] : (rr < -128 ? rr + cst.m[l] : rr);
-      w[u >> 2] |= ((unsigned)rr & 0xffu) << (8 * (u & 3));
-    }
-    if constexpr (TRANS) {
-      const int rl = threadIdx.x & 63, pc = threadIdx.x >> 6;
-      if (l > 0) __syncthreads();   // (the previous plane's reads done)
-      tr[rl * 5 + pc] = oz_v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
-      __syncthreads();
-      const int wr = threadIdx.x >> 2, wp = threadIdx.x & 3;   // row wr, piece wp of the block
-      const long long row = (long long)blockIdx.x * 64 + wr;
-      *reinterpret_cast<oz_v4i*>(planes + (long long)l * plane_bytes + row * ldp + (long long)blockIdx.y * 64 + 16 * wp) =
-          tr[wr * 5 + wp];
+      for (int u = 0; u < 8; u += 2) {
+        const double2 v = *reinterpret_cast<const double2*>(p + u);
+        xs[u] = v.x;
+        xs[u + 1] = v.y;
+      }
     } else {
-      *reinterpret_cast<uint2*>(planes + (long long)l * plane_bytes + (long long)r * ldp + k0 + (long long)0) =
-          make_uint2(w[0], w[1]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u;
+        xs[u] = (side != 0 && r < R && k < Kv && oz_keep(mask, r, k)) ? p[u] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xs[u] = rint(ldexp(xs[u], e));
+    int8_t* dst = planes + (long long)r * ldp + k0;
+    for (int l = 0; l < cst.nmod; ++l) {
+      const double m = (double)cst.m[l], im = 1.0 / m;
+      unsigned w0 = 0u, w1 = 0u;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        w0 |= oz_res8(xs[u], m, im, cst.m[l]) << (8 * u);
+        w1 |= oz_res8(xs[u + 4], m, im, cst.m[l]) << (8 * u);
+      }
+      *reinterpret_cast<uint2*>(dst + (long long)l * plane_bytes) = make_uint2(w0, w1);
+    }
+  } else {
+    __shared__ __attribute__((aligned(16))) unsigned tr[64 * 20];   // [row][16 words + 4 pad]
+    const int lane = threadIdx.x & 63, rp = lane & 31, kg = (int)threadIdx.x >> 5;
+    const int r = (int)blockIdx.x * 64 + 2 * rp;          // rows r, r + 1
+    const int k0 = (int)blockIdx.y * 64 + 8 * kg;         // k0 .. k0 + 7
+    const int e0 = ex[r], e1 = ex[r + 1];
+    double x0[8], x1[8];
+    const double* p = src + r + (long long)k0 * ld;
+    const bool vec = r + 1 < R && ((reinterpret_cast<uintptr_t>(src + r) & 15) == 0) && (ld & 1) == 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + u;
+      double a = 0.0, b = 0.0;
+      if (k < Kv) {
+        if (vec) {
+          const double2 v = *reinterpret_cast<const double2*>(p + (long long)u * ld);
+          a = v.x;
+          b = v.y;
+        } else {
+          if (r < R) a = p[(long long)u * ld];
+          if (r + 1 < R) b = p[(long long)u * ld + 1];
+        }
+      }
+      x0[u] = oz_keep(mask, r, k) ? a : 0.0;
+      x1[u] = oz_keep(mask, r + 1, k) ? b : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      x0[u] = rint(ldexp(x0[u], e0));
+      x1[u] = rint(ldexp(x1[u], e1));
+    }
+    const int wr = (int)threadIdx.x >> 2, wp = (int)threadIdx.x & 3;   // row wr, piece wp of the block
+    int8_t* dst = planes + ((long long)blockIdx.x * 64 + wr) * ldp + (long long)blockIdx.y * 64 + 16 * wp;
+    for (int l = 0; l < cst.nmod; ++l) {
+      const double m = (double)cst.m[l], im = 1.0 / m;
+      unsigned a0 = 0u, a1 = 0u, b0 = 0u, b1 = 0u;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a0 |= oz_res8(x0[u], m, im, cst.m[l]) << (8 * u);
+        a1 |= oz_res8(x0[u + 4], m, im, cst.m[l]) << (8 * u);
+        b0 |= oz_res8(x1[u], m, im, cst.m[l]) << (8 * u);
+        b1 |= oz_res8(x1[u + 4], m, im, cst.m[l]) << (8 * u);
+      }
+      if (l > 0) __syncthreads();   // (the previous plane's reads done)
+      *reinterpret_cast<uint2*>(tr + (2 * rp) * 20 + 2 * kg) = make_uint2(a0, a1);
+      *reinterpret_cast<uint2*>(tr + (2 * rp + 1) * 20 + 2 * kg) = make_uint2(b0, b1);
+      __syncthreads();
+      *reinterpret_cast<uint4*>(dst + (long long)l * plane_bytes) = *reinterpret_cast<const uint4*>(tr + wr * 20 + 4 * wp);
     }
   }
 }
