@@ -1518,9 +1518,12 @@ int trsv_lower(gpe_ctx* c, Fact& F, const double* R, long long ldr, int P, doubl
 
 // ---------------------------------------------------------------- A^-1 on the int8 cores
 // (gpemu_ozaki.hpp).  Used by the objective's gradient for OZ_MIN_NP <= n_pad <= OZ_MAX_NP:
-// below, the fp64 LAUUM is a few short launches; above, the planes and residues (each
-// N bytes per lower entry) would take more than ~13 GB per context.
-constexpr int OZ_MIN_NP = 2048, OZ_MAX_NP = 32768;
+// below, the fp64 LAUUM is a few short launches.  At the top, n_pad = 65536 (BASELINE
+// configs[3] on one GPU), the K = 65536 sums still fit the int32 accumulators (2^30) and 16
+// moduli still give 53-bit operands, and the planes, residues and T scratch take 77 GB beside
+// the 69 GB of A and B (of the 288 GB).  The posterior's product keeps OZ_POST_MAX_NP: its
+// planes of the whole square L^-1 (N n_pad^2 bytes) would add 69 GB more there.
+constexpr int OZ_MIN_NP = 2048, OZ_MAX_NP = 65536, OZ_POST_MAX_NP = 32768;
 bool oz_use(const gpe_ctx* c) { return c->oz_on && c->n_pad >= OZ_MIN_NP && c->n_pad <= OZ_MAX_NP; }
 
 // the TRTRI levels on the int8 cores: every pair of a level whose blocks have at least
@@ -2636,7 +2639,7 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
   if (precision == 32 && full_var) return fail(c, GPE_ERR_UNSUPPORTED, "precision 32 is for the diagonal variance");
   CHK(ensure_linv(c));
   const bool f32 = precision == 32;
-  const bool ozp = oz_use(c);   // V on the int8 cores (posterior_oz), either precision
+  const bool ozp = oz_use(c) && c->n_pad <= OZ_POST_MAX_NP;   // V on the int8 cores (posterior_oz)
   const int d = c->d, q = c->q, P = q + 1;
   const long long np = c->n_pad;
   const long long CHUNK = full_var ? 16384 : 8192;
