@@ -189,6 +189,7 @@ struct gpe_ctx {
   bool x32_valid = false;
   float* dK32 = nullptr;
   size_t k32_cap = 0;
+  hipEvent_t ev_pipe[2] = {nullptr, nullptr};   // the diagonal posterior's chunk pipeline
   // posterior V = L^-1 K* on the int8 cores (posterior_oz): planes of L^-1's rows and their
   // exponents (formed once per factor and moduli count), each chunk's K* planes, exponents
   // and residues, the tile list
@@ -1870,6 +1871,8 @@ void gpe_destroy(gpe_ctx* c) {
     if (e) hipEventDestroy(e);
   for (auto& e : c->gev) (void)hipEventDestroy(e);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  for (hipEvent_t e : c->ev_pipe)
+    if (e) (void)hipEventDestroy(e);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->ev_host) (void)hipEventDestroy(c->ev_host);
   if (c->stream2) {
@@ -2435,6 +2438,12 @@ static int posterior_oz(gpe_ctx* c, bool f32, const double* Ks, long long mp, do
     c->px_valid = true;
     c->px_nmod = N;
   }
+  const long long pB = (long long)mp2 * np2, rb = (long long)nti * ntj * OZ_T * OZ_T;
+  // (the diagonal posterior queues chunk i + 1 while chunk i runs: a new tile list or larger
+  // buffers wait for it)
+  if (c->pl_nti != nti || c->pl_ntj != ntj || (size_t)N * pB > c->pkp_cap || (size_t)mp2 > c->pke_cap ||
+      (size_t)N * rb > c->pres_cap)
+    HIPCHK(c, hipStreamSynchronize(st));
   if (c->pl_nti != nti || c->pl_ntj != ntj) {
     const std::vector<unsigned> l = oz_list(nti, ntj, false, [&](int ti, int) { return (double)(OZ_T * (ti + 1)); });
     c->pl_nti = c->pl_ntj = 0;
@@ -2444,7 +2453,6 @@ static int posterior_oz(gpe_ctx* c, bool f32, const double* Ks, long long mp, do
     c->pl_nti = nti;
     c->pl_ntj = ntj;
   }
-  const long long pB = (long long)mp2 * np2, rb = (long long)nti * ntj * OZ_T * OZ_T;
   CHK(grow_buf(c, &c->dpkp, &c->pkp_cap, (size_t)N * pB));
   CHK(grow_buf(c, &c->dpke, &c->pke_cap, (size_t)mp2));
   CHK(grow_buf(c, &c->dpres, &c->pres_cap, (size_t)N * rb));
@@ -2697,30 +2705,42 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
   kernel_consts(c->f_kernel, c->f_nu, true, &coff, &cdiag);
   const double s2 = sigma * sigma;
 
-  for (long long s0 = 0; s0 < m; s0 += CHUNK) {
+  // workspace for the largest chunk (the first): K* (np x mp) and V (np x mp), the chunk's
+  // points, two pinned staging slots of points and two of results, two device result slots
+  const long long mp0 = ((std::min<long long>(CHUNK, m) + TILE - 1) / TILE) * TILE;
+  if ((size_t)np * mp0 > c->w_cap) {
+    c->w_cap = 0;
+    CHK(dalloc(c, &c->dW1, (size_t)np * mp0));
+    CHK(dalloc(c, &c->dW2, (size_t)np * mp0));
+    c->w_cap = (size_t)np * mp0;
+  }
+  if ((size_t)mp0 * d > c->xs_cap) {
+    c->xs_cap = 0;
+    CHK(dalloc(c, &c->dXs, (size_t)mp0 * d));
+    CHK(dalloc(c, &c->dXsw, (size_t)mp0 * d));
+    c->xs_cap = (size_t)mp0 * d;
+  }
+  const size_t rs = (size_t)mp0 * P + mp0;   // one result slot: Y (mp x P), then the column norms
+  CHK(ensure_small(c, 2 * rs + 64));
+  // (the full covariance also stages T Kq^-T, mp x kq, at the front: the capacity is set here
+  // once, so the slots never move)
+  CHK(ensure_pinned(c, std::max<size_t>(2 * (size_t)mp0 * d + 2 * rs + d, (size_t)mp0 * kq) + 64));
+  double* pin_in[2] = {c->hpin, c->hpin + (size_t)mp0 * d};
+  double* pin_out[2] = {c->hpin + 2 * (size_t)mp0 * d, c->hpin + 2 * (size_t)mp0 * d + rs};
+  double* pin_dl = c->hpin + 2 * (size_t)mp0 * d + 2 * rs;   // 1 / delta
+  for (int k = 0; k < d; ++k) pin_dl[k] = 1.0 / c->f_delta[k];
+  HIPCHK(c, hipMemcpyAsync(c->dinvdelta, pin_dl, d * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  if (!c->ev_pipe[0])
+    for (hipEvent_t& e : c->ev_pipe) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  // one chunk's device work: its points from the pinned slot pin, K*, Y = K*^T [gamma, G]
+  // into dY, V = L^-1 K* into vdst (fp32 path: into dK32)
+  auto dev_chunk = [&](long long s0, double* pin, double* dY, double* vdst) -> int {
     const long long mc = std::min(CHUNK, m - s0);
     const long long mp = ((mc + TILE - 1) / TILE) * TILE;
     const int mt = (int)(mp / TILE);
-    // workspace: K* (np x mp) and V (np x mp) [+ full var mp x mp]
-    const size_t need = (size_t)np * mp;
-    if (need > c->w_cap) {
-      c->w_cap = 0;
-      CHK(dalloc(c, &c->dW1, need));
-      CHK(dalloc(c, &c->dW2, need));
-      c->w_cap = need;
-    }
-    if ((size_t)mp * d > c->xs_cap) {
-      c->xs_cap = 0;
-      CHK(dalloc(c, &c->dXs, (size_t)mp * d));
-      CHK(dalloc(c, &c->dXsw, (size_t)mp * d));
-      c->xs_cap = (size_t)mp * d;
-    }
-    CHK(ensure_pinned(c, std::max<size_t>((size_t)mp * d, (size_t)mp * P) + 64));
-    std::memset(c->hpin, 0, (size_t)mp * d * sizeof(double));
-    std::memcpy(c->hpin, Xs + s0 * d, (size_t)mc * d * sizeof(double));
-    HIPCHK(c, hipMemcpyAsync(c->dXs, c->hpin, (size_t)mp * d * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    for (int k = 0; k < d; ++k) c->hpin[(size_t)mp * d + k] = 1.0 / c->f_delta[k];
-    HIPCHK(c, hipMemcpyAsync(c->dinvdelta, c->hpin + (size_t)mp * d, d * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    std::memset(pin, 0, (size_t)mp * d * sizeof(double));
+    std::memcpy(pin, Xs + s0 * d, (size_t)mc * d * sizeof(double));
+    HIPCHK(c, hipMemcpyAsync(c->dXs, pin, (size_t)mp * d * sizeof(double), hipMemcpyHostToDevice, c->stream));
     {
       const long long tot = mp * d;
       hipLaunchKernelGGL(k_scale_points, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream,
@@ -2736,9 +2756,6 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
       CHK(launch_pairs(c, a, c->NB * mt));
     }
     // Y = K*^T [gamma, G]  (mp x P)
-    double* dY = c->dR2;   // reuse (np >= ... not guaranteed) -> use dsmall
-    CHK(ensure_small(c, (size_t)mp * P + 64));
-    dY = c->dsmall;
     // skinny transposed over a full matrix: M = K* (np x mp), k tiles = NB, out tiles = mt;
     // 32 columns of [gamma, G] at a time
     for (int c0 = 0; c0 < P; c0 += SK_PMAX) {
@@ -2769,7 +2786,7 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
     }
     // V = L^-1 K*   (np x mp), X lower-triangular -> kend = (ti+1)*128
     if (ozp) {
-      CHK(posterior_oz(c, f32, c->dW1, mp, big ? c->dVall + s0 * np : c->dW2));
+      CHK(posterior_oz(c, f32, c->dW1, mp, vdst));
     } else if (f32) {
       const size_t need32 = 2 * (size_t)np * mp;
       if (need32 > c->k32_cap) {
@@ -2788,7 +2805,6 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
                          c->stream, c->dX32, np, K32, np, V32, np, c->NB, (int)np, 1);
       HIPCHK(c, hipGetLastError());
     } else {
-      double* vdst = big ? c->dVall + s0 * np : c->dW2;
       std::vector<GemmProb> pv = {mkprob(c->tr.B, np, c->dW1, np, vdst, np, c->NB, mt, (int)np,
                                          G_KEND_TI, 1.0, 0.0)};
       pv[0].tile_begin = 0;
@@ -2797,11 +2813,71 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
       Launch L{3, ADHOC_DESC_BASE, 1, c->NB * mt, 0.0};
       CHK(launch_gemm_range(c, L));
     }
+    return GPE_OK;
+  };
+  if (!full_var) {
+    // diagonal variance, pipelined: chunk i's device work (and the copy of its Y and column
+    // norms into pinned slot i % 2) is queued before the host turns chunk i - 1's results
+    // into means and variances, so the GPU does not idle on the host between chunks
+    auto host_chunk = [&](long long s0, const double* out) {
+      const long long mc = std::min(CHUNK, m - s0);
+      const long long mp = ((mc + TILE - 1) / TILE) * TILE;
+      const double* Yh = out;
+      const double* nrm = out + (size_t)mp * P;
+      for (long long s = 0; s < mc; ++s) {
+        const double* hs = Hs + (s0 + s) * q;
+        double mu = Yh[s];
+        for (int i = 0; i < q; ++i) mu += hs[i] * beta[i];
+        mean_out[s0 + s] = mu;
+        double tq = 0.0;   // |T Kq^-T|^2, T = Hs - K*^T G
+        for (int o = 0; o < q; ++o) {
+          double acc = 0.0;
+          for (int i = 0; i < q; ++i) acc += (hs[i] - Yh[s + (long long)(i + 1) * mp]) * Kinv[o * q + i];
+          tq += acc * acc;
+        }
+        var_out[s0 + s] = s2 * (cdiag - nrm[s] + tq);
+      }
+    };
+    int slot = 0;
+    long long prev = -1;
+    for (long long s0 = 0; s0 < m; s0 += CHUNK, slot ^= 1) {
+      const long long mc = std::min(CHUNK, m - s0);
+      const long long mp = ((mc + TILE - 1) / TILE) * TILE;
+      double* dY = c->dsmall + slot * rs;
+      double* dn = dY + (size_t)mp * P;
+      CHK(dev_chunk(s0, pin_in[slot], dY, c->dW2));
+      if (f32 && !ozp)
+        hipLaunchKernelGGL(k_colnorm2_f32, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, c->stream,
+                           c->dK32 + (size_t)np * mp, np, (int)np, (int)mp, dn);
+      else
+        hipLaunchKernelGGL(k_colnorm2, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, c->stream, c->dW2, np,
+                           (int)np, (int)mp, dn);
+      HIPCHK(c, hipGetLastError());
+      HIPCHK(c, hipMemcpyAsync(pin_out[slot], dY, ((size_t)mp * P + mp) * sizeof(double), hipMemcpyDeviceToHost,
+                               c->stream));
+      HIPCHK(c, hipEventRecord(c->ev_pipe[slot], c->stream));
+      if (prev >= 0) {
+        HIPCHK(c, hipEventSynchronize(c->ev_pipe[slot ^ 1]));
+        host_chunk(prev, pin_out[slot ^ 1]);
+      }
+      prev = s0;
+    }
+    HIPCHK(c, hipEventSynchronize(c->ev_pipe[slot ^ 1]));
+    host_chunk(prev, pin_out[slot ^ 1]);
+    return GPE_OK;
+  }
+
+  for (long long s0 = 0; s0 < m; s0 += CHUNK) {
+    const long long mc = std::min(CHUNK, m - s0);
+    const long long mp = ((mc + TILE - 1) / TILE) * TILE;
+    const int mt = (int)(mp / TILE);
+    double* dY = c->dsmall;
+    CHK(dev_chunk(s0, pin_in[0], dY, big ? c->dVall + s0 * np : c->dW2));
     // host pieces: mean, T = Hs - K*^T G
     std::vector<double> Yh((size_t)mp * P);
-    HIPCHK(c, hipMemcpyAsync(c->hpin, dY, (size_t)mp * P * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(pin_out[0], dY, (size_t)mp * P * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    std::memcpy(Yh.data(), c->hpin, Yh.size() * sizeof(double));
+    std::memcpy(Yh.data(), pin_out[0], Yh.size() * sizeof(double));
     std::vector<double> Tt((size_t)mc * q);   // T Kq^-T, row-major mc x q
     for (long long s = 0; s < mc; ++s) {
       const double* hs = Hs + (s0 + s) * q;
@@ -2822,24 +2898,7 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
         for (int o = 0; o < q; ++o) Th[(s0 + s) + (size_t)o * mtot] = Tt[s * q + o];
       continue;
     }
-    if (!full_var) {
-      CHK(ensure_small(c, (size_t)mp * P + mp + 64));
-      double* dn = c->dsmall + (size_t)mp * P;
-      if (f32 && !ozp)
-        hipLaunchKernelGGL(k_colnorm2_f32, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, c->stream,
-                           c->dK32 + (size_t)np * mp, np, (int)np, (int)mp, dn);
-      else
-        hipLaunchKernelGGL(k_colnorm2, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, c->stream, c->dW2, np,
-                           (int)np, (int)mp, dn);
-      HIPCHK(c, hipGetLastError());
-      HIPCHK(c, hipMemcpyAsync(c->hpin, dn, (size_t)mp * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      for (long long s = 0; s < mc; ++s) {
-        double tq = 0.0;
-        for (int o = 0; o < q; ++o) tq += Tt[s * q + o] * Tt[s * q + o];
-        var_out[s0 + s] = s2 * (cdiag - c->hpin[s] + tq);
-      }
-    } else {
+    {
       // C = s2 * (A** - V^T V + Tt Tt^T), all tiles (full symmetric)
       const size_t needc = (size_t)mp * mp;
       if (needc + (size_t)mp * kq > c->w3_cap) {
