@@ -161,6 +161,7 @@ struct gpe_ctx {
   // the objective's A^-1 on the int8 matrix cores (gpemu_ozaki.hpp): GPEMU_OZAKI=0 keeps the
   // fp64 LAUUM; GPEMU_OZAKI_MODULI sets the number of moduli (default 16: 53-bit operands)
   int oz_on = 1, oz_nmod = OZ_MAXMOD;
+  int oz_min_np = 6144;           // OZ_MIN_NP (GPEMU_OZAKI_MIN_NP)
   int oz_np2 = 0, oz_list_len = 0;
   OzConst oz_c{};
   int8_t* dozp = nullptr;         // the N int8 planes of X (lower 256-column panels)
@@ -1524,8 +1525,12 @@ int trsv_lower(gpe_ctx* c, Fact& F, const double* R, long long ldr, int P, doubl
 // moduli still give 53-bit operands, and the planes, residues and T scratch take 77 GB beside
 // the 69 GB of A and B (of the 288 GB).  The posterior's product keeps OZ_POST_MAX_NP: its
 // planes of the whole square L^-1 (N n_pad^2 bytes) would add 69 GB more there.
-constexpr int OZ_MIN_NP = 2048, OZ_MAX_NP = 65536, OZ_POST_MAX_NP = 32768;
-bool oz_use(const gpe_ctx* c) { return c->oz_on && c->n_pad >= OZ_MIN_NP && c->n_pad <= OZ_MAX_NP; }
+// The lower ends are where the int8 path starts paying (`profiles/oz_crossover_r06.log`): the
+// objective's A^-1 from n_pad 6144 (0.31 against 0.13 ms at 2048, 1.25 against 1.30 at 6144,
+// 2.33 against 2.82 at 8192), the posterior's product from 4096 (GPEMU_OZAKI_MIN_NP lowers
+// both, for tests).
+constexpr int OZ_MIN_NP = 6144, OZ_POST_MIN_NP = 4096, OZ_MAX_NP = 65536, OZ_POST_MAX_NP = 32768;
+bool oz_use(const gpe_ctx* c) { return c->oz_on && c->n_pad >= c->oz_min_np && c->n_pad <= OZ_MAX_NP; }
 
 // the TRTRI levels on the int8 cores: every pair of a level whose blocks have at least
 // oz_tri_min rows (GPEMU_OZAKI_TRI_MIN; the levels below stay fp64: their products are a
@@ -1762,6 +1767,7 @@ gpe_ctx* gpe_create(int32_t device) {
     if (const char* et = std::getenv("GPEMU_TINY")) c->tiny = std::atoi(et) != 0;
     if (const char* ed = std::getenv("GPEMU_DEBUG_SKIP_WAIT")) c->dbg_skip_wait = std::atoi(ed);
     if (const char* eo = std::getenv("GPEMU_OZAKI")) c->oz_on = std::atoi(eo) != 0;
+    if (const char* en = std::getenv("GPEMU_OZAKI_MIN_NP")) c->oz_min_np = std::max(512, std::atoi(en));
     if (const char* em = std::getenv("GPEMU_OZAKI_MODULI")) c->oz_nmod = std::max(8, std::min(OZ_MAXMOD, std::atoi(em)));
     if (const char* et = std::getenv("GPEMU_OZAKI_TRI_MIN")) c->oz_tri_min = std::max(512, std::atoi(et));
     if (const char* es = std::getenv("GPEMU_POTRF_SB")) {
@@ -2647,7 +2653,8 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
   if (precision == 32 && full_var) return fail(c, GPE_ERR_UNSUPPORTED, "precision 32 is for the diagonal variance");
   CHK(ensure_linv(c));
   const bool f32 = precision == 32;
-  const bool ozp = oz_use(c) && c->n_pad <= OZ_POST_MAX_NP;   // V on the int8 cores (posterior_oz)
+  const bool ozp = c->oz_on && c->n_pad >= std::min(c->oz_min_np, OZ_POST_MIN_NP) &&
+                   c->n_pad <= OZ_POST_MAX_NP;   // V on the int8 cores (posterior_oz)
   const int d = c->d, q = c->q, P = q + 1;
   const long long np = c->n_pad;
   const long long CHUNK = full_var ? 16384 : 8192;

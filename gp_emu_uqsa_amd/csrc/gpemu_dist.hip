@@ -440,6 +440,7 @@ struct gpe_dist {
   int oz_nmod = OZ_MAXMOD;
   bool oz_now = false;                         // this data's partial on the int8 cores
   long long oz_cap_mb = 16384;                 // at most this many MiB of planes per rank
+  int oz_min_np = 6144;                        // from this n_pad (as gpemu.hip; GPEMU_OZAKI_MIN_NP)
   int oz_tri_min = 8192;                       // P = 1: TRTRI levels of blocks this tall on the
                                                // int8 cores (GPEMU_OZAKI_TRI_MIN, as gpemu.hip)
   int oz_np2 = 0, oz_kp = 0;                   // planes: oz_np2 rows (columns of X_r) x oz_kp k
@@ -1153,7 +1154,7 @@ int ensure_grad(gpe_dist* h) {
   // they fit oz_cap_mb (16 GiB; GPEMU_DIST_OZAKI_MB), so a rank of C4 takes them from P = 8
   const int nlx0 = (NB - 1) / P + 1;
   const double oz_planes = (double)h->oz_nmod * ((np + OZ_T - 1) / OZ_T * OZ_T) * nlx0 * TILE;
-  h->oz_now = h->oz_on && np >= 2048 && (long long)nlx0 * TILE < (1 << 17) &&
+  h->oz_now = h->oz_on && np >= h->oz_min_np && (long long)nlx0 * TILE < (1 << 17) &&
               oz_planes <= (double)h->oz_cap_mb * (1 << 20);
   if (h->oz_now && h->slab_rows < NB && (h->slab_rows & 1)) h->slab_rows = std::max(2, h->slab_rows - 1);
   const long long lds = (long long)h->slab_rows * TILE;
@@ -1652,6 +1653,7 @@ gpe_dist* gpe_dist_create(int32_t device, int32_t nranks, int32_t rank, const ui
   if (const char* e = std::getenv("GPEMU_DIST_FUSE_NEXT")) h->fuse_next = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPEMU_OZAKI")) h->oz_on = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPEMU_DIST_OZAKI_MB")) h->oz_cap_mb = std::max(0ll, std::atoll(e));
+  if (const char* e = std::getenv("GPEMU_OZAKI_MIN_NP")) h->oz_min_np = std::max(512, std::atoi(e));
   if (const char* e = std::getenv("GPEMU_OZAKI_TRI_MIN")) h->oz_tri_min = std::max(512, std::atoi(e));
   if (const char* e = std::getenv("GPEMU_OZAKI_MODULI")) h->oz_nmod = std::max(8, std::min(OZ_MAXMOD, std::atoi(e)));
   if (const char* e = std::getenv("GPEMU_DIST_W")) {   // "4:80,2:40": {width, min remaining}

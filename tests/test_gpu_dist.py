@@ -179,6 +179,8 @@ def _oz_bytes(nb, P, nmod=16):
     ranks): nmod planes of X_r^T (np2 x rank 0's rows) and nmod residue images of the largest
     slab's 256-tiles (slabs of an even number of tile rows)."""
     np_ = nb * 128
+    if np_ < 6144:   # (the int8 partial's default start)
+        return 0
     np2 = -(-np_ // 256) * 256
     kp = ((nb - 1) // P + 1) * 128
     whole = nb * 128 * np_
@@ -245,6 +247,7 @@ def test_loopback_int8_partial_matches_fp64(monkeypatch, P, slab_mb):
     hp = _hp(d)
     if slab_mb:
         monkeypatch.setenv("GPEMU_DIST_SLAB_MB", str(slab_mb))
+    monkeypatch.setenv("GPEMU_OZAKI_MIN_NP", "2048")   # (default start 6144)
     # P = 1: the TRTRI levels of blocks >= 1024 rows on the int8 cores as well (pairs
     # (0, 8, 16) and (0, 16, 24) at 24 tile rows: a ragged second block)
     monkeypatch.setenv("GPEMU_OZAKI_TRI_MIN", "1024")

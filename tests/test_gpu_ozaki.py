@@ -16,6 +16,18 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
+def oz():
+    """A context with the int8 products from n_pad 2048 (their default start is 6144, where
+    they begin to pay; these sizes keep the oracle checks quick)."""
+    mp = pytest.MonkeyPatch()
+    mp.setenv("GPEMU_OZAKI_MIN_NP", "2048")
+    c = native.Context(0)
+    mp.undo()
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
 def fp64():
     mp = pytest.MonkeyPatch()
     mp.setenv("GPEMU_OZAKI", "0")
@@ -39,7 +51,7 @@ CASES = [   # (variant, kernel, fit nugget, r)
 
 @pytest.mark.parametrize("n,d", [(2048, 10), (2200, 5), (3000, 20)])
 @pytest.mark.parametrize("case", CASES, ids=["gp4ml_fit", "mucm_fix", "alt_r", "std_r"])
-def test_ozaki_gradient(ctx, fp64, n, d, case):
+def test_ozaki_gradient(oz, fp64, n, d, case):
     variant, kind, fitn, use_r = case
     X, f, H = orc.synthetic_problem(n, d, seed=n + d)
     r = np.random.RandomState(n).uniform(1e-4, 1e-3, size=n) if use_r else None
@@ -50,9 +62,9 @@ def test_ozaki_gradient(ctx, fp64, n, d, case):
         hp.append(1.1)
     hp = np.array(hp)
     nu_fixed = 5e-3 if not fitn else 0.0
-    ctx.set_data(X, f, H, r)
+    oz.set_data(X, f, H, r)
     fp64.set_data(X, f, H, r)
-    llh, g, s2 = ctx.objective(variant, kind, hp, nu_fixed=nu_fixed)
+    llh, g, s2 = oz.objective(variant, kind, hp, nu_fixed=nu_fixed)
     llh64, g64, s64 = fp64.objective(variant, kind, hp, nu_fixed=nu_fixed)
     assert llh == llh64 and s2 == s64
     err64 = np.max(np.abs(g - g64) / _scale(g64))
@@ -68,6 +80,7 @@ def test_ozaki_fewer_moduli_still_accurate(fp64):
     1e-9 of the fp64 path (the truncated operands' error, not a wrong reconstruction)."""
     mp = pytest.MonkeyPatch()
     mp.setenv("GPEMU_OZAKI_MODULI", "12")
+    mp.setenv("GPEMU_OZAKI_MIN_NP", "2048")
     c = native.Context(0)
     mp.undo()
     try:

@@ -68,6 +68,7 @@ def test_posterior_precision32_diagonal(monkeypatch, oz):
     |L^-1 k*|^2 to cancellation, tolerance 2e-5 * sigma^2."""
     from gp_emu_uqsa_amd import native, synthetic
     monkeypatch.setenv("GPEMU_OZAKI", oz)
+    monkeypatch.setenv("GPEMU_OZAKI_MIN_NP", "2048")   # (the int8 product's default start: 4096)
     ctx = native.Context(0)
     X, f, H = synthetic.problem(2000, 6, seed=3)
     ctx.set_data(X, f, H)
@@ -98,6 +99,7 @@ def test_posterior_int8_matches_fp64(monkeypatch):
     xs = synthetic.design(9000, d, seed=8)
     hs = synthetic.linear_basis(xs)
     out = {}
+    monkeypatch.setenv("GPEMU_OZAKI_MIN_NP", "2048")   # (the int8 product's default start: 4096)
     for oz in ("0", "1"):
         monkeypatch.setenv("GPEMU_OZAKI", oz)
         c = native.Context(0)
