@@ -162,6 +162,7 @@ struct gpe_ctx {
   // fp64 LAUUM; GPEMU_OZAKI_MODULI sets the number of moduli (default 16: 53-bit operands)
   int oz_on = 1, oz_nmod = OZ_MAXMOD;
   int oz_min_np = 6144;           // OZ_MIN_NP (GPEMU_OZAKI_MIN_NP)
+  int chol_solo = 0;              // GPEMU_CHOL_SOLO (A/B)
   int oz_np2 = 0, oz_list_len = 0;
   OzConst oz_c{};
   int8_t* dozp = nullptr;         // the N int8 planes of X (lower 256-column panels)
@@ -387,9 +388,9 @@ int launch_pairs(gpe_ctx* c, const PairArgs& a, int nblocks) {
   return GPE_OK;
 }
 
-int launch_gemm_range(gpe_ctx* c, const Launch& L, hipStream_t st = nullptr) {
+int launch_gemm_range(gpe_ctx* c, const Launch& L, hipStream_t st = nullptr, size_t lds = 0) {
   if (!st) st = c->stream;
-  const size_t lds = G_LDS_LAUNCH_DOUBLES * sizeof(double);
+  if (!lds) lds = G_LDS_LAUNCH_DOUBLES * sizeof(double);
   const GemmProb* pr = c->dprobs + L.first;
   const unsigned* tl = (L.list >= 0) ? c->dtiles + L.list : nullptr;
   if (c->prof) {
@@ -1220,6 +1221,13 @@ int grow_buf(gpe_ctx* c, T** p, size_t* cap, size_t need) {
   return GPE_OK;
 }
 
+// (A/B, GPEMU_CHOL_SOLO=S) the sweep's launches from step S on with more LDS than two
+// workgroups share, so every workgroup has its CU alone: the diagonal factor without a
+// co-resident bulk tile
+size_t chol_lds(const gpe_ctx* c, int t) {
+  return (c->chol_solo > 0 && t >= c->chol_solo) ? (size_t)96 * 1024 : 0;
+}
+
 int potrf(gpe_ctx* c, Fact& F, bool with_aug = false) {
   CHK(build_plan(c, F));
   const Plan& pl = F.plan;
@@ -1237,7 +1245,7 @@ int potrf(gpe_ctx* c, Fact& F, bool with_aug = false) {
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
     for (int t = 0; t < NB; ++t)
-      if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]], c->stream2));
+      if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]], c->stream2, chol_lds(c, t)));
     HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     return GPE_OK;
@@ -1253,7 +1261,7 @@ int potrf(gpe_ctx* c, Fact& F, bool with_aug = false) {
   }
 #endif
   for (int t = 0; t < NB; ++t)
-    if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]]));
+    if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]], nullptr, chol_lds(c, t)));
   return GPE_OK;
 }
 
@@ -1768,6 +1776,7 @@ gpe_ctx* gpe_create(int32_t device) {
     if (const char* ed = std::getenv("GPEMU_DEBUG_SKIP_WAIT")) c->dbg_skip_wait = std::atoi(ed);
     if (const char* eo = std::getenv("GPEMU_OZAKI")) c->oz_on = std::atoi(eo) != 0;
     if (const char* en = std::getenv("GPEMU_OZAKI_MIN_NP")) c->oz_min_np = std::max(512, std::atoi(en));
+    if (const char* es = std::getenv("GPEMU_CHOL_SOLO")) c->chol_solo = std::max(0, std::atoi(es));
     if (const char* em = std::getenv("GPEMU_OZAKI_MODULI")) c->oz_nmod = std::max(8, std::min(OZ_MAXMOD, std::atoi(em)));
     if (const char* et = std::getenv("GPEMU_OZAKI_TRI_MIN")) c->oz_tri_min = std::max(512, std::atoi(et));
     if (const char* es = std::getenv("GPEMU_POTRF_SB")) {
@@ -2847,31 +2856,38 @@ static int posterior_impl(gpe_ctx* c, int64_t m, const double* Xs, const double*
     };
     int slot = 0;
     long long prev = -1;
-    for (long long s0 = 0; s0 < m; s0 += CHUNK, slot ^= 1) {
-      const long long mc = std::min(CHUNK, m - s0);
-      const long long mp = ((mc + TILE - 1) / TILE) * TILE;
-      double* dY = c->dsmall + slot * rs;
-      double* dn = dY + (size_t)mp * P;
-      CHK(dev_chunk(s0, pin_in[slot], dY, c->dW2));
-      if (f32 && !ozp)
-        hipLaunchKernelGGL(k_colnorm2_f32, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, c->stream,
-                           c->dK32 + (size_t)np * mp, np, (int)np, (int)mp, dn);
-      else
-        hipLaunchKernelGGL(k_colnorm2, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, c->stream, c->dW2, np,
-                           (int)np, (int)mp, dn);
-      HIPCHK(c, hipGetLastError());
-      HIPCHK(c, hipMemcpyAsync(pin_out[slot], dY, ((size_t)mp * P + mp) * sizeof(double), hipMemcpyDeviceToHost,
-                               c->stream));
-      HIPCHK(c, hipEventRecord(c->ev_pipe[slot], c->stream));
-      if (prev >= 0) {
-        HIPCHK(c, hipEventSynchronize(c->ev_pipe[slot ^ 1]));
-        host_chunk(prev, pin_out[slot ^ 1]);
+    auto pipeline = [&]() -> int {
+      for (long long s0 = 0; s0 < m; s0 += CHUNK, slot ^= 1) {
+        const long long mc = std::min(CHUNK, m - s0);
+        const long long mp = ((mc + TILE - 1) / TILE) * TILE;
+        double* dY = c->dsmall + slot * rs;
+        double* dn = dY + (size_t)mp * P;
+        CHK(dev_chunk(s0, pin_in[slot], dY, c->dW2));
+        if (f32 && !ozp)
+          hipLaunchKernelGGL(k_colnorm2_f32, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, c->stream,
+                             c->dK32 + (size_t)np * mp, np, (int)np, (int)mp, dn);
+        else
+          hipLaunchKernelGGL(k_colnorm2, dim3((unsigned)((mp + 3) / 4)), dim3(256), 0, c->stream, c->dW2, np,
+                             (int)np, (int)mp, dn);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(pin_out[slot], dY, ((size_t)mp * P + mp) * sizeof(double), hipMemcpyDeviceToHost,
+                                 c->stream));
+        HIPCHK(c, hipEventRecord(c->ev_pipe[slot], c->stream));
+        if (prev >= 0) {
+          HIPCHK(c, hipEventSynchronize(c->ev_pipe[slot ^ 1]));
+          host_chunk(prev, pin_out[slot ^ 1]);
+        }
+        prev = s0;
       }
-      prev = s0;
-    }
-    HIPCHK(c, hipEventSynchronize(c->ev_pipe[slot ^ 1]));
-    host_chunk(prev, pin_out[slot ^ 1]);
-    return GPE_OK;
+      HIPCHK(c, hipEventSynchronize(c->ev_pipe[slot ^ 1]));
+      host_chunk(prev, pin_out[slot ^ 1]);
+      return GPE_OK;
+    };
+    const int rc = pipeline();
+    // (a failed step may leave copies into the pinned slots queued: drained before the
+    // staging buffer can be reused or regrown)
+    if (rc != GPE_OK) (void)hipStreamSynchronize(c->stream);
+    return rc;
   }
 
   for (long long s0 = 0; s0 < m; s0 += CHUNK) {
