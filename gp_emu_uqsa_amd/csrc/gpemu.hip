@@ -162,7 +162,6 @@ struct gpe_ctx {
   // fp64 LAUUM; GPEMU_OZAKI_MODULI sets the number of moduli (default 16: 53-bit operands)
   int oz_on = 1, oz_nmod = OZ_MAXMOD;
   int oz_min_np = 6144;           // OZ_MIN_NP (GPEMU_OZAKI_MIN_NP)
-  int chol_solo = 0;              // GPEMU_CHOL_SOLO (A/B)
   int oz_np2 = 0, oz_list_len = 0;
   OzConst oz_c{};
   int8_t* dozp = nullptr;         // the N int8 planes of X (lower 256-column panels)
@@ -388,9 +387,9 @@ int launch_pairs(gpe_ctx* c, const PairArgs& a, int nblocks) {
   return GPE_OK;
 }
 
-int launch_gemm_range(gpe_ctx* c, const Launch& L, hipStream_t st = nullptr, size_t lds = 0) {
+int launch_gemm_range(gpe_ctx* c, const Launch& L, hipStream_t st = nullptr) {
   if (!st) st = c->stream;
-  if (!lds) lds = G_LDS_LAUNCH_DOUBLES * sizeof(double);
+  const size_t lds = G_LDS_LAUNCH_DOUBLES * sizeof(double);
   const GemmProb* pr = c->dprobs + L.first;
   const unsigned* tl = (L.list >= 0) ? c->dtiles + L.list : nullptr;
   if (c->prof) {
@@ -1221,13 +1220,6 @@ int grow_buf(gpe_ctx* c, T** p, size_t* cap, size_t need) {
   return GPE_OK;
 }
 
-// (A/B, GPEMU_CHOL_SOLO=S) the sweep's launches from step S on with more LDS than two
-// workgroups share, so every workgroup has its CU alone: the diagonal factor without a
-// co-resident bulk tile
-size_t chol_lds(const gpe_ctx* c, int t) {
-  return (c->chol_solo > 0 && t >= c->chol_solo) ? (size_t)96 * 1024 : 0;
-}
-
 int potrf(gpe_ctx* c, Fact& F, bool with_aug = false) {
   CHK(build_plan(c, F));
   const Plan& pl = F.plan;
@@ -1245,7 +1237,7 @@ int potrf(gpe_ctx* c, Fact& F, bool with_aug = false) {
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
     for (int t = 0; t < NB; ++t)
-      if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]], c->stream2, chol_lds(c, t)));
+      if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]], c->stream2));
     HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     return GPE_OK;
@@ -1261,7 +1253,7 @@ int potrf(gpe_ctx* c, Fact& F, bool with_aug = false) {
   }
 #endif
   for (int t = 0; t < NB; ++t)
-    if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]], nullptr, chol_lds(c, t)));
+    if (fidx[t] >= 0) CHK(launch_gemm_range(c, pl.launches[fidx[t]]));
   return GPE_OK;
 }
 
@@ -1776,7 +1768,6 @@ gpe_ctx* gpe_create(int32_t device) {
     if (const char* ed = std::getenv("GPEMU_DEBUG_SKIP_WAIT")) c->dbg_skip_wait = std::atoi(ed);
     if (const char* eo = std::getenv("GPEMU_OZAKI")) c->oz_on = std::atoi(eo) != 0;
     if (const char* en = std::getenv("GPEMU_OZAKI_MIN_NP")) c->oz_min_np = std::max(512, std::atoi(en));
-    if (const char* es = std::getenv("GPEMU_CHOL_SOLO")) c->chol_solo = std::max(0, std::atoi(es));
     if (const char* em = std::getenv("GPEMU_OZAKI_MODULI")) c->oz_nmod = std::max(8, std::min(OZ_MAXMOD, std::atoi(em)));
     if (const char* et = std::getenv("GPEMU_OZAKI_TRI_MIN")) c->oz_tri_min = std::max(512, std::atoi(et));
     if (const char* es = std::getenv("GPEMU_POTRF_SB")) {
