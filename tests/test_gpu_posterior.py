@@ -148,3 +148,28 @@ def test_kernel_gradients_golden(kind):
     Gn = K.grad_nugget_A(X, s2)
     refn = z["grad_nugget"]
     assert np.max(np.abs(Gn - refn)) <= 1e-14 * np.max(np.abs(refn))
+
+
+def test_posterior_int8_full_covariance_two_chunks(monkeypatch):
+    """The full posterior covariance beyond one chunk (m = 16500: two 16384-point chunks whose V
+    = L^-1 K* the int8 product writes into the device-resident V of all points, then the m x m
+    blocks) at n_pad = 4224 (the int8 product's default range), against GPEMU_OZAKI=0."""
+    from gp_emu_uqsa_amd import native, synthetic
+    n, d, m = 4100, 3, 16500
+    X, f, H = synthetic.problem(n, d, seed=21)
+    xs = synthetic.design(m, d, seed=22)
+    hs = synthetic.linear_basis(xs)
+    out = {}
+    for oz in ("0", "1"):
+        monkeypatch.setenv("GPEMU_OZAKI", oz)
+        c = native.Context(0)
+        c.set_data(X, f, H)
+        c.factor(native.KERNEL_STD, np.full(d, 0.5), 1e-3, 1.0, 0.0)
+        beta = c.beta()
+        out[oz] = c.posterior(xs, hs, beta, 0.9, full_var=True)
+        c.close()
+    (m0, v0), (m1, v1) = out["0"], out["1"]
+    assert np.array_equal(m0, m1)
+    err = float(np.max(np.abs(v1 - v0)))
+    del out, v0, v1
+    assert err < 1e-11 * 0.81, err
