@@ -251,8 +251,10 @@ class Context:
         return out
 
     def posterior(self, Xs, Hs, beta, sigma, full_var=True, precision=64):
-        """(mean, var): var is m x m when full_var, else its diagonal.  precision=32
-        runs the L^-1 K* product on fp32 MFMA (diagonal variance only)."""
+        """(mean, var): var is m x m when full_var, else its diagonal.  The L^-1 K* product
+        runs as exact int8 products (4096 <= n_pad <= 32768): of 53-bit operands at precision
+        64, of 24-bit ones at precision=32 (diagonal variance only; fp32 MFMA outside that
+        range or with GPEMU_OZAKI=0)."""
         if precision not in (32, 64):
             raise ValueError("precision must be 32 or 64")
         Xs = _f64(Xs)

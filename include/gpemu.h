@@ -115,7 +115,7 @@ int gpe_beta(gpe_ctx* ctx, double* beta_out);
  * mean_out m; var_out m x m (row-major) when full_var != 0, else its diagonal
  * (m values); any m, in chunks of 16384 points (full: blocks of the m x m result
  * formed on the device and written to the host).  sigma is par.sigma.
- * precision 64: fp64 accuracy; for 2048 <= n_pad <= 32768 the dominant product
+ * precision 64: fp64 accuracy; for 4096 <= n_pad <= 32768 the dominant product
  * L^-1 K* (n^2 m flops) runs as exact int8 products of 53-bit operands (16 moduli).
  * precision 32 (diagonal only; SURVEY 8b/8d, BASELINE config C5): that product from
  * 24-bit operands (8 moduli; GPEMU_OZAKI=0 or n_pad outside that range: fp32 MFMA on

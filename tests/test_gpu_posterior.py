@@ -87,7 +87,7 @@ def test_posterior_precision32_diagonal(monkeypatch, oz):
 
 
 def test_posterior_int8_matches_fp64(monkeypatch):
-    """V = L^-1 K* on the int8 cores (posterior_oz, n_pad >= 2048) against the fp64 k_gemm
+    """V = L^-1 K* on the int8 cores (posterior_oz, started from n_pad 2048 here) against the fp64 k_gemm
     product (GPEMU_OZAKI=0) and the oracle: precision 64 (16 moduli, 53-bit operands) to
     1e-11 sigma^2 in the diagonal and in the full covariance, precision 32 (8 moduli, 24-bit
     operands) to 4e-6 sigma^2, below the fp32 GEMM's own error on these inputs; ragged n (2200: 9 tiles of 256) and chunks (9000 points: a full
