@@ -543,15 +543,26 @@ inline OzConst oz_consts(int nmod, int np2) {
   return k;
 }
 
-// A product's tile list: blocks of OZ_BR tile rows x OZ_BC tile columns (clipped to the lower
+// A product's tile list: blocks of OZ_BR tile rows x OZ_BC tile columns (8 x 4; GPEMU_OZ_BLOCK
+// "RxC" for A/B runs: 4 x 8, 16 x 2 and 8 x 8 measured within 1%, the LAUUM ~0.15 ms slower
+// at 4 x 8, profiles/ozblock_ab_r06*.log) (clipped to the lower
 // triangle when lower), heaviest first, greedily binned by work into 8 XCD bins, interleaved
 // position by position (bin = position % 8, the XCD under round-robin dispatch), bins padded
 // to one length with 0xffffffff; tile rows ti0 .. ti0 + nti - 1.  An XCD's 32 CUs then run one
-// block at a time: its tiles share 4 A panels and 8 B panels (a whole tile row on one XCD
+// block at a time: its tiles share 8 A panels and 4 B panels (a whole tile row on one XCD
 // shared one A panel among 32 different B panels: L2 hit rate ~0.5)
 template <class W>
 std::vector<unsigned> oz_list(int nti, int ntj, bool lower, W work, int ti0 = 0) {
-  constexpr int OZ_BR = 4, OZ_BC = 8;
+  static const std::pair<int, int> blk = [] {   // (A/B: GPEMU_OZ_BLOCK="RxC")
+    int r = 8, c = 4;
+    if (const char* e = std::getenv("GPEMU_OZ_BLOCK")) {
+      const int rr = std::atoi(e);
+      const char* x = std::strchr(e, 'x');
+      if (rr > 0 && x && std::atoi(x + 1) > 0) { r = rr; c = std::atoi(x + 1); }
+    }
+    return std::make_pair(r, c);
+  }();
+  const int OZ_BR = blk.first, OZ_BC = blk.second;
   struct Blk { double w; std::vector<unsigned> t; };
   std::vector<Blk> blks;
   for (int r0 = ti0; r0 < ti0 + nti; r0 += OZ_BR)
