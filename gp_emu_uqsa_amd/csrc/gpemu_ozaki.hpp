@@ -48,6 +48,16 @@ struct OzConst {
 typedef int oz_v4i __attribute__((ext_vector_type(4)));
 typedef int oz_v16i __attribute__((ext_vector_type(16)));
 
+// A row (or column) holding a NaN or an infinity gets the exponent OZ_EX_NAN: its planes are
+// zero and every product entry in its row (column) comes out NaN, as an fp64 GEMM's would
+// (k_oz_il_to_ex: an atomically max-ed OZ_IL_BAD)
+constexpr int OZ_EX_NAN = -(1 << 20), OZ_IL_BAD = 1 << 29;
+// max that keeps a NaN of either side
+__device__ __forceinline__ double oz_pmax(double a, double b) { return (a > b || a != a) ? a : b; }
+__device__ __forceinline__ int oz_ex_of(double mx, int beta) {
+  return !(mx <= 1.7976931348623157e308) ? OZ_EX_NAN : (mx > 0.0 ? (beta - 1) - ilogb(mx) : 0);
+}
+
 // byte offset of column-panel cb in the planes: panel cb holds columns [256 cb, 256 cb + 256),
 // rows [256 cb, np2), column-major with ld np2 - 256 cb
 __host__ __device__ __forceinline__ long long oz_panel_off(int cb, int np2) {
@@ -62,9 +72,9 @@ static __global__ void __launch_bounds__(256) k_oz_colexp(const double* __restri
   if (j >= np2) return;
   double mx = 0.0;
   if (j < np)
-    for (int k = j + lane; k < np; k += 64) mx = fmax(mx, fabs(X[k + (long long)j * ldx]));
-  for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off, 64));
-  if (lane == 0) ex[j] = mx > 0.0 ? (beta - 1) - ilogb(mx) : 0;
+    for (int k = j + lane; k < np; k += 64) mx = oz_pmax(mx, fabs(X[k + (long long)j * ldx]));
+  for (int off = 32; off > 0; off >>= 1) mx = oz_pmax(mx, __shfl_xor(mx, off, 64));
+  if (lane == 0) ex[j] = oz_ex_of(mx, beta);
 }
 
 // X -> the N int8 planes: thread = 8 consecutive rows of one column (a wave reads 4 KB of
@@ -95,7 +105,7 @@ static __global__ void __launch_bounds__(256) k_oz_split(const double* __restric
     }
   }
 #pragma unroll
-  for (int u = 0; u < OZ_SPLIT_ROWS; ++u) xs[u] = rint(ldexp(xs[u], e));   // |.| <= 2^beta, exact integer
+  for (int u = 0; u < OZ_SPLIT_ROWS; ++u) xs[u] = e == OZ_EX_NAN ? 0.0 : rint(ldexp(xs[u], e));   // |.| <= 2^beta
   const long long ld = np2 - r0;
   int8_t* dst = planes + oz_panel_off(cb, np2) + (long long)(j - r0) * ld + (k0 - r0);
   for (int l = 0; l < cst.nmod; ++l) {
@@ -347,7 +357,9 @@ static __global__ void __launch_bounds__(256) k_oz_crt(OzCrt g, OzConst cst) {
     const int gn = gn0 + (r & 3) + 8 * (r >> 2);
     if (gn >= g.cols || (g.lower128 && (gm >> 7) < (gn >> 7))) continue;
     const double v = (shi[r] - rint(shi[r])) + slo[r];   // C' / M, centred
-    g.C[gm - OZ_T * g.ti0 + (long long)gn * g.ldc] = v * ldexp(sc, -(em + g.exc[gn]));
+    const int en = g.exc[gn];
+    g.C[gm - OZ_T * g.ti0 + (long long)gn * g.ldc] =
+        (em == OZ_EX_NAN || en == OZ_EX_NAN) ? __builtin_nan("") : v * ldexp(sc, -(em + en));
   }
 }
 
@@ -372,9 +384,9 @@ static __global__ void __launch_bounds__(256) k_oz_rowexp(const double* __restri
     double mx = 0.0;
     if (r < R)
       for (int k = lane; k < Kv; k += 64)
-        if (oz_keep(mask, r, k)) mx = fmax(mx, fabs(src[k + (long long)r * ld]));
-    for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off, 64));
-    if (lane == 0) ex[r] = mx > 0.0 ? (beta - 1) - ilogb(mx) : 0;
+        if (oz_keep(mask, r, k)) mx = oz_pmax(mx, fabs(src[k + (long long)r * ld]));
+    for (int off = 32; off > 0; off >>= 1) mx = oz_pmax(mx, __shfl_xor(mx, off, 64));
+    if (lane == 0) ex[r] = oz_ex_of(mx, beta);
   } else {
     __shared__ double red[4][64];
     const int rl = threadIdx.x & 63, q = threadIdx.x >> 6, r = blockIdx.x * 64 + rl;
@@ -384,19 +396,20 @@ static __global__ void __launch_bounds__(256) k_oz_rowexp(const double* __restri
 #pragma unroll 8
       for (int u = 0; u < 64; ++u) {
         const int k = k0 + 4 * u + q;
-        if (k < Kv && oz_keep(mask, r, k)) mx = fmax(mx, fabs(src[r + (long long)k * ld]));
+        if (k < Kv && oz_keep(mask, r, k)) mx = oz_pmax(mx, fabs(src[r + (long long)k * ld]));
       }
     red[q][rl] = mx;
     __syncthreads();
     if (q == 0 && r < R) {
-      mx = fmax(fmax(red[0][rl], red[1][rl]), fmax(red[2][rl], red[3][rl]));
-      if (mx > 0.0) atomicMax(ex + r, ilogb(mx) + 2048);
+      mx = oz_pmax(oz_pmax(red[0][rl], red[1][rl]), oz_pmax(red[2][rl], red[3][rl]));
+      if (!(mx <= 1.7976931348623157e308)) atomicMax(ex + r, OZ_IL_BAD);
+      else if (mx > 0.0) atomicMax(ex + r, ilogb(mx) + 2048);
     }
   }
 }
 static __global__ void __launch_bounds__(256) k_oz_il_to_ex(int* __restrict__ ex, int Rp, int beta) {
   const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r < Rp) ex[r] = ex[r] > 0 ? (beta - 1) - (ex[r] - 2048) : 0;
+  if (r < Rp) ex[r] = ex[r] >= OZ_IL_BAD ? OZ_EX_NAN : (ex[r] > 0 ? (beta - 1) - (ex[r] - 2048) : 0);
 }
 
 // x (an integer-valued double, |x| <= 2^53) -> its centred residue mod m as one byte
@@ -445,7 +458,7 @@ static __global__ void __launch_bounds__(256) k_oz_split_rect(const double* __re
       }
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) xs[u] = rint(ldexp(xs[u], e));
+    for (int u = 0; u < 8; ++u) xs[u] = e == OZ_EX_NAN ? 0.0 : rint(ldexp(xs[u], e));
     int8_t* dst = planes + (long long)r * ldp + k0;
     for (int l = 0; l < cst.nmod; ++l) {
       const double m = (double)cst.m[l], im = 1.0 / m;
@@ -485,8 +498,8 @@ static __global__ void __launch_bounds__(256) k_oz_split_rect(const double* __re
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      x0[u] = rint(ldexp(x0[u], e0));
-      x1[u] = rint(ldexp(x1[u], e1));
+      x0[u] = e0 == OZ_EX_NAN ? 0.0 : rint(ldexp(x0[u], e0));
+      x1[u] = e1 == OZ_EX_NAN ? 0.0 : rint(ldexp(x1[u], e1));
     }
     const int wr = (int)threadIdx.x >> 2, wp = (int)threadIdx.x & 3;   // row wr, piece wp of the block
     int8_t* dst = planes + ((long long)blockIdx.x * 64 + wr) * ldp + (long long)blockIdx.y * 64 + 16 * wp;

@@ -124,6 +124,39 @@ def test_posterior_int8_matches_fp64(monkeypatch):
     assert np.max(np.abs(v1[sel] - np.diag(v_ref))) < 1e-8
 
 
+def test_posterior_int8_nan_point(monkeypatch):
+    """A NaN prediction point gives a NaN mean and variance on the int8 product as on the fp64 one
+    (its K* row gets the OZ_EX_NAN exponent: zero planes, NaN out of the CRT), and leaves every
+    other point's variance as it is without it."""
+    from gp_emu_uqsa_amd import native, synthetic
+    n, d, s2 = 2200, 5, 0.9 ** 2
+    X, f, H = synthetic.problem(n, d, seed=5)
+    delta = np.full(d, 0.7)
+    xs = synthetic.design(600, d, seed=8)
+    xs[17, 2] = np.nan
+    hs = synthetic.linear_basis(xs)
+    monkeypatch.setenv("GPEMU_OZAKI_MIN_NP", "2048")
+    out = {}
+    for oz in ("0", "1"):
+        monkeypatch.setenv("GPEMU_OZAKI", oz)
+        c = native.Context(0)
+        c.set_data(X, f, H)
+        c.factor(native.KERNEL_STD, delta, 1e-3, 1.0, 0.0)
+        beta = c.beta()
+        out[oz] = [c.posterior(xs, hs, beta, 0.9, full_var=False, precision=p) for p in (64, 32)]
+        c.close()
+    ok = np.ones(600, bool)
+    ok[17] = False
+    for p in range(2):
+        for oz in ("0", "1"):
+            m, v = out[oz][p]
+            assert np.isnan(m[17]) and np.isnan(v[17]), (oz, p)
+            assert np.all(np.isfinite(m[ok])) and np.all(np.isfinite(v[ok])), (oz, p)
+    (m0, v0), (m1, v1) = out["0"][0], out["1"][0]
+    assert np.max(np.abs(v1[ok] - v0[ok])) < 1e-11 * s2
+    assert np.array_equal(m1[ok], m0[ok])
+
+
 @pytest.mark.parametrize("kind", [orc.STD, orc.ALT])
 def test_kernel_gradients_golden(kind):
     """kernel.grad_delta_A / grad_nugget_A through the kernel objects (gpe_kernel_grad)
