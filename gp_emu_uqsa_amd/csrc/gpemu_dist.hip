@@ -1656,6 +1656,10 @@ gpe_dist* gpe_dist_create(int32_t device, int32_t nranks, int32_t rank, const ui
   if (const char* e = std::getenv("GPEMU_OZAKI_MIN_NP")) h->oz_min_np = std::max(512, std::atoi(e));
   if (const char* e = std::getenv("GPEMU_OZAKI_TRI_MIN")) h->oz_tri_min = std::max(512, std::atoi(e));
   if (const char* e = std::getenv("GPEMU_OZAKI_MODULI")) h->oz_nmod = std::max(8, std::min(OZ_MAXMOD, std::atoi(e)));
+  // one rank: 8 wide while 64 tile columns remain (n = 16384, value 29.95-30.43 -> 29.49-29.60 ms,
+  // gradient 66.1 -> 65.8-65.9; n = 65536 unchanged); with more ranks 8:160 stays (two loopback
+  // ranks 44.6-44.8 against 47.6-47.9 ms for 8:64; profiles/dist_w_r06*.log)
+  if (nranks == 1) h->groups = {{8, 64}, {4, 0}};
   if (const char* e = std::getenv("GPEMU_DIST_W")) {   // "4:80,2:40": {width, min remaining}
     h->groups.clear();
     std::string spec(e);
